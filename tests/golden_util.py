@@ -1,0 +1,43 @@
+"""Helpers to load the golden fixtures and regenerate their seeded inputs."""
+import json
+import os
+
+import numpy as np
+
+from oracle.seeding import synth_batch, synth_params
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+SEGMENT_FIXTURES = ["segment20_n2_128.npz", "segment3_n2_64x96.npz"]
+
+
+class SegmentFixture:
+    def __init__(self, name):
+        z = np.load(os.path.join(GOLDEN, name))
+        self.z = z
+        self.meta = json.loads(str(z["meta"]))
+        m = self.meta
+        self.cin, self.n, self.h, self.w = m["cin"], m["n"], m["h"], m["w"]
+        self.shapes = [(k, tuple(s)) for k, s in m["shapes"]]
+        self.params = synth_params(self.shapes, m["param_seed"])
+        self.x, self.mask = synth_batch(self.n, self.cin, self.h, self.w, m["batch_seed"])
+        self.param_names = m["param_names"]
+        self.grad_none = set(m["grad_none"])
+        self.buffer_keys = m["buffer_keys"]
+        sizes = [int(np.prod(dict(self.shapes)[k])) for k in self.param_names]
+        self.offsets = np.concatenate([[0], np.cumsum(sizes)])
+
+    def grad(self, key, which="grad64"):
+        i = self.param_names.index(key)
+        shape = dict(self.shapes)[key]
+        return self.z[which][self.offsets[i]:self.offsets[i + 1]].reshape(shape)
+
+    def buffers64(self):
+        out = {}
+        off = 0
+        flat = self.z["bufs64"]
+        for k in self.buffer_keys:
+            n = int(np.prod(dict(self.shapes)[k])) if dict(self.shapes)[k] else 1
+            out[k] = flat[off:off + n].reshape(dict(self.shapes)[k])
+            off += n
+        return out
