@@ -1,0 +1,224 @@
+"""Headline benchmark: train images/s of the reference model (Segment(20) = RGB + 17
+keypoint heatmaps, BCE + Adam; train_instance.py:294-382) on synthetic COCO-person
+1024x1024 batches, bs 2 per GPU (BASELINE.json configs[1]; configs[2] when launched on
+8 GPUs is the same per-replica work). One process per GPU (torchrun), image-batch data
+parallel with an RCCL gradient all-reduce.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+
+Prints ONE JSON line (rank 0) with the driver's contract fields plus:
+  roofline     — the dominant kernel (largest share of step time, picked by a per-op
+                 timing pass), timed live in the timed region with HIP events around it;
+  cpu_baseline — the oracle's CPU restatement (fp32 torch eager) of the same train step,
+                 timed on this host's cores (rank 0, N=1 only).
+"""
+import argparse
+import json
+import os
+import time
+
+import torch
+import torch.distributed as dist
+
+PEAK_F32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix 157.3 TF (spec)
+PEAK_HBM_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=2, help="images per GPU")
+    ap.add_argument("--size", type=int, default=1024)
+    ap.add_argument("--cin", type=int, default=20, choices=(3, 20))
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--profile-ops", default="", help="write per-op timing table to this path")
+    return ap.parse_args()
+
+
+def setup_dist():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, local
+
+
+def op_timing(trainer, reps=3):
+    """Time every recorded op alone (HIP events on the launch stream)."""
+    from instancesegmentation_amd import _lib as L
+    stream = torch.cuda.current_stream()
+    rows = []
+    for phase, ol in (("fwd", trainer.plan.fwd), ("bwd", trainer.plan.bwd)):
+        for i, r in enumerate(ol.recs):
+            sub = ol.slice(i, i + 1)
+            sub.run(trainer.table, L.stream_ptr())
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(reps):
+                sub.run(trainer.table, L.stream_ptr())
+            e1.record(stream)
+            e1.synchronize()
+            rows.append(dict(phase=phase, idx=i, label=r.label, kind=r.kind,
+                             ms=e0.elapsed_time(e1) / reps, flops=r.flops, nbytes=r.nbytes))
+    # leave the trainer's arenas consistent: rerun a full fwd/bwd afterwards
+    return rows
+
+
+def roofline_of(rec, ms):
+    ai = rec.flops / rec.nbytes if rec.nbytes else 0.0
+    ridge = PEAK_F32_MFMA_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)
+    if rec.flops and ai >= ridge:
+        ach = rec.flops / (ms * 1e-3) / 1e12
+        return {"bound": "mfma", "achieved": round(ach, 3), "peak": PEAK_F32_MFMA_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(ach / PEAK_F32_MFMA_TFLOPS, 4), "traffic": None}
+    ach = rec.nbytes / (ms * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": None}
+
+
+def cpu_baseline(args):
+    """Oracle (torch eager fp32 CPU) train step on the same config: bounded sample."""
+    import numpy as np
+    from oracle import segment_oracle
+    from oracle.seeding import synth_params
+    from instancesegmentation_amd.model.segment import Segment
+    threads = len(os.sched_getaffinity(0))
+    env_t = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if env_t:
+        threads = min(threads, env_t)
+    torch.set_num_threads(threads)
+    m = Segment(args.cin)
+    shapes = [(k, tuple(v.shape)) for k, v in m.state_dict().items()]
+    params = synth_params(shapes, 1)
+    from instancesegmentation_amd.data import synthetic_batch
+    img, hm, mask = synthetic_batch(args.batch, args.size, args.size, seed=3,
+                                    with_heatmaps=args.cin == 20)
+    x = np.concatenate([img, hm], 1) if hm is not None else img
+    P = {k: torch.as_tensor(v).float() if np.issubdtype(np.asarray(v).dtype, np.floating)
+         else torch.as_tensor(v) for k, v in params.items()}
+    steps, t_total = 0, 0.0
+    segment_oracle.train_step(P, x, mask, torch.float32)  # warm-up
+    while t_total < args.cpu_seconds or steps < 2:
+        t0 = time.perf_counter()
+        segment_oracle.train_step(P, x, mask, torch.float32)
+        t_total += time.perf_counter() - t0
+        steps += 1
+    return {"value": round(steps * args.batch / t_total, 3), "unit": "images/s",
+            "cores": threads, "kind": "port",
+            "sample": f"{steps} fp32 train steps (fwd+bwd) of Segment({args.cin}) at "
+                      f"bs{args.batch} {args.size}x{args.size} on {threads} host threads"}
+
+
+def main():
+    args = parse()
+    world, rank, local = setup_dist()
+    dev = torch.device("cuda", local)
+    from instancesegmentation_amd import _lib as L
+    from instancesegmentation_amd.data import device_batch
+    from instancesegmentation_amd.model.segment import Segment
+    from instancesegmentation_amd.train import Trainer
+
+    torch.manual_seed(1234)
+    model = Segment(args.cin)
+    xs, mask = device_batch(args.batch, args.size, args.size, dev, seed=100 + rank, cin=args.cin)
+    in_shapes = [tuple(x.shape) for x in xs]
+    trainer = Trainer(model, args.batch, in_shapes, device=dev)
+    trainer.step(xs, mask)
+    torch.cuda.synchronize()
+
+    # ---- dominant op (per-op timing pass, untimed) ----------------------------------
+    dom = None
+    if not args.no_roofline:
+        rows = op_timing(trainer)
+        if args.profile_ops and rank == 0:
+            with open(args.profile_ops, "w") as f:
+                tot = sum(r["ms"] for r in rows)
+                for r in sorted(rows, key=lambda r: -r["ms"]):
+                    f.write(f"{r['phase']} {r['idx']:4d} {r['ms']*1e3:9.1f}us "
+                            f"{100*r['ms']/tot:5.1f}% {r['label']} kind={r['kind']} "
+                            f"flops={r['flops']} bytes={r['nbytes']}\n")
+        best = max(rows, key=lambda r: r["ms"])
+        dom = (best["phase"], best["idx"])
+    for _ in range(args.warmup):
+        trainer.step()
+    torch.cuda.synchronize()
+
+    # split the dominant op's list so it can be bracketed by events inside the timed loop
+    ev_pairs = []
+    if dom is not None:
+        phase, idx = dom
+        ol = trainer.plan.fwd if phase == "fwd" else trainer.plan.bwd
+        pre, mid, post = ol.slice(0, idx), ol.slice(idx, idx + 1), ol.slice(idx + 1, len(ol.recs))
+        dom_rec = ol.recs[idx]
+        stream = torch.cuda.current_stream()
+
+        def timed_list(table, st, _pre=pre, _mid=mid, _post=post):
+            _pre.run(table, st)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            _mid.run(table, st)
+            e1.record(stream)
+            ev_pairs.append((e0, e1))
+            _post.run(table, st)
+
+        class _Wrap:
+            def __init__(self, f):
+                self.run = f
+                self.recs = ol.recs
+        if phase == "fwd":
+            trainer.plan.fwd = _Wrap(timed_list)
+        else:
+            trainer.plan.bwd = _Wrap(timed_list)
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        trainer.step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    loss = trainer.loss()
+
+    roof = None
+    if ev_pairs:
+        ms = sum(a.elapsed_time(b) for a, b in ev_pairs) / len(ev_pairs)
+        roof = roofline_of(dom_rec, ms)
+        roof["kernel"] = f"{dom[0]}:{dom_rec.label}"
+        roof["avg_ms"] = round(ms, 4)
+
+    value = world * args.batch * args.steps / elapsed
+    out = {
+        "metric": "train images/sec, COCO-person 1024x1024 synthetic (Segment(20) RGB+17 "
+                  "heatmaps, BCE+Adam)",
+        "value": round(value, 3), "unit": "images/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (seeded image/heatmaps/ellipse masks resident in HBM)",
+        "config": {"workload": f"train_instance.py step, Segment({args.cin}), bs{args.batch}/GPU, "
+                               f"{args.size}x{args.size}", "global_batch": world * args.batch,
+                   "image_size": args.size, "parallelism": f"dp{world}"},
+        "roofline": roof, "loss": round(loss, 6),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

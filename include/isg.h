@@ -1,0 +1,271 @@
+/*
+ * isg.h — C-ABI of libisg.so, the MI355X (gfx950) kernels behind the
+ * instance-segmentation hot path.
+ *
+ * The reference (YanMiaoW/instanceSegmentation) is pure Python with no FFI; every
+ * entry point below replaces the torch eager kernels that one reference call site
+ * runs (file:line into /root/reference). The Python host
+ * (instancesegmentation_amd/_lib.py, ctypes) binds exactly these symbols; see
+ * INTEGRATION.md for the binding a maintainer adds on the reference side.
+ *
+ * Conventions:
+ *   - all tensors are fp32 NCHW device pointers owned by the caller (torch's caching
+ *     allocator); the library never allocates, frees or synchronises;
+ *   - "virtual" inputs (isg_vtensor) are raw conv outputs plus a per-channel
+ *     transform applied on load (BatchNorm fwd + activation, or BatchNorm bwd);
+ *     channel segments let a consumer read a concat without materialising it;
+ *   - every call enqueues on the caller's hipStream_t and returns 0, or a negative
+ *     status with a thread-local message in isg_last_error();
+ *   - functions are stateless and re-entrant (backward runs on torch's autograd
+ *     worker thread).
+ */
+#ifndef ISG_H
+#define ISG_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* isg_stream_t; /* == hipStream_t */
+
+#define ISG_OK 0
+#define ISG_ERR_INVALID -1
+#define ISG_ERR_UNSUPPORTED -2
+#define ISG_ERR_HIP -3
+
+#define ISG_MAX_SEGS 3
+#define ISG_MAX_CH 512
+#define ISG_LIST_CHUNK 32
+
+enum { ISG_ACT_NONE = 0, ISG_ACT_RELU = 1, ISG_ACT_PRELU = 2 };
+enum { ISG_XF_PLAIN = 0, ISG_XF_BN_FWD = 1, ISG_XF_BN_BWD = 2 };
+enum { ISG_SINK_STORE = 0, ISG_SINK_ACCUM = 1, ISG_SINK_ACTBWD = 2, ISG_SINK_NONE = 3 };
+
+/* One BatchNorm2d layer (segment.py:41 `nn.BatchNorm2d(c2)`; eps 1e-5, momentum 0.1).
+ * stats layout: [sum(C) | sumsq(C) | gsum(C) | gysum(C)] in double; sum/sumsq are of
+ * the raw (pre-BN, bias included) conv output over N*H*W, gsum/gysum of the gradient
+ * w.r.t. the BN output g and of g*y. train=0 uses the running statistics. */
+typedef struct {
+    const float* gamma;
+    const float* beta;
+    const float* running_mean;
+    const float* running_var;
+    double* stats;
+    int32_t C;
+    int32_t train;
+    float count; /* N*H*W */
+    float eps;
+} isg_bn;
+
+/* A channel segment of a virtual tensor.
+ *   PLAIN : v = p
+ *   BN_FWD: v = act((p - mean) * gamma*rstd + beta)            (Conv.forward, segment.py:44-45)
+ *   BN_BWD: v = dL/d(conv output) rebuilt from g (= dL/d BN-output) and the forward
+ *           raw y: A*g + B*(y - mean) + C                       (BatchNorm2d backward) */
+typedef struct {
+    const float* p;
+    const float* y;        /* BN_BWD only */
+    int64_t n_stride;      /* elements between images of p */
+    int64_t y_n_stride;
+    int32_t C;
+    int32_t xform;
+    int32_t act;           /* BN_FWD only */
+    int32_t pad_;
+    const float* slope;    /* PReLU weight [C] (segment.py:24 nn.PReLU(planes)) */
+    isg_bn bn;
+} isg_vseg;
+
+typedef struct {
+    isg_vseg s[ISG_MAX_SEGS];
+    int32_t nseg;
+    int32_t N, H, W;       /* C = sum of segment channels */
+} isg_vtensor;
+
+/* Where a kernel writes channels [c0, c0+C) of its result.
+ *   STORE : p = v + bias; optional BN sum/sumsq into stats   (forward conv outputs)
+ *   ACCUM : p += v                                            (gradient of a consumed tensor)
+ *   ACTBWD: v is dL/dz for z = act(BN(y)); writes g = v*act'(BN(y)) into p and
+ *           accumulates bn.stats gsum/gysum and the PReLU slope gradient. */
+typedef struct {
+    float* p;
+    int64_t n_stride;
+    int32_t c0, C;
+    int32_t mode;
+    int32_t act;
+    const float* bias;
+    double* stats;         /* STORE: 2*C doubles (sum, sumsq) or NULL */
+    const float* y;        /* ACTBWD */
+    int64_t y_n_stride;
+    const float* slope;    /* ACTBWD + PRELU */
+    double* slope_grad;    /* ACTBWD + PRELU, C doubles */
+    isg_bn bn;             /* ACTBWD; bn.stats==NULL means "no BN" (identity) */
+} isg_sink;
+
+typedef struct {
+    isg_sink s[ISG_MAX_SEGS];
+    int32_t nsink;
+} isg_sinks;
+
+typedef struct {
+    int32_t N, Ci, H, W;         /* conv input  */
+    int32_t Co, OH, OW;          /* conv output */
+    int32_t KH, KW, SH, SW, PH, PW, DH, DW;
+    int32_t groups;              /* 1 (dense) or Ci == Co (depthwise) */
+} isg_conv_geom;
+
+/* Residual-block tail: out = act(sum_i term_i), term_i = vtensor channel-aligned
+ * with the output, optionally nearest-upsampled x2 (segment.py:76-77, 107-109,
+ * 147-148, 202-207, 255-259, 331-333). */
+typedef struct {
+    isg_vseg term[3];
+    int32_t up[3];
+    int32_t nterm;
+    int32_t act;
+    const float* slope;
+    float* out;
+    int64_t out_n_stride;
+    int32_t N, C, H, W;
+} isg_tail;
+
+typedef struct {
+    isg_tail f;
+    const float* dout;        /* dL/d out */
+    int64_t dout_n_stride;
+    float* g;                 /* dL/d(sum) written here when non-NULL */
+    int64_t g_n_stride;
+    float* dterm[3];          /* PLAIN terms: gradient destination (ACCUM or store) */
+    int64_t dterm_n_stride[3];
+    int32_t dterm_accum[3];
+    double* slope_grad;
+} isg_tail_grad;
+
+/* ---- forward / backward building blocks -------------------------------- */
+
+/* Dense or depthwise conv forward: y = conv(x) (+bias, BN stats) into `out` sinks.
+ * Replaces nn.Conv2d.forward inside Conv (segment.py:39-45) and the bare convs at
+ * segment.py:91-92, 323, 343, 437. Dense convs run as implicit GEMM on
+ * v_mfma_f32_16x16x4_f32; depthwise on VALU. */
+int32_t isg_conv_fwd(const isg_conv_geom* g, const isg_vtensor* x, const float* w,
+                     const isg_sinks* out, isg_stream_t stream);
+
+/* Input gradient of a conv: dx = conv^T(dy, w) into per-segment sinks. */
+int32_t isg_conv_dgrad(const isg_conv_geom* g, const isg_vtensor* dy, const float* w,
+                       const isg_sinks* dx, isg_stream_t stream);
+
+/* Weight/bias gradient: dw += sum dy (x) im2col(x); dbias += sum dy (either may be
+ * NULL). dw and dbias must be zeroed by the caller before the first contribution. */
+int32_t isg_conv_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x,
+                       float* dw, float* dbias, isg_stream_t stream);
+
+/* ConvTranspose2d forward (segment.py:305-306, 435-436) with kernel = 2*stride,
+ * weight [Ci][Co][K][K], as a sub-pixel direct kernel. geom describes the transposed
+ * conv: input (N,Ci,H,W) -> output (N,Co,OH,OW), KH=KW=K, SH=SW=s, PH=PW=p. */
+int32_t isg_convT_fwd(const isg_conv_geom* g, const isg_vtensor* x, const float* w,
+                      const isg_sinks* out, isg_stream_t stream);
+
+/* Max-pool k x k stride k (segment.py:29, 145) of a virtual tensor into a slice. */
+int32_t isg_maxpool_fwd(const isg_vtensor* x, int32_t k, float* out, int64_t out_n_stride,
+                        isg_stream_t stream);
+/* Route dL/d out to the arg-max of each window (first max wins, torch CPU semantics). */
+int32_t isg_maxpool_bwd(const isg_vtensor* x, int32_t k, const float* dout,
+                        int64_t dout_n_stride, const isg_sinks* dx, isg_stream_t stream);
+
+int32_t isg_tail_fwd(const isg_tail* t, isg_stream_t stream);
+int32_t isg_tail_bwd(const isg_tail_grad* t, isg_stream_t stream);
+
+/* BatchNorm running-stat update for `nitems` layers; `items` is a HOST array (copied
+ * into kernel arguments in chunks of ISG_LIST_CHUNK) (torch BatchNorm2d train semantics):
+ * rm = (1-m) rm + m mean; rv = (1-m) rv + m var*M/(M-1); nbt += 1. */
+typedef struct {
+    const double* stats;
+    float* running_mean;
+    float* running_var;
+    int64_t* num_batches_tracked;
+    int32_t C;
+    float count;
+    float momentum;
+    int32_t pad_;
+} isg_bn_update;
+int32_t isg_bn_update_running(const isg_bn_update* items, int32_t nitems, isg_stream_t stream);
+
+/* Parameter-gradient finalisation (HOST item array, like isg_bn_update_running):
+ *   dgamma = rstd*(gysum - mean*gsum), dbeta = gsum,
+ *   dbias(conv before BN) = sum of rebuilt dy, dslope = double accumulator -> float. */
+typedef struct {
+    const double* stats;       /* BN stats (4*C) or NULL */
+    const float* gamma;
+    const float* running_mean; /* eval-mode backward */
+    const float* running_var;
+    float* dgamma;
+    float* dbeta;
+    float* dconv_bias;         /* may be NULL */
+    const double* slope_acc;   /* may be NULL (then stats describe a BN) */
+    float* dslope;
+    int32_t C;
+    int32_t train;
+    float count;
+    float eps;
+} isg_grad_final;
+int32_t isg_grad_finalize(const isg_grad_final* items, int32_t nitems, isg_stream_t stream);
+
+/* sigmoid + nn.BCELoss(mean) forward and backward in one pass (segment.py:534,
+ * train_instance.py:299,378-379), torch clamp semantics: log clamped at -100,
+ * dL/dp = (p-y)/max(p(1-p),1e-12)/n, dL/dlogit = dL/dp * p(1-p).
+ * loss_acc: one double (sum); dlogits may be NULL. */
+int32_t isg_bce_sigmoid(const float* logits, const float* target, int64_t n, double* loss_acc,
+                        float* dlogits, float grad_scale, isg_stream_t stream);
+int32_t isg_sigmoid_fwd(const float* x, float* y, int64_t n, isg_stream_t stream);
+int32_t isg_sigmoid_bwd(const float* y, const float* dy, float* dx, int64_t n,
+                        isg_stream_t stream);
+
+/* torch.optim.Adam (defaults lr 1e-3, betas (0.9,0.999), eps 1e-8; train_instance.py:297)
+ * over a flat fp32 buffer. `live` (uint8 per element, may be NULL) masks parameters
+ * whose grad is None (they are skipped, as torch does). step is 1-based. */
+int32_t isg_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                 const uint8_t* live, int64_t n, int32_t step, float lr, float beta1,
+                 float beta2, float eps, float weight_decay, isg_stream_t stream);
+
+int32_t isg_fill_f64(double* p, int64_t n, double v, isg_stream_t stream);
+
+/* ---- infer post-process (build-defined; infer.py:32-36 is a stub) -------- */
+
+/* A13: paste K crop probability maps [K,S,S] back onto an HxW canvas through their
+ * crop windows boxes[K][4] = (x0,y0,x1,y1), bilinear, uint8 by truncation of p*255
+ * (train_instance.py:398-399). Contract: oracle/maskops_oracle.py (bit-exact). */
+int32_t isg_mask_paste(const float* prob, int32_t K, int32_t S, const int32_t* boxes,
+                       int32_t H, int32_t W, uint8_t* out, isg_stream_t stream);
+
+/* A14: per-mask count/sum/score and greedy mask-NMS (K <= 64). keep[K] receives the
+ * kept indices in keep order, *nkeep their number (both device memory).
+ * work: isg_mask_nms_workspace(K,H,W) bytes, caller-owned. */
+int64_t isg_mask_nms_workspace(int32_t K, int32_t H, int32_t W);
+int32_t isg_mask_nms(const uint8_t* masks, int32_t K, int32_t H, int32_t W, float iou_thr,
+                     void* work, float* scores_out, int32_t* keep, int32_t* nkeep,
+                     isg_stream_t stream);
+
+/* ---- plan executor ------------------------------------------------------ */
+
+/* A recorded op list (built once per input shape by the Python planner) replayed
+ * with a table of base pointers: pointer = table[slot] + byte offset. */
+typedef struct {
+    int32_t slot;
+    int32_t pad_;
+    int64_t offset;
+} isg_ref;
+
+int32_t isg_exec(const void* ops, int32_t nops, void* const* table, isg_stream_t stream);
+
+/* sizeof() of the ABI structs and executor records (0 vtensor, 1 sinks, 2 conv record,
+ * 3 wgrad record, 4 pool record, 5 tail, 6 tail_grad, 7 bn_update, 8 grad_final,
+ * 9 bce record, 10 conv_geom, 11 bn, 12 vseg, 13 sink) so bindings can verify layouts. */
+int32_t isg_record_size(int32_t which);
+
+const char* isg_last_error(void);
+int32_t isg_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

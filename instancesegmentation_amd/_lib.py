@@ -1,0 +1,181 @@
+"""ctypes binding of libisg.so (include/isg.h) — the only way Python reaches the kernels.
+
+The library is built in-tree by `instancesegmentation_amd.build_lib` (hipcc,
+gfx950). There is no fallback: if the .so is missing or fails to load, every op
+raises. torch must be imported first so libisg.so binds to the HIP runtime torch
+already loaded (both carry SONAME libamdhip64.so.7).
+"""
+import ctypes
+import os
+from ctypes import POINTER, Structure, c_char_p, c_double, c_float, c_int32, c_int64, c_void_p
+
+import torch  # noqa: F401  (load torch's HIP runtime before libisg)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libisg.so")
+
+ACT = {"none": 0, "relu": 1, "prelu": 2}
+XF_PLAIN, XF_BN_FWD, XF_BN_BWD = 0, 1, 2
+SINK_STORE, SINK_ACCUM, SINK_ACTBWD, SINK_NONE = 0, 1, 2, 3
+MAX_SEGS = 3
+LIST_CHUNK = 32
+
+
+class Bn(Structure):
+    _fields_ = [("gamma", c_void_p), ("beta", c_void_p), ("running_mean", c_void_p),
+                ("running_var", c_void_p), ("stats", c_void_p), ("C", c_int32),
+                ("train", c_int32), ("count", c_float), ("eps", c_float)]
+
+
+class VSeg(Structure):
+    _fields_ = [("p", c_void_p), ("y", c_void_p), ("n_stride", c_int64),
+                ("y_n_stride", c_int64), ("C", c_int32), ("xform", c_int32), ("act", c_int32),
+                ("pad_", c_int32), ("slope", c_void_p), ("bn", Bn)]
+
+
+class VTensor(Structure):
+    _fields_ = [("s", VSeg * MAX_SEGS), ("nseg", c_int32), ("N", c_int32), ("H", c_int32),
+                ("W", c_int32)]
+
+
+class Sink(Structure):
+    _fields_ = [("p", c_void_p), ("n_stride", c_int64), ("c0", c_int32), ("C", c_int32),
+                ("mode", c_int32), ("act", c_int32), ("bias", c_void_p), ("stats", c_void_p),
+                ("y", c_void_p), ("y_n_stride", c_int64), ("slope", c_void_p),
+                ("slope_grad", c_void_p), ("bn", Bn)]
+
+
+class Sinks(Structure):
+    _fields_ = [("s", Sink * MAX_SEGS), ("nsink", c_int32)]
+
+
+class Geom(Structure):
+    _fields_ = [(n, c_int32) for n in ("N", "Ci", "H", "W", "Co", "OH", "OW", "KH", "KW", "SH",
+                                       "SW", "PH", "PW", "DH", "DW", "groups")]
+
+
+class Tail(Structure):
+    _fields_ = [("term", VSeg * 3), ("up", c_int32 * 3), ("nterm", c_int32), ("act", c_int32),
+                ("slope", c_void_p), ("out", c_void_p), ("out_n_stride", c_int64),
+                ("N", c_int32), ("C", c_int32), ("H", c_int32), ("W", c_int32)]
+
+
+class TailGrad(Structure):
+    _fields_ = [("f", Tail), ("dout", c_void_p), ("dout_n_stride", c_int64), ("g", c_void_p),
+                ("g_n_stride", c_int64), ("dterm", c_void_p * 3),
+                ("dterm_n_stride", c_int64 * 3), ("dterm_accum", c_int32 * 3),
+                ("slope_grad", c_void_p)]
+
+
+class BnUpdate(Structure):
+    _fields_ = [("stats", c_void_p), ("running_mean", c_void_p), ("running_var", c_void_p),
+                ("num_batches_tracked", c_void_p), ("C", c_int32), ("count", c_float),
+                ("momentum", c_float), ("pad_", c_int32)]
+
+
+class GradFinal(Structure):
+    _fields_ = [("stats", c_void_p), ("gamma", c_void_p), ("running_mean", c_void_p),
+                ("running_var", c_void_p), ("dgamma", c_void_p), ("dbeta", c_void_p),
+                ("dconv_bias", c_void_p), ("slope_acc", c_void_p), ("dslope", c_void_p),
+                ("C", c_int32), ("train", c_int32), ("count", c_float), ("eps", c_float)]
+
+
+# executor records (api.cpp)
+class ConvRec(Structure):
+    _fields_ = [("g", Geom), ("a", VTensor), ("w", c_void_p), ("out", Sinks)]
+
+
+class WgradRec(Structure):
+    _fields_ = [("g", Geom), ("dy", VTensor), ("x", VTensor), ("dw", c_void_p), ("dbias", c_void_p)]
+
+
+class PoolRec(Structure):
+    _fields_ = [("x", VTensor), ("k", c_int32), ("pad_", c_int32), ("out", c_void_p),
+                ("out_ns", c_int64), ("dout", c_void_p), ("dout_ns", c_int64), ("dx", Sinks)]
+
+
+class ListRec(Structure):
+    _fields_ = [("n", c_int32), ("pad_", c_int32)]
+
+
+class BceRec(Structure):
+    _fields_ = [("logits", c_void_p), ("target", c_void_p), ("n", c_int64), ("loss", c_void_p),
+                ("dlogits", c_void_p), ("grad_scale", c_float), ("pad_", c_int32)]
+
+
+class MemsetRec(Structure):
+    _fields_ = [("p", c_void_p), ("bytes", c_int64)]
+
+
+OP_CONV_FWD, OP_CONV_DGRAD, OP_CONV_WGRAD, OP_CONVT_FWD = 1, 2, 3, 4
+OP_MAXPOOL_FWD, OP_MAXPOOL_BWD, OP_TAIL_FWD, OP_TAIL_BWD = 5, 6, 7, 8
+OP_BN_UPDATE, OP_GRAD_FINAL, OP_BCE, OP_MEMSET = 9, 10, 11, 12
+
+_RECORD_CHECK = [(0, VTensor), (1, Sinks), (2, ConvRec), (3, WgradRec), (4, PoolRec), (5, Tail),
+                 (6, TailGrad), (7, BnUpdate), (8, GradFinal), (9, BceRec), (10, Geom), (11, Bn),
+                 (12, VSeg), (13, Sink)]
+
+# exported symbol -> (restype, argtypes)
+SIGNATURES = {
+    "isg_conv_fwd": (c_int32, [POINTER(Geom), POINTER(VTensor), c_void_p, POINTER(Sinks), c_void_p]),
+    "isg_conv_dgrad": (c_int32, [POINTER(Geom), POINTER(VTensor), c_void_p, POINTER(Sinks), c_void_p]),
+    "isg_conv_wgrad": (c_int32, [POINTER(Geom), POINTER(VTensor), POINTER(VTensor), c_void_p,
+                                 c_void_p, c_void_p]),
+    "isg_convT_fwd": (c_int32, [POINTER(Geom), POINTER(VTensor), c_void_p, POINTER(Sinks), c_void_p]),
+    "isg_maxpool_fwd": (c_int32, [POINTER(VTensor), c_int32, c_void_p, c_int64, c_void_p]),
+    "isg_maxpool_bwd": (c_int32, [POINTER(VTensor), c_int32, c_void_p, c_int64, POINTER(Sinks),
+                                  c_void_p]),
+    "isg_tail_fwd": (c_int32, [POINTER(Tail), c_void_p]),
+    "isg_tail_bwd": (c_int32, [POINTER(TailGrad), c_void_p]),
+    "isg_bn_update_running": (c_int32, [POINTER(BnUpdate), c_int32, c_void_p]),
+    "isg_grad_finalize": (c_int32, [POINTER(GradFinal), c_int32, c_void_p]),
+    "isg_bce_sigmoid": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_float, c_void_p]),
+    "isg_sigmoid_fwd": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p]),
+    "isg_sigmoid_bwd": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
+    "isg_adam": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32,
+                           c_float, c_float, c_float, c_float, c_float, c_void_p]),
+    "isg_fill_f64": (c_int32, [c_void_p, c_int64, c_double, c_void_p]),
+    "isg_mask_paste": (c_int32, [c_void_p, c_int32, c_int32, c_void_p, c_int32, c_int32, c_void_p,
+                                 c_void_p]),
+    "isg_mask_nms_workspace": (c_int64, [c_int32, c_int32, c_int32]),
+    "isg_mask_nms": (c_int32, [c_void_p, c_int32, c_int32, c_int32, c_float, c_void_p, c_void_p,
+                               c_void_p, c_void_p, c_void_p]),
+    "isg_exec": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p]),
+    "isg_last_error": (c_char_p, []),
+    "isg_abi_version": (c_int32, []),
+    "isg_record_size": (c_int32, [c_int32]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load (once) and return the ctypes handle; raises if the HIP library is absent."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"libisg.so not found at {LIB_PATH}; build it with "
+                "`python -m instancesegmentation_amd.build_lib` (there is no CPU fallback)")
+        h = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(h, name)
+            fn.restype = res
+            fn.argtypes = args
+        for which, cls in _RECORD_CHECK:
+            n = h.isg_record_size(which)
+            if n != ctypes.sizeof(cls):
+                raise RuntimeError(f"ABI mismatch: {cls.__name__} is {ctypes.sizeof(cls)} bytes "
+                                   f"in Python, {n} in libisg.so")
+        _lib = h
+    return _lib
+
+
+def check(rc, what=""):
+    if rc != 0:
+        msg = lib().isg_last_error().decode(errors="replace")
+        raise RuntimeError(f"libisg {what} failed ({rc}): {msg}")
+    return rc
+
+
+def stream_ptr(device=None):
+    return torch.cuda.current_stream(device).cuda_stream

@@ -1,0 +1,265 @@
+// C-ABI front of libisg.so: error plumbing, conv dispatch (dense MFMA vs depthwise
+// VALU) and the plan executor (include/isg.h).
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/isg.h"
+
+static thread_local std::string g_last_error;
+
+int32_t isg_set_error(int32_t code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return code;
+}
+
+int32_t isg_check_launch(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return isg_set_error(ISG_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+    return ISG_OK;
+}
+
+// implemented in conv_mfma.hip / dw_convt.hip
+int32_t isg_dense_conv_fwd(const isg_conv_geom*, const isg_vtensor*, const float*, const isg_sinks*,
+                           hipStream_t);
+int32_t isg_dense_conv_dgrad(const isg_conv_geom*, const isg_vtensor*, const float*, const isg_sinks*,
+                             hipStream_t);
+int32_t isg_dense_conv_wgrad(const isg_conv_geom*, const isg_vtensor*, const isg_vtensor*, float*,
+                             float*, hipStream_t);
+int32_t isg_depthwise_fwd(const isg_conv_geom*, const isg_vtensor*, const float*, const isg_sinks*,
+                          hipStream_t);
+int32_t isg_depthwise_dgrad(const isg_conv_geom*, const isg_vtensor*, const float*, const isg_sinks*,
+                            hipStream_t);
+int32_t isg_depthwise_wgrad(const isg_conv_geom*, const isg_vtensor*, const isg_vtensor*, float*,
+                            float*, hipStream_t);
+
+static int32_t check_geom(const isg_conv_geom* g) {
+    if (!g) return isg_set_error(ISG_ERR_INVALID, "conv: NULL geometry");
+    if (g->N < 1 || g->Ci < 1 || g->Co < 1 || g->H < 1 || g->W < 1 || g->KH < 1 || g->KW < 1 ||
+        g->SH < 1 || g->SW < 1 || g->DH < 1 || g->DW < 1 || g->PH < 0 || g->PW < 0)
+        return isg_set_error(ISG_ERR_INVALID, "conv: invalid geometry");
+    const int oh = (g->H + 2 * g->PH - g->DH * (g->KH - 1) - 1) / g->SH + 1;
+    const int ow = (g->W + 2 * g->PW - g->DW * (g->KW - 1) - 1) / g->SW + 1;
+    if (oh != g->OH || ow != g->OW)
+        return isg_set_error(ISG_ERR_INVALID, "conv: output %dx%d but geometry gives %dx%d", g->OH,
+                             g->OW, oh, ow);
+    if (g->groups != 1 && !(g->groups == g->Ci && g->Ci == g->Co))
+        return isg_set_error(ISG_ERR_UNSUPPORTED, "conv: groups=%d (dense or depthwise only)",
+                             g->groups);
+    return ISG_OK;
+}
+
+extern "C" {
+
+const char* isg_last_error(void) { return g_last_error.c_str(); }
+int32_t isg_abi_version(void) { return 1; }
+
+int32_t isg_conv_fwd(const isg_conv_geom* g, const isg_vtensor* x, const float* w,
+                     const isg_sinks* out, isg_stream_t st) {
+    if (int32_t e = check_geom(g)) return e;
+    if (g->groups == 1) return isg_dense_conv_fwd(g, x, w, out, st);
+    return isg_depthwise_fwd(g, x, w, out, st);
+}
+
+int32_t isg_conv_dgrad(const isg_conv_geom* g, const isg_vtensor* dy, const float* w,
+                       const isg_sinks* dx, isg_stream_t st) {
+    if (int32_t e = check_geom(g)) return e;
+    if (g->groups == 1) return isg_dense_conv_dgrad(g, dy, w, dx, st);
+    return isg_depthwise_dgrad(g, dy, w, dx, st);
+}
+
+int32_t isg_conv_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x,
+                       float* dw, float* dbias, isg_stream_t st) {
+    if (int32_t e = check_geom(g)) return e;
+    if (g->groups == 1) return isg_dense_conv_wgrad(g, dy, x, dw, dbias, st);
+    return isg_depthwise_wgrad(g, dy, x, dw, dbias, st);
+}
+
+// ---- plan executor ----------------------------------------------------------------
+// Blob layout, per op (all 8-byte aligned):
+//   int32 kind, int32 desc_bytes, int32 nfix, int32 pad
+//   desc_bytes of the op's argument record (one of the structs below)
+//   nfix x { int32 loc, int32 slot, int64 offset }: *(void**)(desc+loc) = table[slot]+offset
+enum {
+    OP_CONV_FWD = 1,
+    OP_CONV_DGRAD = 2,
+    OP_CONV_WGRAD = 3,
+    OP_CONVT_FWD = 4,
+    OP_MAXPOOL_FWD = 5,
+    OP_MAXPOOL_BWD = 6,
+    OP_TAIL_FWD = 7,
+    OP_TAIL_BWD = 8,
+    OP_BN_UPDATE = 9,
+    OP_GRAD_FINAL = 10,
+    OP_BCE = 11,
+    OP_MEMSET = 12,
+};
+
+struct ConvRec {
+    isg_conv_geom g;
+    isg_vtensor a;
+    const float* w;
+    isg_sinks out;
+};
+struct WgradRec {
+    isg_conv_geom g;
+    isg_vtensor dy;
+    isg_vtensor x;
+    float* dw;
+    float* dbias;
+};
+struct PoolRec {
+    isg_vtensor x;
+    int32_t k;
+    int32_t pad_;
+    float* out;
+    int64_t out_ns;
+    const float* dout;
+    int64_t dout_ns;
+    isg_sinks dx;
+};
+struct ListRec {  // followed in the record by n items (host memory)
+    int32_t n;
+    int32_t pad_;
+};
+struct BceRec {
+    const float* logits;
+    const float* target;
+    int64_t n;
+    double* loss;
+    float* dlogits;
+    float grad_scale;
+    int32_t pad_;
+};
+struct MemsetRec {
+    void* p;
+    int64_t bytes;
+};
+
+struct OpHdr {
+    int32_t kind, desc_bytes, nfix, pad_;
+};
+struct Fix {
+    int32_t loc, slot;
+    int64_t offset;
+};
+
+int32_t isg_exec(const void* ops, int32_t nops, void* const* table, isg_stream_t st) {
+    const char* p = (const char*)ops;
+    alignas(16) char buf[8192];
+    for (int i = 0; i < nops; ++i) {
+        OpHdr h;
+        std::memcpy(&h, p, sizeof(h));
+        p += sizeof(h);
+        if (h.desc_bytes < 0 || h.desc_bytes > (int)sizeof(buf))
+            return isg_set_error(ISG_ERR_INVALID, "exec: op %d bad desc size %d", i, h.desc_bytes);
+        std::memcpy(buf, p, h.desc_bytes);
+        p += (h.desc_bytes + 7) & ~7;
+        for (int f = 0; f < h.nfix; ++f) {
+            Fix fx;
+            std::memcpy(&fx, p, sizeof(fx));
+            p += sizeof(fx);
+            char* base = fx.slot >= 0 ? (char*)table[fx.slot] : nullptr;
+            void* v = base ? base + fx.offset : nullptr;
+            std::memcpy(buf + fx.loc, &v, sizeof(v));
+        }
+        int32_t rc = 0;
+        switch (h.kind) {
+            case OP_CONV_FWD: {
+                auto* r = (ConvRec*)buf;
+                rc = isg_conv_fwd(&r->g, &r->a, r->w, &r->out, st);
+                break;
+            }
+            case OP_CONV_DGRAD: {
+                auto* r = (ConvRec*)buf;
+                rc = isg_conv_dgrad(&r->g, &r->a, r->w, &r->out, st);
+                break;
+            }
+            case OP_CONV_WGRAD: {
+                auto* r = (WgradRec*)buf;
+                rc = isg_conv_wgrad(&r->g, &r->dy, &r->x, r->dw, r->dbias, st);
+                break;
+            }
+            case OP_CONVT_FWD: {
+                auto* r = (ConvRec*)buf;
+                rc = isg_convT_fwd(&r->g, &r->a, r->w, &r->out, st);
+                break;
+            }
+            case OP_MAXPOOL_FWD: {
+                auto* r = (PoolRec*)buf;
+                rc = isg_maxpool_fwd(&r->x, r->k, r->out, r->out_ns, st);
+                break;
+            }
+            case OP_MAXPOOL_BWD: {
+                auto* r = (PoolRec*)buf;
+                rc = isg_maxpool_bwd(&r->x, r->k, r->dout, r->dout_ns, &r->dx, st);
+                break;
+            }
+            case OP_TAIL_FWD:
+                rc = isg_tail_fwd((const isg_tail*)buf, st);
+                break;
+            case OP_TAIL_BWD:
+                rc = isg_tail_bwd((const isg_tail_grad*)buf, st);
+                break;
+            case OP_BN_UPDATE: {
+                auto* r = (ListRec*)buf;
+                rc = isg_bn_update_running((const isg_bn_update*)(buf + sizeof(ListRec)), r->n, st);
+                break;
+            }
+            case OP_GRAD_FINAL: {
+                auto* r = (ListRec*)buf;
+                rc = isg_grad_finalize((const isg_grad_final*)(buf + sizeof(ListRec)), r->n, st);
+                break;
+            }
+            case OP_BCE: {
+                auto* r = (BceRec*)buf;
+                rc = isg_bce_sigmoid(r->logits, r->target, r->n, r->loss, r->dlogits, r->grad_scale, st);
+                break;
+            }
+            case OP_MEMSET: {
+                auto* r = (MemsetRec*)buf;
+                if (hipMemsetAsync(r->p, 0, (size_t)r->bytes, st) != hipSuccess)
+                    rc = isg_check_launch("memset");
+                break;
+            }
+            default:
+                return isg_set_error(ISG_ERR_INVALID, "exec: op %d unknown kind %d", i, h.kind);
+        }
+        if (rc) {
+            std::string m = g_last_error;
+            return isg_set_error(rc, "exec op %d (kind %d): %s", i, h.kind, m.c_str());
+        }
+    }
+    return ISG_OK;
+}
+
+// sizes of the executor records, so the Python planner can verify its ctypes mirrors
+int32_t isg_record_size(int32_t which) {
+    switch (which) {
+        case 0: return (int32_t)sizeof(isg_vtensor);
+        case 1: return (int32_t)sizeof(isg_sinks);
+        case 2: return (int32_t)sizeof(ConvRec);
+        case 3: return (int32_t)sizeof(WgradRec);
+        case 4: return (int32_t)sizeof(PoolRec);
+        case 5: return (int32_t)sizeof(isg_tail);
+        case 6: return (int32_t)sizeof(isg_tail_grad);
+        case 7: return (int32_t)sizeof(isg_bn_update);
+        case 8: return (int32_t)sizeof(isg_grad_final);
+        case 9: return (int32_t)sizeof(BceRec);
+        case 10: return (int32_t)sizeof(isg_conv_geom);
+        case 11: return (int32_t)sizeof(isg_bn);
+        case 12: return (int32_t)sizeof(isg_vseg);
+        case 13: return (int32_t)sizeof(isg_sink);
+        default: return -1;
+    }
+}
+
+}  // extern "C"

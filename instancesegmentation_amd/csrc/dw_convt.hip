@@ -1,0 +1,382 @@
+// Depthwise convolutions and sub-pixel transposed convolutions (VALU, gfx950).
+//
+// Depthwise: the dilated 3x3 (segment.py:64-65, 127-128, 167, 183, 226) and the
+// 5x1 / 1x5 pair (segment.py:91-92, 96-97). AI is 2.5-4.5 flop/B (SURVEY.md
+// appendix), so these are plain HBM-streaming kernels: one output pixel per lane,
+// the channel's BN/activation coefficients held in registers, taps served by L1.
+//
+// Transposed conv (kernel = 2*stride, pad = stride/2; segment.py:305-306 k4s2p1 and
+// :435-436 k8s4p2): every output pixel receives exactly 2x2 taps, so a lane owns one
+// input-resolution cell and produces its full s x s output block for every output
+// channel from the cell's 3x3 input neighbourhood. Weight indices are compile-time
+// per (phase, tap) and wave-uniform, so they come from the scalar cache; the s x s
+// block is written as s vectors of s floats (coalesced across lanes).
+#include "common.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+
+ISG_DEV ChanCoef seg_coef(const isg_vseg& sg, int c) {
+    ChanCoef k = {0.f, 1.f, 0.f, 0.f};
+    if (sg.xform == ISG_XF_BN_FWD) {
+        if (sg.bn.stats || !sg.bn.train) k = fwd_coef(sg.bn, sg.slope, c);
+        else k.c3 = sg.slope ? sg.slope[c] : 0.f;
+    } else if (sg.xform == ISG_XF_BN_BWD) {
+        k = bwd_coef(sg.bn, c);
+    }
+    return k;
+}
+
+// single-segment virtual load with coefficients in registers
+ISG_DEV float seg_load(const isg_vseg& sg, const ChanCoef& k, int n, int c, int64_t hw,
+                       int64_t pix) {
+    const float x = sg.p[(int64_t)n * sg.n_stride + (int64_t)c * hw + pix];
+    if (sg.xform == ISG_XF_PLAIN) return x;
+    if (sg.xform == ISG_XF_BN_FWD) return apply_act((x - k.c0) * k.c1 + k.c2, sg.act, k.c3);
+    const float y = sg.y[(int64_t)n * sg.y_n_stride + (int64_t)c * hw + pix];
+    return k.c0 * x + k.c1 * (y - k.c2) + k.c3;
+}
+
+// Block reduction of up to 3 floats; thread 0 returns the block totals.
+template <int NV>
+ISG_DEV void block_reduce(float (&v)[NV], float* sh /* [NV][4] */) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] = wave_sum(v[i]);
+    if (lane == 0)
+#pragma unroll
+        for (int i = 0; i < NV; ++i) sh[i * 4 + wave] = v[i];
+    __syncthreads();
+    if (threadIdx.x == 0)
+#pragma unroll
+        for (int i = 0; i < NV; ++i) v[i] = sh[i * 4] + sh[i * 4 + 1] + sh[i * 4 + 2] + sh[i * 4 + 3];
+}
+
+// Single-channel sink application with the BN/act coefficients of that channel.
+struct Sink1 {
+    float mean, scale, beta, slope;
+};
+
+ISG_DEV Sink1 sink1_coef(const isg_sink& k, int cl) {
+    Sink1 s = {0.f, 1.f, 0.f, 0.f};
+    if (k.mode == ISG_SINK_ACTBWD) {
+        if (k.bn.stats || !k.bn.train) {
+            ChanCoef f = fwd_coef(k.bn, k.slope, cl);
+            s.mean = f.c0; s.scale = f.c1; s.beta = f.c2;
+        }
+        s.slope = k.slope ? k.slope[cl] : 0.f;
+    }
+    return s;
+}
+
+ISG_DEV void sink1_apply(const isg_sink& k, const Sink1& f, int cl, int n, int64_t hw,
+                         int64_t pix, float v, float (&red)[3]) {
+    if (k.mode == ISG_SINK_NONE) return;
+    const int64_t off = (int64_t)n * k.n_stride + (int64_t)cl * hw + pix;
+    if (k.mode == ISG_SINK_STORE) {
+        if (k.bias) v += k.bias[cl];
+        k.p[off] = v;
+        red[0] += v;
+        red[1] += v * v;
+    } else if (k.mode == ISG_SINK_ACCUM) {
+        k.p[off] += v;
+    } else {
+        const float y = k.y[(int64_t)n * k.y_n_stride + (int64_t)cl * hw + pix];
+        const float z = (y - f.mean) * f.scale + f.beta;
+        float g = v;
+        if (k.act == ISG_ACT_RELU) {
+            g = z > 0.f ? v : 0.f;
+        } else if (k.act == ISG_ACT_PRELU) {
+            g = z > 0.f ? v : v * f.slope;
+            red[2] += z > 0.f ? 0.f : z * v;
+        }
+        k.p[off] = g;
+        red[0] += g;
+        red[1] += g * y;
+    }
+}
+
+ISG_DEV void sink1_flush(const isg_sink& k, int cl, const float (&red)[3]) {
+    if (k.mode == ISG_SINK_STORE) {
+        if (k.stats) {
+            atomicAdd(&k.stats[cl], (double)red[0]);
+            atomicAdd(&k.stats[k.C + cl], (double)red[1]);
+        }
+    } else if (k.mode == ISG_SINK_ACTBWD) {
+        if (k.bn.stats) {
+            atomicAdd(&k.bn.stats[2 * k.C + cl], (double)red[0]);
+            atomicAdd(&k.bn.stats[3 * k.C + cl], (double)red[1]);
+        }
+        if (k.slope_grad && k.act == ISG_ACT_PRELU) atomicAdd(&k.slope_grad[cl], (double)red[2]);
+    }
+}
+
+ISG_DEV bool sink1_needs_red(const isg_sink& k) {
+    return (k.mode == ISG_SINK_STORE && k.stats) || k.mode == ISG_SINK_ACTBWD;
+}
+
+struct DwArgs {
+    isg_vseg x;      // fwd: input; dgrad: dy
+    isg_sink out;
+    const float* w;  // [C][KH][KW]
+    int N, C, H, W, OH, OW, KH, KW, PH, PW, DH, DW;
+};
+
+// forward (dgrad=false): out[c,oy,ox] = sum_t w[c,t] * x[c, oy-PH+kh*DH, ox-PW+kw*DW]
+// dgrad (dgrad=true)   : dx[c,iy,ix] = sum_t w[c,t] * dy[c, iy+PH-kh*DH, ix+PW-kw*DW]
+template <bool DGRAD>
+__global__ __launch_bounds__(kThreads) void dw_kernel(DwArgs a) {
+    __shared__ float sh[12];
+    const int c = blockIdx.y, n = blockIdx.z;
+    // source plane = x (fwd) or dy (dgrad); destination plane = out (fwd) or dx
+    const int SH_ = DGRAD ? a.OH : a.H, SW_ = DGRAD ? a.OW : a.W;
+    const int DH_ = DGRAD ? a.H : a.OH, DW_ = DGRAD ? a.W : a.OW;
+    const int64_t dhw = (int64_t)DH_ * DW_, shw = (int64_t)SH_ * SW_;
+    const int64_t pix = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    const ChanCoef k = seg_coef(a.x, c);
+    const Sink1 f = sink1_coef(a.out, c);
+    float red[3] = {0.f, 0.f, 0.f};
+    if (pix < dhw) {
+        const int oy = (int)(pix / DW_), ox = (int)(pix - (int64_t)oy * DW_);
+        const float* wc = a.w + c * a.KH * a.KW;
+        float acc = 0.f;
+        for (int kh = 0; kh < a.KH; ++kh) {
+            const int iy = DGRAD ? oy + a.PH - kh * a.DH : oy - a.PH + kh * a.DH;
+            if (iy < 0 || iy >= SH_) continue;
+            for (int kw = 0; kw < a.KW; ++kw) {
+                const int ix = DGRAD ? ox + a.PW - kw * a.DW : ox - a.PW + kw * a.DW;
+                if (ix < 0 || ix >= SW_) continue;
+                acc += wc[kh * a.KW + kw] * seg_load(a.x, k, n, c, shw, (int64_t)iy * SW_ + ix);
+            }
+        }
+        sink1_apply(a.out, f, c, n, dhw, pix, acc, red);
+    }
+    if (sink1_needs_red(a.out)) {
+        block_reduce<3>(red, sh);
+        if (threadIdx.x == 0) sink1_flush(a.out, c, red);
+    }
+}
+
+// weight gradient: dw[c,t] += sum_p dy[c,p] * x[c, p + tap_t]; dbias[c] += sum_p dy
+constexpr int kMaxTaps = 9;
+struct DwWgArgs {
+    isg_vseg dy, x;
+    float* dw;
+    float* dbias;
+    int N, C, H, W, OH, OW, KH, KW, PH, PW, DH, DW;
+    int64_t pix_per_block;
+};
+
+__global__ __launch_bounds__(kThreads) void dw_wgrad_kernel(DwWgArgs a) {
+    __shared__ float sh[(kMaxTaps + 1) * 4];
+    const int c = blockIdx.y;
+    const ChanCoef kd = seg_coef(a.dy, c);
+    const ChanCoef kx = seg_coef(a.x, c);
+    const int64_t ohw = (int64_t)a.OH * a.OW, xhw = (int64_t)a.H * a.W;
+    const int64_t P = (int64_t)a.N * ohw;
+    const int64_t pb = (int64_t)blockIdx.x * a.pix_per_block;
+    int64_t pe = pb + a.pix_per_block;
+    if (pe > P) pe = P;
+    const int KK = a.KH * a.KW;
+    float acc[kMaxTaps + 1];
+#pragma unroll
+    for (int t = 0; t <= kMaxTaps; ++t) acc[t] = 0.f;
+    for (int64_t p = pb + threadIdx.x; p < pe; p += kThreads) {
+        const int n = (int)(p / ohw);
+        const int64_t pix = p - (int64_t)n * ohw;
+        const int oy = (int)(pix / a.OW), ox = (int)(pix - (int64_t)oy * a.OW);
+        const float d = seg_load(a.dy, kd, n, c, ohw, pix);
+        acc[kMaxTaps] += d;
+#pragma unroll
+        for (int t = 0; t < kMaxTaps; ++t) {
+            if (t < KK) {
+                const int kh = t / a.KW, kw = t - kh * a.KW;
+                const int iy = oy - a.PH + kh * a.DH, ix = ox - a.PW + kw * a.DW;
+                if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
+                    acc[t] += d * seg_load(a.x, kx, n, c, xhw, (int64_t)iy * a.W + ix);
+            }
+        }
+    }
+    block_reduce<kMaxTaps + 1>(acc, sh);
+    if (threadIdx.x == 0) {
+        for (int t = 0; t < KK; ++t) atomicAdd(&a.dw[c * KK + t], acc[t]);
+        if (a.dbias) atomicAdd(&a.dbias[c], acc[kMaxTaps]);
+    }
+}
+
+// ---- transposed convolution, kernel 2S, stride S, pad S/2 --------------------------
+struct CtArgs {
+    isg_vseg x;      // [N][Ci][H][W]
+    isg_sink out;    // [N][Co][H*S][W*S]
+    const float* w;  // [Ci][Co][2S][2S]
+    int N, Ci, H, W;
+};
+
+template <int S, int CO>
+__global__ __launch_bounds__(kThreads) void convT_kernel(CtArgs a) {
+    constexpr int K = 2 * S, P = S / 2;
+    __shared__ float sh[CO][2][4];
+    const int64_t hw = (int64_t)a.H * a.W;
+    const int64_t cell = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    const int64_t ncell = (int64_t)a.N * hw;
+    const bool valid = cell < ncell;
+    int n = 0, i = 0, j = 0;
+    if (valid) {
+        n = (int)(cell / hw);
+        const int64_t r = cell - (int64_t)n * hw;
+        i = (int)(r / a.W);
+        j = (int)(r - (int64_t)i * a.W);
+    }
+    float acc[S][S][CO];
+#pragma unroll
+    for (int u = 0; u < S; ++u)
+#pragma unroll
+        for (int v = 0; v < S; ++v)
+#pragma unroll
+            for (int co = 0; co < CO; ++co) acc[u][v][co] = 0.f;
+
+    for (int ci = 0; ci < a.Ci; ++ci) {
+        const ChanCoef kc = seg_coef(a.x, ci);
+        float nb[3][3];
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx) {
+                const int yy = i + dy - 1, xx = j + dx - 1;
+                nb[dy][dx] = (valid && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W)
+                                 ? seg_load(a.x, kc, n, ci, hw, (int64_t)yy * a.W + xx)
+                                 : 0.f;
+            }
+        const float* wci = a.w + (int64_t)ci * CO * K * K;
+#pragma unroll
+        for (int u = 0; u < S; ++u)
+#pragma unroll
+            for (int dy = 0; dy < 3; ++dy) {
+                const int kh = u + P - (dy - 1) * S;  // oh = i*S+u = (i+dy-1)*S - P + kh
+                if (kh < 0 || kh >= K) continue;
+#pragma unroll
+                for (int v = 0; v < S; ++v)
+#pragma unroll
+                    for (int dx = 0; dx < 3; ++dx) {
+                        const int kw = v + P - (dx - 1) * S;
+                        if (kw < 0 || kw >= K) continue;
+                        const float xv = nb[dy][dx];
+#pragma unroll
+                        for (int co = 0; co < CO; ++co)
+                            acc[u][v][co] += xv * wci[(co * K + kh) * K + kw];
+                    }
+            }
+    }
+    // epilogue
+    const isg_sink& o = a.out;
+    const int OW = a.W * S;
+    const int64_t ohw = hw * S * S;
+    float s0[CO], s1[CO];
+#pragma unroll
+    for (int co = 0; co < CO; ++co) {
+        s0[co] = 0.f;
+        s1[co] = 0.f;
+        const float b = o.bias ? o.bias[co] : 0.f;
+        if (valid) {
+            float* dst = o.p + (int64_t)n * o.n_stride + (int64_t)co * ohw;
+#pragma unroll
+            for (int u = 0; u < S; ++u) {
+                float vals[S];
+#pragma unroll
+                for (int v = 0; v < S; ++v) {
+                    vals[v] = acc[u][v][co] + b;
+                    s0[co] += vals[v];
+                    s1[co] += vals[v] * vals[v];
+                }
+                float* row = dst + (int64_t)(i * S + u) * OW + j * S;
+                if constexpr (S == 4) {
+                    *reinterpret_cast<f32x4*>(row) = f32x4{vals[0], vals[1], vals[2], vals[3]};
+                } else {
+#pragma unroll
+                    for (int v = 0; v < S; ++v) row[v] = vals[v];
+                }
+            }
+        }
+    }
+    if (o.stats) {
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+        for (int co = 0; co < CO; ++co) {
+            const float a0 = wave_sum(s0[co]), a1 = wave_sum(s1[co]);
+            if (lane == 0) {
+                sh[co][0][wave] = a0;
+                sh[co][1][wave] = a1;
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x < CO) {
+            const int co = threadIdx.x;
+            const float t0 = sh[co][0][0] + sh[co][0][1] + sh[co][0][2] + sh[co][0][3];
+            const float t1 = sh[co][1][0] + sh[co][1][1] + sh[co][1][2] + sh[co][1][3];
+            atomicAdd(&o.stats[co], (double)t0);
+            atomicAdd(&o.stats[o.C + co], (double)t1);
+        }
+    }
+}
+
+}  // namespace
+
+int32_t isg_depthwise_fwd(const isg_conv_geom* g, const isg_vtensor* x, const float* w,
+                          const isg_sinks* out, hipStream_t st) {
+    if (x->nseg != 1 || out->nsink != 1 || g->SH != 1 || g->SW != 1 || g->Ci != g->Co)
+        return isg_set_error(ISG_ERR_UNSUPPORTED, "depthwise fwd: need 1 seg/sink, stride 1");
+    DwArgs a{x->s[0], out->s[0], w, g->N, g->Ci, g->H, g->W, g->OH, g->OW,
+             g->KH, g->KW, g->PH, g->PW, g->DH, g->DW};
+    dim3 grid((unsigned)(((int64_t)g->OH * g->OW + kThreads - 1) / kThreads), g->Ci, g->N);
+    hipLaunchKernelGGL(dw_kernel<false>, grid, dim3(kThreads), 0, st, a);
+    return isg_check_launch("dw_kernel<fwd>");
+}
+
+int32_t isg_depthwise_dgrad(const isg_conv_geom* g, const isg_vtensor* dy, const float* w,
+                            const isg_sinks* dx, hipStream_t st) {
+    if (dy->nseg != 1 || dx->nsink != 1 || g->SH != 1 || g->SW != 1 || g->Ci != g->Co)
+        return isg_set_error(ISG_ERR_UNSUPPORTED, "depthwise dgrad: need 1 seg/sink, stride 1");
+    DwArgs a{dy->s[0], dx->s[0], w, g->N, g->Ci, g->H, g->W, g->OH, g->OW,
+             g->KH, g->KW, g->PH, g->PW, g->DH, g->DW};
+    dim3 grid((unsigned)(((int64_t)g->H * g->W + kThreads - 1) / kThreads), g->Ci, g->N);
+    hipLaunchKernelGGL(dw_kernel<true>, grid, dim3(kThreads), 0, st, a);
+    return isg_check_launch("dw_kernel<dgrad>");
+}
+
+int32_t isg_depthwise_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x,
+                            float* dw, float* dbias, hipStream_t st) {
+    if (dy->nseg != 1 || x->nseg != 1 || g->KH * g->KW > kMaxTaps)
+        return isg_set_error(ISG_ERR_UNSUPPORTED, "depthwise wgrad: need 1 seg, <= 9 taps");
+    DwWgArgs a{};
+    a.dy = dy->s[0]; a.x = x->s[0]; a.dw = dw; a.dbias = dbias;
+    a.N = g->N; a.C = g->Ci; a.H = g->H; a.W = g->W; a.OH = g->OH; a.OW = g->OW;
+    a.KH = g->KH; a.KW = g->KW; a.PH = g->PH; a.PW = g->PW; a.DH = g->DH; a.DW = g->DW;
+    const int64_t P = (int64_t)g->N * g->OH * g->OW;
+    int64_t splits = (P + 4095) / 4096;
+    const int64_t maxsplit = (2048 + g->Ci - 1) / g->Ci;
+    if (splits > maxsplit) splits = maxsplit;
+    if (splits < 1) splits = 1;
+    a.pix_per_block = (P + splits - 1) / splits;
+    hipLaunchKernelGGL(dw_wgrad_kernel, dim3((unsigned)splits, g->Ci), dim3(kThreads), 0, st, a);
+    return isg_check_launch("dw_wgrad_kernel");
+}
+
+int32_t isg_convT_fwd(const isg_conv_geom* g, const isg_vtensor* x, const float* w,
+                      const isg_sinks* out, isg_stream_t st) {
+    if (x->nseg != 1 || out->nsink != 1 || out->s[0].mode != ISG_SINK_STORE)
+        return isg_set_error(ISG_ERR_UNSUPPORTED, "convT fwd: need 1 seg / 1 STORE sink");
+    const int S = g->SH;
+    if (g->SW != S || g->KH != 2 * S || g->KW != 2 * S || g->PH != S / 2 || g->PW != S / 2 ||
+        g->OH != g->H * S || g->OW != g->W * S)
+        return isg_set_error(ISG_ERR_UNSUPPORTED, "convT fwd: need k=2s, p=s/2");
+    CtArgs a{x->s[0], out->s[0], w, g->N, g->Ci, g->H, g->W};
+    dim3 grid((unsigned)(((int64_t)g->N * g->H * g->W + kThreads - 1) / kThreads));
+    if (S == 2 && g->Co == 16) hipLaunchKernelGGL((convT_kernel<2, 16>), grid, dim3(kThreads), 0, st, a);
+    else if (S == 2 && g->Co == 4) hipLaunchKernelGGL((convT_kernel<2, 4>), grid, dim3(kThreads), 0, st, a);
+    else if (S == 4 && g->Co == 4) hipLaunchKernelGGL((convT_kernel<4, 4>), grid, dim3(kThreads), 0, st, a);
+    else if (S == 4 && g->Co == 1) hipLaunchKernelGGL((convT_kernel<4, 1>), grid, dim3(kThreads), 0, st, a);
+    else if (S == 2 && g->Co == 1) hipLaunchKernelGGL((convT_kernel<2, 1>), grid, dim3(kThreads), 0, st, a);
+    else return isg_set_error(ISG_ERR_UNSUPPORTED, "convT fwd: s=%d Co=%d", S, g->Co);
+    return isg_check_launch("convT_kernel");
+}

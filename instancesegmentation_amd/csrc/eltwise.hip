@@ -1,0 +1,539 @@
+// Element-wise / reduction kernels of the hot path (gfx950, HBM-streaming).
+//
+//  * residual-block tails  out = act(sum of BN'd / plain / upsampled terms)
+//    (segment.py:76-77, 107-109, 147-148, 202-207, 255-259, 331-333) and their
+//    backward, which also produces the BatchNorm-backward statistics of every BN term
+//    and the PReLU slope gradient in the same pass;
+//  * max-pool k x k / stride k (segment.py:29, 145) forward and backward;
+//  * BatchNorm running-stat update and parameter-gradient finalisation;
+//  * fused sigmoid + BCELoss (segment.py:534, train_instance.py:299,378);
+//  * Adam (train_instance.py:297,380).
+#include <cstring>
+
+#include "common.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+
+ISG_DEV ChanCoef seg_coef(const isg_vseg& sg, int c) {
+    ChanCoef k = {0.f, 1.f, 0.f, 0.f};
+    if (sg.xform == ISG_XF_BN_FWD) {
+        if (sg.bn.stats || !sg.bn.train) k = fwd_coef(sg.bn, sg.slope, c);
+        else k.c3 = sg.slope ? sg.slope[c] : 0.f;
+    } else if (sg.xform == ISG_XF_BN_BWD) {
+        k = bwd_coef(sg.bn, c);
+    }
+    return k;
+}
+
+ISG_DEV float seg_val(const isg_vseg& sg, const ChanCoef& k, float x, float y) {
+    if (sg.xform == ISG_XF_PLAIN) return x;
+    if (sg.xform == ISG_XF_BN_FWD) return apply_act((x - k.c0) * k.c1 + k.c2, sg.act, k.c3);
+    return k.c0 * x + k.c1 * (y - k.c2) + k.c3;
+}
+
+template <int NV>
+ISG_DEV void block_reduce(float (&v)[NV], float* sh) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] = wave_sum(v[i]);
+    if (lane == 0)
+#pragma unroll
+        for (int i = 0; i < NV; ++i) sh[i * 4 + wave] = v[i];
+    __syncthreads();
+    if (threadIdx.x == 0)
+#pragma unroll
+        for (int i = 0; i < NV; ++i) v[i] = sh[i * 4] + sh[i * 4 + 1] + sh[i * 4 + 2] + sh[i * 4 + 3];
+}
+
+// ---- residual tail ----------------------------------------------------------------
+// Thread unit: a 2x2 pixel quad of one (n, c) plane (H, W are even in this network:
+// input sides are multiples of 16), so an x2-upsampled term is one
+// low-resolution value per thread and its gradient is the quad's sum.
+ISG_DEV float term_raw(const isg_vseg& t, int up, int n, int c, int H, int W, int y, int x,
+                       float* yraw) {
+    int64_t hw, pix;
+    if (up) {
+        const int h2 = H >> 1, w2 = W >> 1;
+        hw = (int64_t)h2 * w2;
+        pix = (int64_t)(y >> 1) * w2 + (x >> 1);
+    } else {
+        hw = (int64_t)H * W;
+        pix = (int64_t)y * W + x;
+    }
+    *yraw = 0.f;
+    return t.p[(int64_t)n * t.n_stride + (int64_t)c * hw + pix];
+}
+
+__global__ __launch_bounds__(kThreads) void tail_fwd_kernel(isg_tail t) {
+    const int c = blockIdx.y, n = blockIdx.z;
+    const int H = t.H, W = t.W;
+    const int qw = W >> 1;
+    const int64_t nq = (int64_t)(H >> 1) * qw;
+    const int64_t q = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (q >= nq) return;
+    const int qy = (int)(q / qw), qx = (int)(q - (int64_t)qy * qw);
+    ChanCoef k[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+        if (i < t.nterm) k[i] = seg_coef(t.term[i], c);
+    const float slope = (t.act == ISG_ACT_PRELU) ? t.slope[c] : 0.f;
+    const int64_t hw = (int64_t)H * W;
+    float* out = t.out + (int64_t)n * t.out_n_stride + (int64_t)c * hw;
+#pragma unroll
+    for (int dy = 0; dy < 2; ++dy) {
+        float v[2] = {0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            if (i >= t.nterm) continue;
+            const isg_vseg& tm = t.term[i];
+            const int y = 2 * qy + dy;
+            if (t.up[i]) {
+                float dummy;
+                const float x0 = term_raw(tm, 1, n, c, H, W, y, 2 * qx, &dummy);
+                const float tv = seg_val(tm, k[i], x0, 0.f);
+                v[0] += tv;
+                v[1] += tv;
+            } else {
+                const int64_t off = (int64_t)n * tm.n_stride + (int64_t)c * hw + (int64_t)y * W + 2 * qx;
+                const float2 xv = *reinterpret_cast<const float2*>(tm.p + off);
+                v[0] += seg_val(tm, k[i], xv.x, 0.f);
+                v[1] += seg_val(tm, k[i], xv.y, 0.f);
+            }
+        }
+        float2 o;
+        o.x = apply_act(v[0], t.act, slope);
+        o.y = apply_act(v[1], t.act, slope);
+        *reinterpret_cast<float2*>(out + (int64_t)(2 * qy + dy) * W + 2 * qx) = o;
+    }
+}
+
+__global__ __launch_bounds__(kThreads) void tail_bwd_kernel(isg_tail_grad tg) {
+    __shared__ float sh[8 * 4];
+    const isg_tail& t = tg.f;
+    const int c = blockIdx.y, n = blockIdx.z;
+    const int H = t.H, W = t.W;
+    const int qw = W >> 1;
+    const int64_t nq = (int64_t)(H >> 1) * qw;
+    const int64_t q = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    const bool valid = q < nq;
+    const int qy = valid ? (int)(q / qw) : 0, qx = valid ? (int)(q - (int64_t)qy * qw) : 0;
+    ChanCoef k[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+        if (i < t.nterm) k[i] = seg_coef(t.term[i], c);
+    const float slope = (t.act == ISG_ACT_PRELU) ? t.slope[c] : 0.f;
+    const int64_t hw = (int64_t)H * W;
+    // red: [0..2] gsum per term (same g), [3..5] g*y per term, [6] slope grad
+    float red[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    float gq[2][2];
+    float upsum = 0.f;
+    if (valid) {
+#pragma unroll
+        for (int dy = 0; dy < 2; ++dy) {
+            const int y = 2 * qy + dy;
+            const int64_t prow = (int64_t)y * W + 2 * qx;
+            const float2 d = *reinterpret_cast<const float2*>(
+                tg.dout + (int64_t)n * tg.dout_n_stride + (int64_t)c * hw + prow);
+            float pre[2] = {0.f, 0.f};
+            float raw[3][2];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                raw[i][0] = raw[i][1] = 0.f;
+                if (i >= t.nterm) continue;
+                const isg_vseg& tm = t.term[i];
+                if (t.up[i]) {
+                    float dummy;
+                    const float x0 = term_raw(tm, 1, n, c, H, W, y, 2 * qx, &dummy);
+                    raw[i][0] = raw[i][1] = x0;
+                } else {
+                    const float2 xv = *reinterpret_cast<const float2*>(
+                        tm.p + (int64_t)n * tm.n_stride + (int64_t)c * hw + prow);
+                    raw[i][0] = xv.x;
+                    raw[i][1] = xv.y;
+                }
+                pre[0] += seg_val(tm, k[i], raw[i][0], 0.f);
+                pre[1] += seg_val(tm, k[i], raw[i][1], 0.f);
+            }
+            const float dv[2] = {d.x, d.y};
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                float g = dv[e];
+                if (t.act == ISG_ACT_RELU) {
+                    g = pre[e] > 0.f ? dv[e] : 0.f;
+                } else if (t.act == ISG_ACT_PRELU) {
+                    g = pre[e] > 0.f ? dv[e] : dv[e] * slope;
+                    red[6] += pre[e] > 0.f ? 0.f : pre[e] * dv[e];
+                }
+                gq[dy][e] = g;
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    if (i >= t.nterm) continue;
+                    if (t.term[i].xform == ISG_XF_BN_FWD) {
+                        red[i] += g;
+                        red[3 + i] += g * raw[i][e];
+                    }
+                }
+            }
+            if (tg.g) {
+                *reinterpret_cast<float2*>(tg.g + (int64_t)n * tg.g_n_stride + (int64_t)c * hw + prow) =
+                    make_float2(gq[dy][0], gq[dy][1]);
+            }
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                if (i >= t.nterm || t.term[i].xform != ISG_XF_PLAIN || !tg.dterm[i] || t.up[i]) continue;
+                float* dst = tg.dterm[i] + (int64_t)n * tg.dterm_n_stride[i] + (int64_t)c * hw + prow;
+                float2 o = make_float2(gq[dy][0], gq[dy][1]);
+                if (tg.dterm_accum[i]) {
+                    const float2 old = *reinterpret_cast<const float2*>(dst);
+                    o.x += old.x;
+                    o.y += old.y;
+                }
+                *reinterpret_cast<float2*>(dst) = o;
+            }
+        }
+        upsum = (gq[0][0] + gq[0][1]) + (gq[1][0] + gq[1][1]);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            if (i >= t.nterm || t.term[i].xform != ISG_XF_PLAIN || !tg.dterm[i] || !t.up[i]) continue;
+            const int64_t lhw = (int64_t)(H >> 1) * (W >> 1);
+            float* dst = tg.dterm[i] + (int64_t)n * tg.dterm_n_stride[i] + (int64_t)c * lhw + q;
+            *dst = tg.dterm_accum[i] ? *dst + upsum : upsum;
+        }
+    }
+    bool need = (t.act == ISG_ACT_PRELU && tg.slope_grad);
+    for (int i = 0; i < t.nterm; ++i) need |= (t.term[i].xform == ISG_XF_BN_FWD);
+    if (!need) return;
+    float rv[8] = {red[0], red[1], red[2], red[3], red[4], red[5], red[6], 0.f};
+    block_reduce<8>(rv, sh);
+    if (threadIdx.x == 0) {
+        for (int i = 0; i < t.nterm; ++i) {
+            const isg_vseg& tm = t.term[i];
+            if (tm.xform == ISG_XF_BN_FWD && tm.bn.stats) {
+                atomicAdd(&tm.bn.stats[2 * tm.bn.C + c], (double)rv[i]);
+                atomicAdd(&tm.bn.stats[3 * tm.bn.C + c], (double)rv[3 + i]);
+            }
+        }
+        if (t.act == ISG_ACT_PRELU && tg.slope_grad) atomicAdd(&tg.slope_grad[c], (double)rv[6]);
+    }
+}
+
+// ---- max-pool ---------------------------------------------------------------------
+struct PoolArgs {
+    isg_vtensor x;
+    int k;
+    float* out;
+    int64_t out_n_stride;
+    const float* dout;
+    int64_t dout_n_stride;
+    isg_sinks dx;
+};
+
+template <bool BWD>
+__global__ __launch_bounds__(kThreads) void maxpool_kernel(PoolArgs a) {
+    __shared__ ChanCoef coef[ISG_MAX_CH];
+    load_vt_coefs(a.x, coef, threadIdx.x, kThreads);
+    __syncthreads();
+    const int c = blockIdx.y, n = blockIdx.z;
+    const int H = a.x.H, W = a.x.W, k = a.k;
+    const int OH = H / k, OW = W / k;
+    const int64_t ohw = (int64_t)OH * OW, hw = (int64_t)H * W;
+    const int64_t op = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (op >= ohw) return;
+    const int oy = (int)(op / OW), ox = (int)(op - (int64_t)oy * OW);
+    // torch CPU max_pool2d: maxval=-inf, maxindex=window start; take val if
+    // (val > maxval) || isnan(val)  -> first maximum wins, NaN propagates
+    float best = -INFINITY;
+    int bi = 0;
+    for (int dy = 0; dy < k; ++dy)
+        for (int dx = 0; dx < k; ++dx) {
+            const int64_t pix = (int64_t)(oy * k + dy) * W + ox * k + dx;
+            const float v = vt_load(a.x, coef, n, c, hw, pix);
+            if (v > best || isnan(v)) {
+                best = v;
+                bi = dy * k + dx;
+            }
+        }
+    if (!BWD) {
+        a.out[(int64_t)n * a.out_n_stride + (int64_t)c * ohw + op] = best;
+    } else {
+        const float d = a.dout[(int64_t)n * a.dout_n_stride + (int64_t)c * ohw + op];
+        const int s = sink_of(a.dx, c);
+        const isg_sink& sk = a.dx.s[s];
+        const int cl = c - sk.c0;
+        if (sk.mode == ISG_SINK_NONE) return;
+        float* base = sk.p + (int64_t)n * sk.n_stride + (int64_t)cl * hw;
+        for (int dy = 0; dy < k; ++dy)
+            for (int dx = 0; dx < k; ++dx) {
+                const int64_t pix = (int64_t)(oy * k + dy) * W + ox * k + dx;
+                const float v = (dy * k + dx == bi) ? d : 0.f;
+                if (sk.mode == ISG_SINK_ACCUM) {
+                    if (v != 0.f) base[pix] += v;
+                } else {
+                    base[pix] = v;
+                }
+            }
+    }
+}
+
+// ---- BatchNorm running stats & gradient finalisation -------------------------------
+struct BnUpdateList {
+    isg_bn_update it[ISG_LIST_CHUNK];
+};
+struct GradFinalList {
+    isg_grad_final it[ISG_LIST_CHUNK];
+};
+
+__global__ void bn_update_kernel(BnUpdateList items, int nitems) {
+    const int it = blockIdx.x;
+    if (it >= nitems) return;
+    const isg_bn_update& u = items.it[it];
+    for (int c = threadIdx.x; c < u.C; c += blockDim.x) {
+        const double M = (double)u.count;
+        const double mean = u.stats[c] / M;
+        double var = u.stats[u.C + c] / M - mean * mean;
+        if (var < 0.0) var = 0.0;
+        const double unb = M > 1.0 ? var * M / (M - 1.0) : var;
+        const float m = u.momentum;
+        u.running_mean[c] = (1.f - m) * u.running_mean[c] + m * (float)mean;
+        u.running_var[c] = (1.f - m) * u.running_var[c] + m * (float)unb;
+    }
+    if (threadIdx.x == 0 && u.num_batches_tracked) u.num_batches_tracked[0] += 1;
+}
+
+__global__ void grad_final_kernel(GradFinalList items, int nitems) {
+    const int it = blockIdx.x;
+    if (it >= nitems) return;
+    const isg_grad_final& f = items.it[it];
+    for (int c = threadIdx.x; c < f.C; c += blockDim.x) {
+        if (f.slope_acc) {
+            f.dslope[c] = (float)f.slope_acc[c];
+            continue;
+        }
+        const double M = (double)f.count;
+        double mean, rstd;
+        if (f.train) {
+            mean = f.stats[c] / M;
+            double var = f.stats[f.C + c] / M - mean * mean;
+            if (var < 0.0) var = 0.0;
+            rstd = 1.0 / sqrt(var + (double)f.eps);
+        } else {
+            mean = (double)f.running_mean[c];
+            rstd = 1.0 / sqrt((double)f.running_var[c] + (double)f.eps);
+        }
+        const double gs = f.stats[2 * f.C + c];
+        const double gys = f.stats[3 * f.C + c];
+        const double dgamma = rstd * (gys - mean * gs);
+        if (f.dgamma) f.dgamma[c] = (float)dgamma;
+        if (f.dbeta) f.dbeta[c] = (float)gs;
+        if (f.dconv_bias) {
+            // sum over pixels of dy = A*g + B*(y-mean) + C  (BatchNorm backward)
+            const double gam = (double)f.gamma[c];
+            double db;
+            if (f.train) {
+                const double sy = f.stats[c];
+                const double mg = gs / M, mgx = rstd * (gys - mean * gs) / M;
+                db = gam * rstd * (gs - M * mg) - gam * rstd * rstd * mgx * (sy - M * mean);
+            } else {
+                db = gam * rstd * gs;
+            }
+            f.dconv_bias[c] = (float)db;
+        }
+    }
+}
+
+// ---- sigmoid + BCE ----------------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void bce_kernel(const float* logits, const float* target,
+                                                        int64_t n, double* loss_acc, float* dlogits,
+                                                        float grad_scale) {
+#pragma clang fp contract(off)
+    __shared__ double sh[4];
+    double acc = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * kThreads) {
+        const float x = logits[i];
+        const float t = target[i];
+        const float p = 1.f / (1.f + expf(-x));
+        float lp = logf(p);
+        float l1p = logf(1.f - p);
+        lp = lp < -100.f ? -100.f : lp;
+        l1p = l1p < -100.f ? -100.f : l1p;
+        const float l = -(t * lp + (1.f - t) * l1p);
+        acc += (double)l;
+        if (dlogits) {
+            // torch binary_cross_entropy_backward: grad*(p-t)/max((1-p)*p, 1e-12),
+            // then sigmoid_backward: g*(1-p)*p
+            float den = (1.f - p) * p;
+            den = den < 1e-12f ? 1e-12f : den;
+            const float gp = grad_scale * (p - t) / den;
+            dlogits[i] = gp * (1.f - p) * p;
+        }
+    }
+    acc = wave_sum_d(acc);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) sh[wave] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(loss_acc, sh[0] + sh[1] + sh[2] + sh[3]);
+}
+
+__global__ void sigmoid_fwd_kernel(const float* x, float* y, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        y[i] = 1.f / (1.f + expf(-x[i]));
+}
+
+__global__ void sigmoid_bwd_kernel(const float* y, const float* dy, float* dx, int64_t n) {
+#pragma clang fp contract(off)
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        dx[i] = dy[i] * (1.f - y[i]) * y[i];
+}
+
+// ---- Adam ---------------------------------------------------------------------------
+// torch.optim.Adam single-tensor math (torch 2.10 _single_tensor_adam):
+//   m.lerp_(g, 1-b1); v = v*b2 + (1-b2)*g*g; denom = sqrt(v)/sqrt(bc2) + eps;
+//   p += (-lr/bc1) * m / denom
+__global__ void adam_kernel(float* p, const float* g, float* m, float* v, const uint8_t* live,
+                            int64_t n, float w1, float b2, float one_m_b2, float bc2_sqrt,
+                            float neg_step, float eps, float wd) {
+#pragma clang fp contract(off)
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        if (live && !live[i]) continue;
+        float gi = g[i];
+        const float pi = p[i];
+        if (wd != 0.f) gi = gi + wd * pi;
+        float mi = m[i];
+        mi = mi + w1 * (gi - mi);  // lerp with weight < 0.5
+        float vi = v[i] * b2;
+        vi = vi + one_m_b2 * gi * gi;
+        const float denom = sqrtf(vi) / bc2_sqrt + eps;
+        m[i] = mi;
+        v[i] = vi;
+        p[i] = pi + neg_step * mi / denom;
+    }
+}
+
+__global__ void fill_f64_kernel(double* p, int64_t n, double v) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        p[i] = v;
+}
+
+unsigned grid_for(int64_t n, int cap = 2048) {
+    int64_t b = (n + kThreads - 1) / kThreads;
+    if (b > cap) b = cap;
+    if (b < 1) b = 1;
+    return (unsigned)b;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t isg_tail_fwd(const isg_tail* t, isg_stream_t st) {
+    if ((t->H & 1) || (t->W & 1) || t->nterm < 1 || t->nterm > 3)
+        return isg_set_error(ISG_ERR_UNSUPPORTED, "tail fwd: H, W must be even, 1..3 terms");
+    dim3 grid((unsigned)((((int64_t)t->H / 2) * (t->W / 2) + kThreads - 1) / kThreads), t->C, t->N);
+    hipLaunchKernelGGL(tail_fwd_kernel, grid, dim3(kThreads), 0, st, *t);
+    return isg_check_launch("tail_fwd_kernel");
+}
+
+int32_t isg_tail_bwd(const isg_tail_grad* t, isg_stream_t st) {
+    const isg_tail& f = t->f;
+    if ((f.H & 1) || (f.W & 1) || f.nterm < 1 || f.nterm > 3)
+        return isg_set_error(ISG_ERR_UNSUPPORTED, "tail bwd: H, W must be even, 1..3 terms");
+    dim3 grid((unsigned)((((int64_t)f.H / 2) * (f.W / 2) + kThreads - 1) / kThreads), f.C, f.N);
+    hipLaunchKernelGGL(tail_bwd_kernel, grid, dim3(kThreads), 0, st, *t);
+    return isg_check_launch("tail_bwd_kernel");
+}
+
+int32_t isg_maxpool_fwd(const isg_vtensor* x, int32_t k, float* out, int64_t out_n_stride,
+                        isg_stream_t st) {
+    if (k < 1 || x->H % k || x->W % k) return isg_set_error(ISG_ERR_UNSUPPORTED, "maxpool: H,W %% k");
+    int C = 0;
+    for (int i = 0; i < x->nseg; ++i) C += x->s[i].C;
+    PoolArgs a{};
+    a.x = *x; a.k = k; a.out = out; a.out_n_stride = out_n_stride;
+    dim3 grid((unsigned)(((int64_t)(x->H / k) * (x->W / k) + kThreads - 1) / kThreads), C, x->N);
+    hipLaunchKernelGGL(maxpool_kernel<false>, grid, dim3(kThreads), 0, st, a);
+    return isg_check_launch("maxpool_kernel<fwd>");
+}
+
+int32_t isg_maxpool_bwd(const isg_vtensor* x, int32_t k, const float* dout, int64_t dout_n_stride,
+                        const isg_sinks* dx, isg_stream_t st) {
+    if (k < 1 || x->H % k || x->W % k) return isg_set_error(ISG_ERR_UNSUPPORTED, "maxpool: H,W %% k");
+    int C = 0;
+    for (int i = 0; i < x->nseg; ++i) C += x->s[i].C;
+    for (int i = 0; i < dx->nsink; ++i)
+        if (dx->s[i].mode == ISG_SINK_ACTBWD)
+            return isg_set_error(ISG_ERR_UNSUPPORTED, "maxpool bwd: ACTBWD sink");
+    PoolArgs a{};
+    a.x = *x; a.k = k; a.dout = dout; a.dout_n_stride = dout_n_stride; a.dx = *dx;
+    dim3 grid((unsigned)(((int64_t)(x->H / k) * (x->W / k) + kThreads - 1) / kThreads), C, x->N);
+    hipLaunchKernelGGL(maxpool_kernel<true>, grid, dim3(kThreads), 0, st, a);
+    return isg_check_launch("maxpool_kernel<bwd>");
+}
+
+int32_t isg_bn_update_running(const isg_bn_update* items, int32_t nitems, isg_stream_t st) {
+    for (int b = 0; b < nitems; b += ISG_LIST_CHUNK) {
+        const int n = nitems - b < ISG_LIST_CHUNK ? nitems - b : ISG_LIST_CHUNK;
+        BnUpdateList l;
+        memcpy(l.it, items + b, sizeof(isg_bn_update) * n);
+        hipLaunchKernelGGL(bn_update_kernel, dim3(n), dim3(128), 0, st, l, n);
+        if (int32_t e = isg_check_launch("bn_update_kernel")) return e;
+    }
+    return 0;
+}
+
+int32_t isg_grad_finalize(const isg_grad_final* items, int32_t nitems, isg_stream_t st) {
+    for (int b = 0; b < nitems; b += ISG_LIST_CHUNK) {
+        const int n = nitems - b < ISG_LIST_CHUNK ? nitems - b : ISG_LIST_CHUNK;
+        GradFinalList l;
+        memcpy(l.it, items + b, sizeof(isg_grad_final) * n);
+        hipLaunchKernelGGL(grad_final_kernel, dim3(n), dim3(128), 0, st, l, n);
+        if (int32_t e = isg_check_launch("grad_final_kernel")) return e;
+    }
+    return 0;
+}
+
+int32_t isg_bce_sigmoid(const float* logits, const float* target, int64_t n, double* loss_acc,
+                        float* dlogits, float grad_scale, isg_stream_t st) {
+    hipLaunchKernelGGL(bce_kernel, dim3(grid_for(n, 1024)), dim3(kThreads), 0, st, logits, target, n,
+                       loss_acc, dlogits, grad_scale);
+    return isg_check_launch("bce_kernel");
+}
+
+int32_t isg_sigmoid_fwd(const float* x, float* y, int64_t n, isg_stream_t st) {
+    hipLaunchKernelGGL(sigmoid_fwd_kernel, dim3(grid_for(n)), dim3(kThreads), 0, st, x, y, n);
+    return isg_check_launch("sigmoid_fwd_kernel");
+}
+
+int32_t isg_sigmoid_bwd(const float* y, const float* dy, float* dx, int64_t n, isg_stream_t st) {
+    hipLaunchKernelGGL(sigmoid_bwd_kernel, dim3(grid_for(n)), dim3(kThreads), 0, st, y, dy, dx, n);
+    return isg_check_launch("sigmoid_bwd_kernel");
+}
+
+int32_t isg_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                 const uint8_t* live, int64_t n, int32_t step, float lr, float beta1, float beta2,
+                 float eps, float weight_decay, isg_stream_t st) {
+    if (step < 1) return isg_set_error(ISG_ERR_INVALID, "adam: step must be >= 1");
+    // scalar math in double exactly like torch's python-side bias corrections
+    const double bc1 = 1.0 - std::pow((double)beta1, (double)step);
+    const double bc2 = 1.0 - std::pow((double)beta2, (double)step);
+    const float neg_step = (float)(-((double)lr / bc1));
+    const float bc2_sqrt = (float)std::sqrt(bc2);
+    hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(kThreads), 0, st, param, grad, exp_avg,
+                       exp_avg_sq, live, n, (float)(1.0 - (double)beta1), beta2,
+                       (float)(1.0 - (double)beta2), bc2_sqrt, neg_step, eps, weight_decay);
+    return isg_check_launch("adam_kernel");
+}
+
+int32_t isg_fill_f64(double* p, int64_t n, double v, isg_stream_t st) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(fill_f64_kernel, dim3(grid_for(n)), dim3(kThreads), 0, st, p, n, v);
+    return isg_check_launch("fill_f64_kernel");
+}
+
+}  // extern "C"

@@ -1,0 +1,733 @@
+"""Static-schedule engine: turns a module's `emit` description into two recorded op
+lists (forward, backward) for the native executor `isg_exec` (include/isg.h).
+
+Why: the reference runs ~300 forward and ~600 backward eager kernels per step, each
+launched from Python (segment.py:44-45 is conv -> bn -> act as three kernels). Here
+a module is traced once per input shape into a list of fused-op records whose
+pointers are symbolic (slot, byte offset); a call replays the list with one ctypes
+call and a fresh pointer table, and the same list can be captured into a HIP graph.
+
+Values flowing between ops are *virtual tensors*: a raw conv output plus the
+BatchNorm/activation its consumer applies on load (Conv.forward, segment.py:44-45),
+possibly several channel segments (torch.cat, segment.py:31, 331, 485, 494).
+Residual-block tails (`out = act(sum terms)`) are the only materialisation points.
+
+Backward is derived op by op in reverse order:
+  * a consumer of a virtual value writes g = dL/d(BN output) through an ACTBWD sink
+    and accumulates the BN-backward statistics; the producer conv then rebuilds
+    dL/dy on load (BN_BWD segment) for its dgrad and wgrad;
+  * a consumer of a materialised value accumulates dL/dvalue (STORE first, then ACCUM);
+  * BN gamma/beta, conv-bias-before-BN and PReLU gradients are finalised from the
+    double-precision statistics in one pass at the end.
+"""
+import ctypes
+import struct
+
+import torch
+import torch.nn as nn
+
+from . import _lib as L
+
+# fixed pointer-table slots
+S_ACT, S_GRAD, S_STATS, S_PGRAD, S_LOSS, S_TARGET = 0, 1, 2, 3, 4, 5
+S_IN = (6, 7)
+S_OUT = (8, 9)
+S_DOUT = (10, 11)
+S_DIN = (12, 13)
+S_TENSOR0 = 16
+
+ALIGN = 64  # elements (256 B) between arena buffers
+
+
+class Ptr:
+    __slots__ = ("slot", "off")
+
+    def __init__(self, slot, off=0):
+        self.slot = slot
+        self.off = off
+
+    def plus(self, nbytes):
+        return Ptr(self.slot, self.off + nbytes)
+
+
+# ---------------------------------------------------------------------------------
+# record building
+def _fill(obj, spec, base, fix):
+    for k, v in spec.items():
+        fld = getattr(type(obj), k)
+        off = base + fld.offset
+        if v is None:
+            continue
+        if isinstance(v, Ptr):
+            fix.append((off, v.slot, v.off))
+        elif isinstance(v, dict):
+            _fill(getattr(obj, k), v, off, fix)
+        elif isinstance(v, (list, tuple)):
+            arr = getattr(obj, k)
+            esz = ctypes.sizeof(arr._type_)
+            for i, e in enumerate(v):
+                if e is None:
+                    continue
+                if isinstance(e, dict):
+                    _fill(arr[i], e, off + i * esz, fix)
+                elif isinstance(e, Ptr):
+                    fix.append((off + i * esz, e.slot, e.off))
+                else:
+                    arr[i] = e
+        else:
+            setattr(obj, k, v)
+
+
+class Record:
+    def __init__(self, kind, cls, spec, items_cls=None, items=None, label="", flops=0, nbytes=0):
+        self.kind = kind
+        self.label = label
+        self.flops = flops    # algorithmic FLOPs of this launch (2*MAC)
+        self.nbytes = nbytes  # algorithmic HBM bytes (each operand read/written once)
+        rec = cls()
+        fix = []
+        _fill(rec, spec, 0, fix)
+        body = bytes(rec)
+        if items_cls is not None:
+            parts = [body]
+            isz = ctypes.sizeof(items_cls)
+            for i, it in enumerate(items):
+                o = items_cls()
+                _fill(o, it, len(body) + i * isz, fix)
+                parts.append(bytes(o))
+            body = b"".join(parts)
+        self.body = body
+        self.fix = fix
+
+    def pack(self):
+        n = len(self.body)
+        pad = (-n) % 8
+        out = [struct.pack("<iiii", self.kind, n, len(self.fix), 0), self.body, b"\0" * pad]
+        out += [struct.pack("<iiq", loc, slot, off) for loc, slot, off in self.fix]
+        return b"".join(out)
+
+
+class OpList:
+    def __init__(self):
+        self.recs = []
+
+    def add(self, rec):
+        self.recs.append(rec)
+
+    def compile(self):
+        self.blob = b"".join(r.pack() for r in self.recs)
+        self._buf = ctypes.create_string_buffer(self.blob, len(self.blob))
+        return self
+
+    def run(self, table, stream):
+        L.check(L.lib().isg_exec(ctypes.addressof(self._buf), len(self.recs), table, stream),
+                "exec")
+
+    def slice(self, i, j):
+        """A compiled sub-list recs[i:j] (to bracket one op with events)."""
+        o = OpList()
+        o.recs = self.recs[i:j]
+        return o.compile()
+
+
+# ---------------------------------------------------------------------------------
+# graph values
+class Buf:
+    """An NCHW fp32 region of an arena (act or grad) or an external slot."""
+
+    def __init__(self, slot, N, C, H, W, name, off=0):
+        self.slot, self.N, self.C, self.H, self.W, self.name = slot, N, C, H, W, name
+        self.off = off  # elements
+
+    @property
+    def n_stride(self):
+        return self.C * self.H * self.W
+
+    @property
+    def numel(self):
+        return self.N * self.C * self.H * self.W
+
+    def ptr(self, c0=0):
+        return Ptr(self.slot, (self.off + c0 * self.H * self.W) * 4)
+
+
+class BNRef:
+    def __init__(self, mod, C, count, stats_off, names):
+        self.mod, self.C, self.count, self.stats_off = mod, C, count, stats_off
+        self.names = names  # dict: gamma, beta, rm, rv, nbt -> tensor slot
+
+
+class SlopeRef:
+    def __init__(self, mod, C, acc_off, slot):
+        self.mod, self.C, self.acc_off, self.slot = mod, C, acc_off, slot
+        self.used_in_bwd = False
+
+
+class Val:
+    """One channel segment: act(BN(buf[c0:c0+C])) (identity when bn is None, act none)."""
+
+    def __init__(self, buf, c0, C, bn=None, act="none", slope=None, grad=True):
+        self.buf, self.c0, self.C = buf, c0, C
+        self.bn, self.act, self.slope = bn, act, slope
+        self.grad = grad
+
+    @property
+    def virtual(self):
+        return self.bn is not None or self.act != "none"
+
+
+class Value:
+    def __init__(self, segs):
+        self.segs = list(segs)
+        assert len({(s.buf.H, s.buf.W) for s in self.segs}) == 1
+        self.H, self.W = self.segs[0].buf.H, self.segs[0].buf.W
+        self.C = sum(s.C for s in self.segs)
+
+    @property
+    def grad(self):
+        return any(s.grad for s in self.segs)
+
+
+def cat(*vals):
+    segs = []
+    for v in vals:
+        segs += v.segs
+    return Value(segs)
+
+
+# ---------------------------------------------------------------------------------
+class Graph:
+    """Forward trace of an engine module at one input shape."""
+
+    def __init__(self, owner, N, train, need_grad):
+        self.owner = owner
+        self.N = N
+        self.train = train
+        self.need_grad = need_grad
+        self.ops = []
+        self.act_bufs = []
+        self.act_size = 0
+        self.stats_size = 0
+        self.bns = []
+        self.slopes = {}
+        self.bn_by_mod = {}
+        names = {}
+        for pre, m in owner.named_modules():
+            names[id(m)] = pre
+        self.mod_names = names
+        self.tensor_names = [k for k, _ in owner.named_parameters()] + \
+                            [k for k, _ in owner.named_buffers()]
+        self.tslot = {k: S_TENSOR0 + i for i, k in enumerate(self.tensor_names)}
+        self.param_names = [k for k, _ in owner.named_parameters()]
+        self.param_shapes = {k: tuple(p.shape) for k, p in owner.named_parameters()}
+        off = 0
+        self.pgrad_off = {}
+        for k, p in owner.named_parameters():
+            self.pgrad_off[k] = off
+            off += p.numel()  # packed: the flat grad buffer in parameter order
+        self.pgrad_size = off
+        self.used_params = set()
+
+    # -- naming ------------------------------------------------------------------------
+    def pname(self, mod, attr):
+        pre = self.mod_names[id(mod)]
+        return f"{pre}.{attr}" if pre else attr
+
+    def tptr(self, mod, attr):
+        return Ptr(self.tslot[self.pname(mod, attr)])
+
+    def gptr(self, mod, attr):
+        k = self.pname(mod, attr)
+        self.used_params.add(k)
+        return Ptr(S_PGRAD, self.pgrad_off[k] * 4)
+
+    # -- allocation ----------------------------------------------------------------------
+    def act_buf(self, C, H, W, name):
+        b = Buf(S_ACT, self.N, C, H, W, name, off=self.act_size)
+        self.act_size += (b.numel + ALIGN - 1) // ALIGN * ALIGN
+        self.act_bufs.append(b)
+        return b
+
+    def stats_alloc(self, ndouble):
+        off = self.stats_size
+        self.stats_size += (ndouble + 7) // 8 * 8
+        return off
+
+    def bn_ref(self, bn, count):
+        if id(bn) in self.bn_by_mod:
+            raise ValueError("a BatchNorm module used twice in one trace is not supported")
+        if not isinstance(bn, nn.BatchNorm2d) or bn.momentum is None or not bn.affine \
+                or not bn.track_running_stats:
+            raise NotImplementedError("BatchNorm2d(affine, momentum, tracked stats) only")
+        ref = BNRef(bn, bn.num_features, count, self.stats_alloc(4 * bn.num_features), {
+            "gamma": self.tptr(bn, "weight"), "beta": self.tptr(bn, "bias"),
+            "rm": self.tptr(bn, "running_mean"), "rv": self.tptr(bn, "running_var"),
+            "nbt": self.tptr(bn, "num_batches_tracked")})
+        ref.gname = (bn, "weight")
+        ref.bname = (bn, "bias")
+        self.bns.append(ref)
+        self.bn_by_mod[id(bn)] = ref
+        return ref
+
+    def slope_ref(self, prelu):
+        if id(prelu) not in self.slopes:
+            C = prelu.weight.numel()
+            self.slopes[id(prelu)] = SlopeRef(prelu, C, self.stats_alloc(C),
+                                              self.tslot[self.pname(prelu, "weight")])
+        return self.slopes[id(prelu)]
+
+    def act_of(self, act_mod):
+        """(kind, SlopeRef|None) for an activation module of the reference."""
+        if act_mod is None or isinstance(act_mod, nn.Identity):
+            return "none", None
+        if isinstance(act_mod, nn.ReLU):
+            return "relu", None
+        if isinstance(act_mod, nn.PReLU):
+            return "prelu", self.slope_ref(act_mod)
+        raise NotImplementedError(f"activation {type(act_mod).__name__} is not on the hot path")
+
+    # -- ops -----------------------------------------------------------------------------
+    def input(self, idx, C, H, W, grad):
+        b = Buf(S_IN[idx], self.N, C, H, W, f"in{idx}")
+        return Value([Val(b, 0, C, grad=grad)])
+
+    def conv(self, conv, x, bn=None, act="none", slope=None, name=""):
+        """nn.Conv2d (dense or depthwise) on value x, optionally followed by BN/act
+        applied lazily by the consumer."""
+        k, s, p, d = conv.kernel_size, conv.stride, conv.padding, conv.dilation
+        if isinstance(p, str):
+            raise NotImplementedError("string padding")
+        H, W = x.H, x.W
+        OH = (H + 2 * p[0] - d[0] * (k[0] - 1) - 1) // s[0] + 1
+        OW = (W + 2 * p[1] - d[1] * (k[1] - 1) - 1) // s[1] + 1
+        if x.C != conv.in_channels:
+            raise RuntimeError(f"{name}: expected {conv.in_channels} input channels, got {x.C}")
+        if conv.groups not in (1, conv.in_channels) or (conv.groups > 1 and
+                                                         conv.in_channels != conv.out_channels):
+            raise NotImplementedError("grouped conv other than depthwise")
+        geom = dict(N=self.N, Ci=conv.in_channels, H=H, W=W, Co=conv.out_channels, OH=OH, OW=OW,
+                    KH=k[0], KW=k[1], SH=s[0], SW=s[1], PH=p[0], PW=p[1], DH=d[0], DW=d[1],
+                    groups=conv.groups)
+        out = self.act_buf(conv.out_channels, OH, OW, name)
+        bnr = self.bn_ref(bn, self.N * OH * OW) if bn is not None else None
+        op = ConvOp(self, "conv", conv, geom, x, out, bnr)
+        self.ops.append(op)
+        return Value([Val(out, 0, conv.out_channels, bnr, act, slope, grad=self.need_grad)])
+
+    def conv_transpose(self, ct, x, bn=None, act="none", slope=None, name=""):
+        k, s, p = ct.kernel_size, ct.stride, ct.padding
+        if ct.groups != 1 or ct.dilation != (1, 1) or any(ct.output_padding):
+            raise NotImplementedError("convT: groups/dilation/output_padding")
+        H, W = x.H, x.W
+        OH = (H - 1) * s[0] - 2 * p[0] + k[0]
+        OW = (W - 1) * s[1] - 2 * p[1] + k[1]
+        geom = dict(N=self.N, Ci=ct.in_channels, H=H, W=W, Co=ct.out_channels, OH=OH, OW=OW,
+                    KH=k[0], KW=k[1], SH=s[0], SW=s[1], PH=p[0], PW=p[1], DH=1, DW=1, groups=1)
+        out = self.act_buf(ct.out_channels, OH, OW, name)
+        bnr = self.bn_ref(bn, self.N * OH * OW) if bn is not None else None
+        op = ConvOp(self, "convT", ct, geom, x, out, bnr)
+        self.ops.append(op)
+        return Value([Val(out, 0, ct.out_channels, bnr, act, slope, grad=self.need_grad)])
+
+    def maxpool(self, x, k, out=None, c0=0, name=""):
+        if x.H % k or x.W % k:
+            raise RuntimeError(f"max_pool{k}: {x.H}x{x.W} not divisible (reference needs "
+                               "H, W multiples of 16, SURVEY.md §0.5)")
+        if out is None:
+            out = self.act_buf(x.C, x.H // k, x.W // k, name)
+        op = PoolOp(self, x, k, out, c0)
+        self.ops.append(op)
+        return Value([Val(out, c0, x.C, grad=x.grad)])
+
+    def tail(self, terms, act="none", slope=None, out=None, c0=0, name=""):
+        """out = act(sum(terms)); terms = [(Value single-seg, up)]; BN'd terms must have
+        act none (the activation of a Conv(act=None), segment.py:42)."""
+        C = terms[0][0].C
+        H, W = terms[0][0].H * (2 if terms[0][1] else 1), terms[0][0].W * (2 if terms[0][1] else 1)
+        for v, up in terms:
+            assert len(v.segs) == 1 and v.C == C
+            assert v.H * (2 if up else 1) == H and v.W * (2 if up else 1) == W, (v.H, v.W, H, W)
+            assert v.segs[0].act == "none"
+        if out is None:
+            out = self.act_buf(C, H, W, name)
+        op = TailOp(self, [(v.segs[0], up) for v, up in terms], act, slope, out, c0)
+        self.ops.append(op)
+        return Value([Val(out, c0, C, grad=any(v.grad for v, _ in terms))])
+
+    def materialize(self, v, out=None, c0=0, name=""):
+        s = v.segs[0]
+        assert len(v.segs) == 1
+        term = Value([Val(s.buf, s.c0, s.C, s.bn, "none", None, s.grad)])
+        return self.tail([(term, False)], s.act, s.slope, out, c0, name)
+
+
+# ---------------------------------------------------------------------------------
+# spec helpers
+def bn_spec(bnr, train):
+    if bnr is None:
+        return {"train": 1}
+    n = bnr.names
+    return {"gamma": n["gamma"], "beta": n["beta"], "running_mean": n["rm"],
+            "running_var": n["rv"], "stats": Ptr(S_STATS, bnr.stats_off * 8), "C": bnr.C,
+            "train": 1 if train else 0, "count": float(bnr.count), "eps": float(bnr.mod.eps)}
+
+
+def fwd_seg(val, train):
+    s = {"p": val.buf.ptr(val.c0), "n_stride": val.buf.n_stride, "C": val.C,
+         "xform": L.XF_BN_FWD if val.virtual else L.XF_PLAIN, "act": L.ACT[val.act]}
+    if val.virtual:
+        s["bn"] = bn_spec(val.bn, train) if val.bn is not None else {"train": 1}
+        if val.slope is not None:
+            s["slope"] = Ptr(val.slope.slot)
+    return s
+
+
+def vtensor(segs, N, H, W):
+    return {"s": segs, "nseg": len(segs), "N": N, "H": H, "W": W}
+
+
+class GradState:
+    """Backward bookkeeping: gradient buffers in the grad arena."""
+
+    def __init__(self, g):
+        self.g = g
+        self.size = 0
+        self.D = {}       # id(buf) -> grad Buf (materialised values / plain raws)
+        self.G = {}       # id(raw buf) -> g Buf (dL/d BN-output of a virtual value)
+        self.inited = {}  # id(buf) -> set of (c0, C)
+        self.external = {}  # id(buf) -> Buf (e.g. dlogits slot)
+
+    def alloc(self, like, name):
+        b = Buf(S_GRAD, like.N, like.C, like.H, like.W, name, off=self.size)
+        self.size += (b.numel + ALIGN - 1) // ALIGN * ALIGN
+        return b
+
+    def dbuf(self, buf):
+        if id(buf) in self.external:
+            return self.external[id(buf)]
+        if id(buf) not in self.D:
+            self.D[id(buf)] = self.alloc(buf, "d_" + buf.name)
+        return self.D[id(buf)]
+
+    def has_grad(self, buf, c0, C):
+        return id(buf) in self.external or (c0, C) in self.inited.get(id(buf), set())
+
+    def mark(self, buf, c0, C):
+        first = (c0, C) not in self.inited.setdefault(id(buf), set())
+        self.inited[id(buf)].add((c0, C))
+        return first
+
+    def sink_for(self, val, c0_glob, train):
+        """Sink that receives dL/d(val) for channels [c0_glob, c0_glob+val.C) of a kernel's
+        output rows."""
+        if not val.grad:
+            return {"c0": c0_glob, "C": val.C, "mode": L.SINK_NONE}
+        if val.virtual:
+            assert id(val.buf) not in self.G, f"virtual value {val.buf.name} consumed twice"
+            gb = self.alloc(val.buf, "g_" + val.buf.name)
+            self.G[id(val.buf)] = gb
+            s = {"p": gb.ptr(val.c0), "n_stride": gb.n_stride, "c0": c0_glob, "C": val.C,
+                 "mode": L.SINK_ACTBWD, "act": L.ACT[val.act],
+                 "y": val.buf.ptr(val.c0), "y_n_stride": val.buf.n_stride,
+                 "bn": bn_spec(val.bn, train) if val.bn is not None else {"train": 1}}
+            if val.slope is not None:
+                s["slope"] = Ptr(val.slope.slot)
+                s["slope_grad"] = Ptr(S_STATS, val.slope.acc_off * 8)
+                val.slope.used_in_bwd = True
+            return s
+        d = self.dbuf(val.buf)
+        first = self.mark(val.buf, val.c0, val.C)
+        return {"p": d.ptr(val.c0), "n_stride": d.n_stride, "c0": c0_glob, "C": val.C,
+                "mode": L.SINK_STORE if first else L.SINK_ACCUM}
+
+    def dy_seg(self, buf, bnr, train):
+        """The gradient w.r.t. a conv's raw output `buf`, as a virtual segment, or None
+        when nothing downstream produced one (the output does not reach the loss)."""
+        if bnr is not None:
+            if id(buf) not in self.G:
+                return None
+            gb = self.G[id(buf)]
+            return {"p": gb.ptr(), "y": buf.ptr(), "n_stride": gb.n_stride,
+                    "y_n_stride": buf.n_stride, "C": buf.C, "xform": L.XF_BN_BWD,
+                    "bn": bn_spec(bnr, train)}
+        if not self.has_grad(buf, 0, buf.C):
+            return None
+        d = self.dbuf(buf)
+        return {"p": d.ptr(), "n_stride": d.n_stride, "C": buf.C, "xform": L.XF_PLAIN}
+
+
+# ---------------------------------------------------------------------------------
+class ConvOp:
+    def __init__(self, g, kind, mod, geom, x, out, bnr):
+        self.g, self.kind, self.mod, self.geom, self.x, self.out, self.bnr = g, kind, mod, geom, x, out, bnr
+
+    def _cost(self):
+        """(flops, bytes of x, bytes of y, bytes of w) — algorithmic, fp32, each read once."""
+        ge = self.geom
+        N = ge["N"]
+        if self.kind == "convT":
+            macs = N * ge["H"] * ge["W"] * ge["Ci"] * ge["Co"] * ge["KH"] * ge["KW"]
+        elif ge["groups"] > 1:
+            macs = N * ge["OH"] * ge["OW"] * ge["Co"] * ge["KH"] * ge["KW"]
+        else:
+            macs = N * ge["OH"] * ge["OW"] * ge["Co"] * ge["Ci"] * ge["KH"] * ge["KW"]
+        xb = 4 * N * ge["Ci"] * ge["H"] * ge["W"]
+        yb = 4 * N * ge["Co"] * ge["OH"] * ge["OW"]
+        wb = 4 * self.mod.weight.numel()
+        return 2 * macs, xb, yb, wb
+
+    def fwd(self, ops):
+        g = self.g
+        segs = [fwd_seg(v, g.train) for v in self.x.segs]
+        sink = {"p": self.out.ptr(), "n_stride": self.out.n_stride, "c0": 0, "C": self.out.C,
+                "mode": L.SINK_STORE}
+        if self.mod.bias is not None:
+            sink["bias"] = g.tptr(self.mod, "bias")
+        if self.bnr is not None and g.train:
+            sink["stats"] = Ptr(S_STATS, self.bnr.stats_off * 8)
+        ge = self.geom
+        rec = {"g": ge, "a": vtensor(segs, g.N, ge["H"], ge["W"]), "w": g.tptr(self.mod, "weight"),
+               "out": {"s": [sink], "nsink": 1}}
+        kind = L.OP_CONVT_FWD if self.kind == "convT" else L.OP_CONV_FWD
+        fl, xb, yb, wb = self._cost()
+        ops.add(Record(kind, L.ConvRec, rec, label=self.out.name, flops=fl, nbytes=xb + yb + wb))
+
+    def bwd(self, ops, gs):
+        g = self.g
+        ge = self.geom
+        dy = gs.dy_seg(self.out, self.bnr, g.train)
+        if dy is None:
+            return
+        fl, xb, yb, wb = self._cost()
+        dyb = yb * (2 if dy["xform"] == L.XF_BN_BWD else 1)  # g and y for BN backward
+        dyv = vtensor([dy], g.N, ge["OH"], ge["OW"])
+        # ---- input gradient
+        if self.x.grad:
+            sinks = []
+            c = 0
+            for v in self.x.segs:
+                sinks.append(gs.sink_for(v, c, g.train))
+                c += v.C
+            sk = {"s": sinks, "nsink": len(sinks)}
+            w = g.tptr(self.mod, "weight")
+            if self.kind == "convT":
+                # dx_T = conv(dy_T, W) with the forward conv's stride/pad/kernel
+                tg = dict(N=g.N, Ci=ge["Co"], H=ge["OH"], W=ge["OW"], Co=ge["Ci"], OH=ge["H"],
+                          OW=ge["W"], KH=ge["KH"], KW=ge["KW"], SH=ge["SH"], SW=ge["SW"],
+                          PH=ge["PH"], PW=ge["PW"], DH=1, DW=1, groups=1)
+                ops.add(Record(L.OP_CONV_FWD, L.ConvRec, {"g": tg, "a": dyv, "w": w, "out": sk},
+                               label="dx_" + self.out.name, flops=fl, nbytes=dyb + xb + wb))
+            else:
+                ops.add(Record(L.OP_CONV_DGRAD, L.ConvRec, {"g": ge, "a": dyv, "w": w, "out": sk},
+                               label="dx_" + self.out.name, flops=fl, nbytes=dyb + xb + wb))
+        # ---- weight / bias gradient
+        xsegs = [fwd_seg(v, g.train) for v in self.x.segs]
+        dw = g.gptr(self.mod, "weight")
+        has_bias = self.mod.bias is not None
+        if self.kind == "convT":
+            tg = dict(N=g.N, Ci=ge["Co"], H=ge["OH"], W=ge["OW"], Co=ge["Ci"], OH=ge["H"],
+                      OW=ge["W"], KH=ge["KH"], KW=ge["KW"], SH=ge["SH"], SW=ge["SW"],
+                      PH=ge["PH"], PW=ge["PW"], DH=1, DW=1, groups=1)
+            ops.add(Record(L.OP_CONV_WGRAD, L.WgradRec,
+                           {"g": tg, "dy": vtensor(xsegs, g.N, ge["H"], ge["W"]), "x": dyv,
+                            "dw": dw}, label="dw_" + self.out.name, flops=fl,
+                           nbytes=dyb + xb + wb))
+            if has_bias and self.bnr is None:
+                gs.bias_sums.append((self.mod, self.out, dy))
+        else:
+            rec = {"g": ge, "dy": dyv, "x": vtensor(xsegs, g.N, ge["H"], ge["W"]), "dw": dw}
+            if has_bias and self.bnr is None:
+                rec["dbias"] = g.gptr(self.mod, "bias")
+            ops.add(Record(L.OP_CONV_WGRAD, L.WgradRec, rec, label="dw_" + self.out.name,
+                           flops=fl, nbytes=dyb + xb + wb))
+        if has_bias and self.bnr is not None:
+            gs.bias_from_bn.append((self.mod, self.bnr))
+
+
+class PoolOp:
+    def __init__(self, g, x, k, out, c0):
+        self.g, self.x, self.k, self.out, self.c0 = g, x, k, out, c0
+
+    def fwd(self, ops):
+        g = self.g
+        segs = [fwd_seg(v, g.train) for v in self.x.segs]
+        ops.add(Record(L.OP_MAXPOOL_FWD, L.PoolRec,
+                       {"x": vtensor(segs, g.N, self.x.H, self.x.W), "k": self.k,
+                        "out": self.out.ptr(self.c0), "out_ns": self.out.n_stride},
+                       label=self.out.name))
+
+    def bwd(self, ops, gs):
+        g = self.g
+        if not self.x.grad or not gs.has_grad(self.out, self.c0, self.x.C):
+            return
+        d = gs.dbuf(self.out)
+        sinks = []
+        c = 0
+        for v in self.x.segs:
+            if v.virtual:
+                raise NotImplementedError("max-pool of a virtual value needs materialisation")
+            sinks.append(gs.sink_for(v, c, g.train))
+            c += v.C
+        segs = [fwd_seg(v, g.train) for v in self.x.segs]
+        ops.add(Record(L.OP_MAXPOOL_BWD, L.PoolRec,
+                       {"x": vtensor(segs, g.N, self.x.H, self.x.W), "k": self.k,
+                        "dout": d.ptr(self.c0), "dout_ns": d.n_stride,
+                        "dx": {"s": sinks, "nsink": len(sinks)}}, label="dx_" + self.out.name))
+
+
+class TailOp:
+    def __init__(self, g, terms, act, slope, out, c0):
+        self.g, self.terms, self.act, self.slope, self.out, self.c0 = g, terms, act, slope, out, c0
+
+    def spec(self):
+        g = self.g
+        C = self.terms[0][0].C
+        t = {"term": [fwd_seg(v, g.train) for v, _ in self.terms],
+             "up": [1 if up else 0 for _, up in self.terms], "nterm": len(self.terms),
+             "act": L.ACT[self.act], "out": self.out.ptr(self.c0),
+             "out_n_stride": self.out.n_stride, "N": g.N, "C": C, "H": self.out.H,
+             "W": self.out.W}
+        if self.slope is not None:
+            t["slope"] = Ptr(self.slope.slot)
+        return t
+
+    def fwd(self, ops):
+        ops.add(Record(L.OP_TAIL_FWD, L.Tail, self.spec(), label=self.out.name))
+
+    def bwd(self, ops, gs):
+        g = self.g
+        C = self.terms[0][0].C
+        if not gs.has_grad(self.out, self.c0, C):
+            return
+        d = gs.dbuf(self.out)
+        rec = {"f": self.spec(), "dout": d.ptr(self.c0), "dout_n_stride": d.n_stride}
+        if self.slope is not None:
+            rec["slope_grad"] = Ptr(S_STATS, self.slope.acc_off * 8)
+            self.slope.used_in_bwd = True
+        if any(v.bn is not None for v, _ in self.terms):
+            gb = gs.alloc(Buf(S_GRAD, g.N, C, self.out.H, self.out.W, "gt"), "gt_" + self.out.name)
+            rec["g"] = gb.ptr()
+            rec["g_n_stride"] = gb.n_stride
+            for v, _ in self.terms:
+                if v.bn is not None:
+                    assert v.c0 == 0 and v.C == v.buf.C
+                    assert id(v.buf) not in gs.G
+                    gs.G[id(v.buf)] = gb
+        dterm, dns, dacc = [None] * 3, [0] * 3, [0] * 3
+        for i, (v, up) in enumerate(self.terms):
+            if v.bn is None and v.grad:
+                db = gs.dbuf(v.buf)
+                first = gs.mark(v.buf, v.c0, v.C)
+                dterm[i] = db.ptr(v.c0)
+                dns[i] = db.n_stride
+                dacc[i] = 0 if first else 1
+        rec["dterm"] = dterm
+        rec["dterm_n_stride"] = dns
+        rec["dterm_accum"] = dacc
+        ops.add(Record(L.OP_TAIL_BWD, L.TailGrad, rec, label="d_" + self.out.name))
+
+
+# ---------------------------------------------------------------------------------
+class Plan:
+    """Compiled forward (+ optional backward) op lists of one module at one shape."""
+
+    def __init__(self, owner, in_shapes, train, need_grad, in_grad):
+        N = in_shapes[0][0]
+        g = Graph(owner, N, train, need_grad)
+        ins = [g.input(i, s[1], s[2], s[3], in_grad[i]) for i, s in enumerate(in_shapes)]
+        outs = owner.emit(g, *ins)
+        if isinstance(outs, Value):
+            outs = (outs,)
+        self.graph = g
+        # outputs: materialise each into its output slot
+        self.out_bufs = []
+        for i, o in enumerate(outs):
+            ob = Buf(S_OUT[i], N, o.C, o.H, o.W, f"out{i}")
+            self._emit_output(g, o, ob)
+            self.out_bufs.append(ob)
+        self.out_shapes = [(N, b.C, b.H, b.W) for b in self.out_bufs]
+        # ---- forward list
+        fw = OpList()
+        if g.stats_size:
+            fw.add(Record(L.OP_MEMSET, L.MemsetRec, {"p": Ptr(S_STATS), "bytes": g.stats_size * 8}))
+        for op in g.ops:
+            op.fwd(fw)
+        if train and g.bns:
+            items = []
+            for b in g.bns:
+                items.append({"stats": Ptr(S_STATS, b.stats_off * 8),
+                              "running_mean": b.names["rm"], "running_var": b.names["rv"],
+                              "num_batches_tracked": b.names["nbt"], "C": b.C,
+                              "count": float(b.count), "momentum": float(b.mod.momentum)})
+            for i in range(0, len(items), L.LIST_CHUNK):
+                chunk = items[i:i + L.LIST_CHUNK]
+                fw.add(Record(L.OP_BN_UPDATE, L.ListRec, {"n": len(chunk)}, L.BnUpdate, chunk))
+        self.fwd = fw.compile()
+        self.act_size = g.act_size
+        self.stats_size = max(g.stats_size, 8)
+        self.bwd = None
+        if need_grad:
+            self._build_backward(g, ins)
+
+    def _emit_output(self, g, o, ob):
+        # route the value into the output slot with a tail (copy / BN+act)
+        c = 0
+        for s in o.segs:
+            term = Value([Val(s.buf, s.c0, s.C, s.bn, "none", None, s.grad)])
+            g.tail([(term, False)], s.act, s.slope, out=ob, c0=c, name=ob.name)
+            c += s.C
+
+    def _build_backward(self, g, ins):
+        gs = GradState(g)
+        gs.bias_sums = []
+        gs.bias_from_bn = []
+        for i, ob in enumerate(self.out_bufs):
+            gs.external[id(ob)] = Buf(S_DOUT[i], ob.N, ob.C, ob.H, ob.W, f"dout{i}")
+        for i, v in enumerate(ins):
+            if v.grad:
+                b = v.segs[0].buf
+                gs.external[id(b)] = Buf(S_DIN[i], b.N, b.C, b.H, b.W, f"din{i}")
+        bw = OpList()
+        bw.add(Record(L.OP_MEMSET, L.MemsetRec, {"p": Ptr(S_PGRAD), "bytes": g.pgrad_size * 4}))
+        body = OpList()
+        for op in reversed(g.ops):
+            op.bwd(body, gs)
+        for r in body.recs:
+            bw.add(r)
+        self.din_written = [v.grad and bool(gs.inited.get(id(v.segs[0].buf)))
+                            for v in ins]
+        # bias of a conv(T) with no BN after it whose wgrad could not produce it
+        # (convT: the wgrad roles are swapped): sum of its output gradient, via the
+        # wgrad kernel's per-row sum with a throw-away 1x1 weight into scratch
+        for mod, out, dy in gs.bias_sums:
+            scratch = g.stats_alloc((out.C * out.C + 1) // 2)
+            ge = dict(N=g.N, Ci=out.C, H=out.H, W=out.W, Co=out.C, OH=out.H, OW=out.W, KH=1,
+                      KW=1, SH=1, SW=1, PH=0, PW=0, DH=1, DW=1, groups=1)
+            bw.add(Record(L.OP_CONV_WGRAD, L.WgradRec,
+                          {"g": ge, "dy": vtensor([dy], g.N, out.H, out.W),
+                           "x": vtensor([dy], g.N, out.H, out.W),
+                           "dw": Ptr(S_STATS, scratch * 8), "dbias": g.gptr(mod, "bias")},
+                          label="db_" + out.name))
+        # finalisation of BN / PReLU / conv-bias-before-BN gradients
+        conv_before = {id(bnr): mod for mod, bnr in gs.bias_from_bn}
+        items = []
+        for b in g.bns:
+            it = {"stats": Ptr(S_STATS, b.stats_off * 8), "gamma": b.names["gamma"],
+                  "running_mean": b.names["rm"], "running_var": b.names["rv"],
+                  "dgamma": g.gptr(b.mod, "weight"), "dbeta": g.gptr(b.mod, "bias"),
+                  "C": b.C, "train": 1 if g.train else 0, "count": float(b.count),
+                  "eps": float(b.mod.eps)}
+            if id(b) in conv_before:
+                it["dconv_bias"] = g.gptr(conv_before[id(b)], "bias")
+            items.append(it)
+        for sl in g.slopes.values():
+            if sl.used_in_bwd:
+                items.append({"slope_acc": Ptr(S_STATS, sl.acc_off * 8),
+                              "dslope": g.gptr(sl.mod, "weight"), "C": sl.C})
+        for i in range(0, len(items), L.LIST_CHUNK):
+            chunk = items[i:i + L.LIST_CHUNK]
+            bw.add(Record(L.OP_GRAD_FINAL, L.ListRec, {"n": len(chunk)}, L.GradFinal, chunk))
+        self.stats_size = max(g.stats_size, 8)
+        self.bwd = bw.compile()
+        self.grad_size = gs.size
+        self.used_params = set(g.used_params)

@@ -1,0 +1,163 @@
+"""Fused training step for the reference train loop (train_instance.py:371-382):
+
+    optimizer.zero_grad(); out = model.train_batch(x, hm); loss = BCELoss(out, mask)
+    loss.backward(); optimizer.step(); loss.item()
+
+One `Trainer.step` runs, on one HIP stream and without torch autograd:
+  forward op list -> fused sigmoid+BCE (loss + dlogits) -> backward op list ->
+  [RCCL all-reduce(avg) of the flat 1.06 MB gradient bucket when world_size > 1] ->
+  multi-tensor Adam over the flat parameter buffer.
+Parameters, gradients and BN running statistics live in flat buffers (module tensors
+are re-bound as views), so the optimizer is one kernel and the gradient exchange is one
+collective. The whole step is capturable into a HIP graph (`capture()`).
+
+Data parallelism: one process per GPU, image-batch sharded, local BN
+statistics per replica, running stats broadcast from rank 0 each step (DDP's
+broadcast_buffers default), gradient mean over ranks.
+"""
+import ctypes
+
+import torch
+import torch.distributed as dist
+
+from . import _lib as L
+from .engine import (S_ACT, S_DOUT, S_GRAD, S_IN, S_OUT, S_PGRAD, S_STATS, S_TENSOR0, Plan)
+
+
+def flatten_module(model, device):
+    """Re-bind every parameter and floating buffer of `model` as a view of one flat
+    buffer (params) / (float buffers); returns (flat_params, flat_bufs, param_index)."""
+    params = [p for _, p in model.named_parameters()]
+    n = sum(p.numel() for p in params)
+    flat = torch.empty(n, dtype=torch.float32, device=device)
+    index = []
+    off = 0
+    with torch.no_grad():
+        for p in params:
+            k = p.numel()
+            flat[off:off + k].copy_(p.detach().reshape(-1))
+            p.data = flat[off:off + k].view_as(p)
+            index.append((off, k))
+            off += k
+    fbufs = [(m, name, b) for m in model.modules() for name, b in m._buffers.items()
+             if b is not None and b.is_floating_point()]
+    nb = sum(b.numel() for _, _, b in fbufs)
+    flatb = torch.empty(max(nb, 1), dtype=torch.float32, device=device)
+    off = 0
+    with torch.no_grad():
+        for m, name, b in fbufs:
+            k = b.numel()
+            flatb[off:off + k].copy_(b.reshape(-1))
+            m._buffers[name] = flatb[off:off + k].view_as(b)
+            off += k
+    for m in model.modules():
+        for name, b in m._buffers.items():
+            if b is not None and not b.is_floating_point():
+                m._buffers[name] = b.to(device)
+    return flat, flatb, index
+
+
+class Trainer:
+    """train_instance.py:294-382 step body on the MI355X (Segment + BCELoss + Adam)."""
+
+    def __init__(self, model, batch, in_shapes, device=None, lr=1e-3, betas=(0.9, 0.999),
+                 eps=1e-8, weight_decay=0.0, process_group=None):
+        self.device = torch.device(device or "cuda")
+        self.model = model.to(self.device).train()
+        self.flat, self.flatb, self.index = flatten_module(self.model, self.device)
+        self.in_shapes = [tuple(s) for s in in_shapes]
+        self.plan = Plan(self.model, self.in_shapes, True, True,
+                         tuple(False for _ in self.in_shapes))
+        g = self.plan.graph
+        self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        dev = self.device
+        self.act = torch.empty(max(self.plan.act_size, 1), dtype=torch.float32, device=dev)
+        self.stats = torch.empty(self.plan.stats_size, dtype=torch.float64, device=dev)
+        self.gradarena = torch.empty(max(self.plan.grad_size, 1), dtype=torch.float32, device=dev)
+        # the plan's packed param-grad layout is exactly the flat buffer's order
+        self.grad_flat = torch.zeros_like(self.flat)
+        self.pgrad = self.grad_flat
+        assert g.pgrad_size == self.flat.numel()
+        self.logits = torch.empty(self.plan.out_shapes[0], dtype=torch.float32, device=dev)
+        self.dlogits = torch.empty_like(self.logits)
+        self.loss_acc = torch.zeros(1, dtype=torch.float64, device=dev)
+        self._pg_views = []
+        for (k, p), (off, n) in zip(self.model.named_parameters(), self.index):
+            self._pg_views.append((g.pgrad_off[k], off, n, k in self.plan.used_params))
+        live = torch.zeros(self.flat.numel(), dtype=torch.uint8)
+        for _, off, n, used in self._pg_views:
+            if used:
+                live[off:off + n] = 1
+        self.live = live.to(dev)
+        self.exp_avg = torch.zeros_like(self.flat)
+        self.exp_avg_sq = torch.zeros_like(self.flat)
+        self.step_count = 0
+        self.inputs = [torch.empty(s, dtype=torch.float32, device=dev) for s in self.in_shapes]
+        self.target = torch.empty(self.plan.out_shapes[0], dtype=torch.float32, device=dev)
+        self.table = self._make_table()
+        self.graph = None
+
+    def _make_table(self):
+        g = self.plan.graph
+        tab = (ctypes.c_void_p * (S_TENSOR0 + len(g.tensor_names)))()
+        tab[S_ACT] = self.act.data_ptr()
+        tab[S_STATS] = self.stats.data_ptr()
+        tab[S_GRAD] = self.gradarena.data_ptr()
+        tab[S_PGRAD] = self.pgrad.data_ptr()
+        for i, x in enumerate(self.inputs):
+            tab[S_IN[i]] = x.data_ptr()
+        tab[S_OUT[0]] = self.logits.data_ptr()
+        tab[S_DOUT[0]] = self.dlogits.data_ptr()
+        tensors = [p for _, p in self.model.named_parameters()] + \
+                  [b for _, b in self.model.named_buffers()]
+        for j, t in enumerate(tensors):
+            tab[S_TENSOR0 + j] = t.data_ptr()
+        return tab
+
+    # ---- the step body -------------------------------------------------------------
+    def _body(self):
+        lib = L.lib()
+        st = L.stream_ptr(self.device)
+        if self.world > 1:
+            dist.broadcast(self.flatb, 0, group=self.pg)
+        self.plan.fwd.run(self.table, st)
+        n = self.logits.numel()
+        L.check(lib.isg_fill_f64(self.loss_acc.data_ptr(), 1, 0.0, st), "fill")
+        L.check(lib.isg_bce_sigmoid(self.logits.data_ptr(), self.target.data_ptr(), n,
+                                    self.loss_acc.data_ptr(), self.dlogits.data_ptr(),
+                                    1.0 / n, st), "bce")
+        self.plan.bwd.run(self.table, st)
+        if self.world > 1:
+            dist.all_reduce(self.grad_flat, op=dist.ReduceOp.AVG, group=self.pg)
+
+    def _adam(self):
+        self.step_count += 1
+        L.check(L.lib().isg_adam(self.flat.data_ptr(), self.grad_flat.data_ptr(),
+                                 self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(),
+                                 self.live.data_ptr(), self.flat.numel(), self.step_count,
+                                 self.lr, self.betas[0], self.betas[1], self.eps, self.wd,
+                                 L.stream_ptr(self.device)), "adam")
+
+    def step(self, x=None, target=None):
+        """One optimisation step. x: list of input tensors (copied into the static input
+        buffers), target: mask. Returns the loss as a device tensor (no host sync)."""
+        if x is not None:
+            for dst, src in zip(self.inputs, x):
+                dst.copy_(src, non_blocking=True)
+        if target is not None:
+            self.target.copy_(target, non_blocking=True)
+        self._body()
+        self._adam()
+        return self.loss_acc / self.logits.numel()
+
+    def loss(self):
+        return (self.loss_acc / self.logits.numel()).item()
+
+    def grads(self):
+        """Per-parameter gradient views of the last step (None for unused parameters)."""
+        out = []
+        for (k, p), (pgo, off, n, used) in zip(self.model.named_parameters(), self._pg_views):
+            out.append(self.grad_flat[off:off + n].view_as(p) if used else None)
+        return out

@@ -1,0 +1,57 @@
+"""Direct C-ABI call helpers for kernel-level GPU tests (real pointers in the structs)."""
+import ctypes
+
+import torch
+
+from instancesegmentation_amd import _lib as L
+from instancesegmentation_amd.engine import _fill
+
+
+def struct(cls, spec):
+    obj = cls()
+    fix = []
+    _fill(obj, spec, 0, fix)
+    assert not fix
+    return obj
+
+
+def ptr(t):
+    return t.data_ptr() if t is not None else None
+
+
+def bn_spec_eval(gamma, beta, rm, rv, eps=1e-5):
+    return {"gamma": ptr(gamma), "beta": ptr(beta), "running_mean": ptr(rm),
+            "running_var": ptr(rv), "C": gamma.numel(), "train": 0, "count": 1.0, "eps": eps}
+
+
+def bn_spec_train(gamma, beta, stats, count, eps=1e-5):
+    return {"gamma": ptr(gamma), "beta": ptr(beta), "stats": ptr(stats), "C": gamma.numel(),
+            "train": 1, "count": float(count), "eps": eps}
+
+
+def vt(segs, N, H, W):
+    return struct(L.VTensor, {"s": segs, "nseg": len(segs), "N": N, "H": H, "W": W})
+
+
+def sinks(lst):
+    return struct(L.Sinks, {"s": lst, "nsink": len(lst)})
+
+
+def geom(**kw):
+    return struct(L.Geom, kw)
+
+
+def stream():
+    return L.stream_ptr()
+
+
+def call(name, *args):
+    fn = getattr(L.lib(), name)
+    conv = []
+    for a in args:
+        if isinstance(a, ctypes.Structure):
+            conv.append(ctypes.byref(a))
+        else:
+            conv.append(a)
+    L.check(fn(*conv), name)
+    torch.cuda.synchronize()

@@ -1,0 +1,406 @@
+"""Kernel-level parity of libisg.so against fp64 CPU references (torch.nn.functional
+semantics, the same ops the oracle uses). Calls go straight through the C-ABI."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from instancesegmentation_amd import _lib as L
+from tests.isg_helpers import bn_spec_eval, bn_spec_train, call, geom, ptr, sinks, stream, vt
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def close(got, ref, tol=2e-5, what=""):
+    got = got.detach().double().cpu()
+    ref = ref.detach().double().cpu()
+    scale = max(ref.abs().max().item(), 1e-3)
+    err = (got - ref).abs().max().item()
+    assert err <= tol * scale + 1e-6, f"{what}: max err {err:.3e} (scale {scale:.3e})"
+
+
+def rnd(*shape, seed=0, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(*shape, generator=g, dtype=torch.float64) * scale)
+
+
+def bn_eval_params(C, seed):
+    g = torch.Generator().manual_seed(seed)
+    gamma = torch.rand(C, generator=g, dtype=torch.float64) + 0.5
+    beta = torch.rand(C, generator=g, dtype=torch.float64) - 0.5
+    rm = torch.rand(C, generator=g, dtype=torch.float64) - 0.5
+    rv = torch.rand(C, generator=g, dtype=torch.float64) + 0.5
+    slope = torch.rand(C, generator=g, dtype=torch.float64) * 0.4
+    return gamma, beta, rm, rv, slope
+
+
+def fwd_xform_ref(x, gamma, beta, rm, rv, slope, act):
+    z = (x - rm[None, :, None, None]) / torch.sqrt(rv[None, :, None, None] + 1e-5) \
+        * gamma[None, :, None, None] + beta[None, :, None, None]
+    if act == "prelu":
+        return torch.where(z > 0, z, z * slope[None, :, None, None])
+    if act == "relu":
+        return z.clamp_min(0)
+    return z
+
+
+def cuda32(t):
+    return t.to(DEV, torch.float32).contiguous()
+
+
+DENSE = [
+    # (Ci, Co, H, W, k, s, p, d)
+    (48, 16, 32, 32, 1, 1, 0, 1),
+    (20, 16, 64, 48, 5, 2, 2, 1),
+    (36, 16, 32, 32, 2, 2, 0, 1),
+    (16, 16, 24, 40, 3, 1, 1, 1),
+    (4, 1, 32, 32, 3, 1, 1, 1),
+    (4, 16, 64, 64, 8, 4, 2, 1),
+    (96, 48, 16, 16, 1, 1, 0, 1),
+    (48, 128, 16, 16, 1, 1, 0, 1),
+    (16, 16, 20, 20, 3, 1, 2, 2),
+]
+
+
+def _geom(N, Ci, Co, H, W, k, s, p, d, groups=1):
+    OH = (H + 2 * p - d * (k - 1) - 1) // s + 1
+    OW = (W + 2 * p - d * (k - 1) - 1) // s + 1
+    return dict(N=N, Ci=Ci, H=H, W=W, Co=Co, OH=OH, OW=OW, KH=k, KW=k, SH=s, SW=s, PH=p, PW=p,
+                DH=d, DW=d, groups=groups), OH, OW
+
+
+@pytest.mark.parametrize("cfg", DENSE)
+def test_conv_fwd_dense(cfg):
+    Ci, Co, H, W, k, s, p, d = cfg
+    N = 2
+    ge, OH, OW = _geom(N, Ci, Co, H, W, k, s, p, d)
+    x = rnd(N, Ci, H, W, seed=1)
+    w = rnd(Co, Ci, k, k, seed=2, scale=(2.0 / (Ci * k * k)) ** 0.5)
+    b = rnd(Co, seed=3, scale=0.1)
+    gamma, beta, rm, rv, slope = bn_eval_params(Ci, 4)
+    # two segments: first half BN+PReLU on load, second half plain
+    c1 = Ci // 2 if Ci > 1 else Ci
+    xt = x.clone()
+    xt[:, :c1] = fwd_xform_ref(x[:, :c1], gamma[:c1], beta[:c1], rm[:c1], rv[:c1], slope[:c1],
+                               "prelu")
+    ref = F.conv2d(xt, w, b, stride=s, padding=p, dilation=d)
+    X = cuda32(x)
+    G = [cuda32(t[:c1]) for t in (gamma, beta, rm, rv, slope)]
+    segs = [{"p": ptr(X), "n_stride": Ci * H * W, "C": c1, "xform": L.XF_BN_FWD,
+             "act": L.ACT["prelu"], "slope": ptr(G[4]), "bn": bn_spec_eval(*G[:4])}]
+    if Ci - c1 > 0:
+        segs.append({"p": X.data_ptr() + c1 * H * W * 4, "n_stride": Ci * H * W, "C": Ci - c1,
+                     "xform": L.XF_PLAIN})
+    Wt, B = cuda32(w), cuda32(b)
+    Y = torch.full((N, Co, OH, OW), float("nan"), device=DEV)
+    stats = torch.zeros(2 * Co, dtype=torch.float64, device=DEV)
+    sk = sinks([{"p": ptr(Y), "n_stride": Co * OH * OW, "c0": 0, "C": Co,
+                 "mode": L.SINK_STORE, "bias": ptr(B), "stats": ptr(stats)}])
+    call("isg_conv_fwd", geom(**ge), vt(segs, N, H, W), ptr(Wt), sk, stream())
+    close(Y, ref, what="conv fwd")
+    close(stats[:Co], ref.sum((0, 2, 3)), what="sum")
+    close(stats[Co:], (ref * ref).sum((0, 2, 3)), what="sumsq")
+
+
+def _bn_train_state(y, g, seed):
+    """stats [sum, sumsq, gsum, gysum] for raw y and BN-output grad g."""
+    C = y.shape[1]
+    gamma, beta, _, _, slope = bn_eval_params(C, seed)
+    stats = torch.cat([y.sum((0, 2, 3)), (y * y).sum((0, 2, 3)), g.sum((0, 2, 3)),
+                       (g * y).sum((0, 2, 3))])
+    return gamma, beta, stats, slope
+
+
+def _bn_bwd_ref(y, g, gamma):
+    M = y.shape[0] * y.shape[2] * y.shape[3]
+    mean = y.mean((0, 2, 3), keepdim=True)
+    var = y.var((0, 2, 3), unbiased=False, keepdim=True)
+    rstd = 1 / torch.sqrt(var + 1e-5)
+    xhat = (y - mean) * rstd
+    gm = g.mean((0, 2, 3), keepdim=True)
+    gxm = (g * xhat).sum((0, 2, 3), keepdim=True) / M
+    return gamma[None, :, None, None] * rstd * (g - gm - xhat * gxm)
+
+
+@pytest.mark.parametrize("cfg", DENSE)
+def test_conv_dgrad_dense(cfg):
+    Ci, Co, H, W, k, s, p, d = cfg
+    N = 2
+    ge, OH, OW = _geom(N, Ci, Co, H, W, k, s, p, d)
+    w = rnd(Co, Ci, k, k, seed=5, scale=0.3)
+    yraw = rnd(N, Co, OH, OW, seed=6) + 0.3
+    gbn = rnd(N, Co, OH, OW, seed=7)
+    gamma, beta, st, _ = _bn_train_state(yraw, gbn, 8)
+    dy = _bn_bwd_ref(yraw, gbn, gamma)
+    ref = torch.nn.grad.conv2d_input((N, Ci, H, W), w, dy, stride=s, padding=p, dilation=d)
+    # sink: ACTBWD with eval BN + PReLU on the input side
+    xin = rnd(N, Ci, H, W, seed=9)
+    ig, ib, irm, irv, islope = bn_eval_params(Ci, 10)
+    z = fwd_xform_ref(xin, ig, ib, irm, irv, islope, "none")
+    gref = torch.where(z > 0, ref, ref * islope[None, :, None, None])
+    sref = torch.where(z > 0, torch.zeros_like(z), z * ref).sum((0, 2, 3))
+    Yr, Gb, GA, BE, ST = cuda32(yraw), cuda32(gbn), cuda32(gamma), cuda32(beta), \
+        st.to(DEV).contiguous()
+    dyseg = {"p": ptr(Gb), "y": ptr(Yr), "n_stride": Co * OH * OW, "y_n_stride": Co * OH * OW,
+             "C": Co, "xform": L.XF_BN_BWD, "bn": bn_spec_train(GA, BE, ST, N * OH * OW)}
+    DX = torch.full((N, Ci, H, W), float("nan"), device=DEV)
+    XI = cuda32(xin)
+    IG = [cuda32(t) for t in (ig, ib, irm, irv, islope)]
+    istats = torch.zeros(4 * Ci, dtype=torch.float64, device=DEV)
+    sgrad = torch.zeros(Ci, dtype=torch.float64, device=DEV)
+    bn_in = bn_spec_eval(*IG[:4])
+    bn_in["stats"] = ptr(istats)
+    sk = sinks([{"p": ptr(DX), "n_stride": Ci * H * W, "c0": 0, "C": Ci, "mode": L.SINK_ACTBWD,
+                 "act": L.ACT["prelu"], "y": ptr(XI), "y_n_stride": Ci * H * W,
+                 "slope": ptr(IG[4]), "slope_grad": ptr(sgrad), "bn": bn_in}])
+    call("isg_conv_dgrad", geom(**ge), vt([dyseg], N, OH, OW), ptr(cuda32(w)), sk, stream())
+    close(DX, gref, what="dgrad g")
+    close(istats[2 * Ci:3 * Ci], gref.sum((0, 2, 3)), what="gsum")
+    close(istats[3 * Ci:], (gref * xin).sum((0, 2, 3)), what="gysum")
+    close(sgrad, sref, what="slope grad")
+
+
+@pytest.mark.parametrize("cfg", DENSE)
+def test_conv_wgrad_dense(cfg):
+    Ci, Co, H, W, k, s, p, d = cfg
+    N = 2
+    ge, OH, OW = _geom(N, Ci, Co, H, W, k, s, p, d)
+    x = rnd(N, Ci, H, W, seed=11)
+    gamma, beta, rm, rv, slope = bn_eval_params(Ci, 12)
+    xt = fwd_xform_ref(x, gamma, beta, rm, rv, slope, "relu")
+    dy = rnd(N, Co, OH, OW, seed=13)
+    ref = torch.nn.grad.conv2d_weight(xt, (Co, Ci, k, k), dy, stride=s, padding=p, dilation=d)
+    X, DY = cuda32(x), cuda32(dy)
+    G = [cuda32(t) for t in (gamma, beta, rm, rv, slope)]
+    xseg = {"p": ptr(X), "n_stride": Ci * H * W, "C": Ci, "xform": L.XF_BN_FWD,
+            "act": L.ACT["relu"], "bn": bn_spec_eval(*G[:4])}
+    dyseg = {"p": ptr(DY), "n_stride": Co * OH * OW, "C": Co, "xform": L.XF_PLAIN}
+    DW = torch.zeros(Co, Ci, k, k, device=DEV)
+    DB = torch.zeros(Co, device=DEV)
+    call("isg_conv_wgrad", geom(**ge), vt([dyseg], N, OH, OW), vt([xseg], N, H, W), ptr(DW),
+         ptr(DB), stream())
+    close(DW, ref, what="wgrad")
+    close(DB, dy.sum((0, 2, 3)), what="dbias")
+
+
+DW_CFG = [  # (C, H, W, kh, kw, ph, pw, d)
+    (16, 32, 32, 3, 3, 1, 1, 1),
+    (48, 16, 24, 3, 3, 2, 2, 2),
+    (48, 16, 16, 3, 3, 4, 4, 4),
+    (48, 16, 16, 5, 1, 2, 0, 1),
+    (48, 16, 16, 1, 5, 0, 2, 1),
+]
+
+
+@pytest.mark.parametrize("cfg", DW_CFG)
+def test_depthwise(cfg):
+    C, H, W, kh, kw, ph, pw, d = cfg
+    N = 2
+    ge = dict(N=N, Ci=C, H=H, W=W, Co=C, OH=H, OW=W, KH=kh, KW=kw, SH=1, SW=1, PH=ph, PW=pw,
+              DH=d, DW=d, groups=C)
+    x = rnd(N, C, H, W, seed=21)
+    w = rnd(C, 1, kh, kw, seed=22, scale=0.4)
+    b = rnd(C, seed=23, scale=0.1)
+    gamma, beta, rm, rv, slope = bn_eval_params(C, 24)
+    xt = fwd_xform_ref(x, gamma, beta, rm, rv, slope, "prelu")
+    ref = F.conv2d(xt, w, b, padding=(ph, pw), dilation=d, groups=C)
+    X, Wt, B = cuda32(x), cuda32(w), cuda32(b)
+    G = [cuda32(t) for t in (gamma, beta, rm, rv, slope)]
+    xseg = {"p": ptr(X), "n_stride": C * H * W, "C": C, "xform": L.XF_BN_FWD,
+            "act": L.ACT["prelu"], "slope": ptr(G[4]), "bn": bn_spec_eval(*G[:4])}
+    Y = torch.full((N, C, H, W), float("nan"), device=DEV)
+    stats = torch.zeros(2 * C, dtype=torch.float64, device=DEV)
+    sk = sinks([{"p": ptr(Y), "n_stride": C * H * W, "c0": 0, "C": C, "mode": L.SINK_STORE,
+                 "bias": ptr(B), "stats": ptr(stats)}])
+    call("isg_conv_fwd", geom(**ge), vt([xseg], N, H, W), ptr(Wt), sk, stream())
+    close(Y, ref, what="dw fwd")
+    close(stats[:C], ref.sum((0, 2, 3)), what="dw sum")
+    # dgrad (plain dy -> plain store)
+    dy = rnd(N, C, H, W, seed=25)
+    dref = torch.nn.grad.conv2d_input((N, C, H, W), w, dy, padding=(ph, pw), dilation=d, groups=C)
+    DY = cuda32(dy)
+    DX = torch.full((N, C, H, W), float("nan"), device=DEV)
+    sk = sinks([{"p": ptr(DX), "n_stride": C * H * W, "c0": 0, "C": C, "mode": L.SINK_STORE}])
+    call("isg_conv_dgrad", geom(**ge),
+         vt([{"p": ptr(DY), "n_stride": C * H * W, "C": C, "xform": L.XF_PLAIN}], N, H, W),
+         ptr(Wt), sk, stream())
+    close(DX, dref, what="dw dgrad")
+    # wgrad
+    wref = torch.nn.grad.conv2d_weight(xt, (C, 1, kh, kw), dy, padding=(ph, pw), dilation=d,
+                                       groups=C)
+    DWt = torch.zeros(C, 1, kh, kw, device=DEV)
+    DB = torch.zeros(C, device=DEV)
+    call("isg_conv_wgrad", geom(**ge),
+         vt([{"p": ptr(DY), "n_stride": C * H * W, "C": C, "xform": L.XF_PLAIN}], N, H, W),
+         vt([xseg], N, H, W), ptr(DWt), ptr(DB), stream())
+    close(DWt, wref, what="dw wgrad")
+    close(DB, dy.sum((0, 2, 3)), what="dw dbias")
+
+
+@pytest.mark.parametrize("cfg", [(16, 16, 2, 16, 16), (4, 4, 2, 32, 24), (16, 4, 4, 16, 16)])
+def test_convT_fwd(cfg):
+    Ci, Co, S, H, W = cfg
+    N = 2
+    K, P = 2 * S, S // 2
+    x = rnd(N, Ci, H, W, seed=31)
+    w = rnd(Ci, Co, K, K, seed=32, scale=0.2)
+    b = rnd(Co, seed=33, scale=0.1)
+    gamma, beta, rm, rv, slope = bn_eval_params(Ci, 34)
+    xt = fwd_xform_ref(x, gamma, beta, rm, rv, slope, "relu")
+    ref = F.conv_transpose2d(xt, w, b, stride=S, padding=P)
+    OH, OW = ref.shape[2], ref.shape[3]
+    X, Wt, B = cuda32(x), cuda32(w), cuda32(b)
+    G = [cuda32(t) for t in (gamma, beta, rm, rv, slope)]
+    xseg = {"p": ptr(X), "n_stride": Ci * H * W, "C": Ci, "xform": L.XF_BN_FWD,
+            "act": L.ACT["relu"], "bn": bn_spec_eval(*G[:4])}
+    Y = torch.full((N, Co, OH, OW), float("nan"), device=DEV)
+    stats = torch.zeros(2 * Co, dtype=torch.float64, device=DEV)
+    sk = sinks([{"p": ptr(Y), "n_stride": Co * OH * OW, "c0": 0, "C": Co, "mode": L.SINK_STORE,
+                 "bias": ptr(B), "stats": ptr(stats)}])
+    ge = dict(N=N, Ci=Ci, H=H, W=W, Co=Co, OH=OH, OW=OW, KH=K, KW=K, SH=S, SW=S, PH=P, PW=P,
+              DH=1, DW=1, groups=1)
+    call("isg_convT_fwd", geom(**ge), vt([xseg], N, H, W), ptr(Wt), sk, stream())
+    close(Y, ref, what="convT")
+    close(stats[:Co], ref.sum((0, 2, 3)), what="convT sum")
+    close(stats[Co:], (ref * ref).sum((0, 2, 3)), what="convT sumsq")
+
+
+@pytest.mark.parametrize("k", [2, 4])
+def test_maxpool(k):
+    N, C, H, W = 2, 6, 16, 24
+    x = rnd(N, C, H, W, seed=41)
+    x[0, 0, 0, :4] = 1.0  # ties: first max wins
+    ref = F.max_pool2d(x, k, k)
+    X = cuda32(x)
+    Y = torch.full((N, C, H // k, W // k), float("nan"), device=DEV)
+    xs = vt([{"p": ptr(X), "n_stride": C * H * W, "C": C, "xform": L.XF_PLAIN}], N, H, W)
+    call("isg_maxpool_fwd", xs, k, ptr(Y), C * (H // k) * (W // k), stream())
+    close(Y, ref, tol=0, what="maxpool")
+    xr = x.clone().requires_grad_(True)
+    dout = rnd(N, C, H // k, W // k, seed=42)
+    F.max_pool2d(xr, k, k).backward(dout)
+    DX = torch.full((N, C, H, W), float("nan"), device=DEV)
+    sk = sinks([{"p": ptr(DX), "n_stride": C * H * W, "c0": 0, "C": C, "mode": L.SINK_STORE}])
+    call("isg_maxpool_bwd", xs, k, ptr(cuda32(dout)), C * (H // k) * (W // k), sk, stream())
+    close(DX, xr.grad, tol=0, what="maxpool bwd")
+
+
+@pytest.mark.parametrize("act", ["prelu", "relu"])
+@pytest.mark.parametrize("up", [False, True])
+def test_tail(act, up):
+    N, C, H, W = 2, 8, 16, 12
+    y = rnd(N, C, H, W, seed=51) + 0.2
+    r = rnd(N, C, H // 2, W // 2, seed=52) if up else rnd(N, C, H, W, seed=52)
+    gamma, beta, st0, slope = _bn_train_state(y, torch.zeros_like(y), 53)
+    mean = y.mean((0, 2, 3), keepdim=True)
+    var = y.var((0, 2, 3), unbiased=False, keepdim=True)
+    bnout = (y - mean) / torch.sqrt(var + 1e-5) * gamma[None, :, None, None] + \
+        beta[None, :, None, None]
+    rr = F.interpolate(r, scale_factor=2, mode="nearest") if up else r
+    pre = bnout + rr
+    out = torch.where(pre > 0, pre, pre * slope[None, :, None, None]) if act == "prelu" \
+        else pre.clamp_min(0)
+    Y, R, GA, BE, SL = cuda32(y), cuda32(r), cuda32(gamma), cuda32(beta), cuda32(slope)
+    ST = st0.to(DEV).contiguous()
+    bnt = bn_spec_train(GA, BE, ST, N * H * W)
+    t = {"term": [{"p": ptr(Y), "n_stride": C * H * W, "C": C, "xform": L.XF_BN_FWD,
+                   "act": 0, "bn": bnt},
+                  {"p": ptr(R), "n_stride": R[0].numel(), "C": C, "xform": L.XF_PLAIN}],
+         "up": [0, 1 if up else 0, 0], "nterm": 2, "act": L.ACT[act], "slope": ptr(SL),
+         "N": N, "C": C, "H": H, "W": W}
+    O = torch.full((N, C, H, W), float("nan"), device=DEV)
+    t["out"] = ptr(O)
+    t["out_n_stride"] = C * H * W
+    from instancesegmentation_amd import _lib as LL
+    from tests.isg_helpers import struct
+    call("isg_tail_fwd", struct(LL.Tail, t), stream())
+    close(O, out, what="tail fwd")
+    # backward
+    dout = rnd(N, C, H, W, seed=54)
+    g = torch.where(pre > 0, dout, dout * slope[None, :, None, None]) if act == "prelu" \
+        else torch.where(pre > 0, dout, torch.zeros_like(dout))
+    dr = F.avg_pool2d(g, 2) * 4 if up else g
+    Gt = torch.full((N, C, H, W), float("nan"), device=DEV)
+    DR = torch.full(tuple(r.shape), float("nan"), device=DEV)
+    sg = torch.zeros(C, dtype=torch.float64, device=DEV)
+    tg = {"f": t, "dout": ptr(cuda32(dout)), "dout_n_stride": C * H * W, "g": ptr(Gt),
+          "g_n_stride": C * H * W, "dterm": [None, ptr(DR), None],
+          "dterm_n_stride": [0, R[0].numel(), 0], "dterm_accum": [0, 0, 0],
+          "slope_grad": ptr(sg)}
+    call("isg_tail_bwd", struct(LL.TailGrad, tg), stream())
+    close(Gt, g, what="tail g")
+    close(DR, dr, what="tail dterm")
+    close(ST[2 * C:3 * C], g.sum((0, 2, 3)), what="tail gsum")
+    close(ST[3 * C:], (g * y).sum((0, 2, 3)), what="tail gysum")
+    if act == "prelu":
+        close(sg, torch.where(pre > 0, torch.zeros_like(pre), pre * dout).sum((0, 2, 3)),
+              what="tail slope")
+
+
+def test_bce_matches_golden(golden_dir):
+    z = np.load(f"{golden_dir}/bce.npz")
+    lg = torch.from_numpy(z["logits"]).to(DEV)
+    tg = torch.from_numpy(z["target"]).to(DEV)
+    n = lg.numel()
+    acc = torch.zeros(1, dtype=torch.float64, device=DEV)
+    dl = torch.empty_like(lg)
+    call("isg_bce_sigmoid", ptr(lg), ptr(tg), n, ptr(acc), ptr(dl), 1.0 / n, stream())
+    assert abs(acc.item() / n - float(z["loss"])) < 1e-6 * max(1, abs(float(z["loss"])))
+    ref = torch.from_numpy(z["dlogits"]).double()
+    got = dl.double().cpu()
+    assert (got - ref).abs().max().item() < 1e-6 * ref.abs().max().item() + 1e-12
+    # saturation semantics: logit 17 with y=0 -> zero gradient
+    sat = (torch.from_numpy(z["logits"]) >= 17) & (torch.from_numpy(z["target"]) == 0)
+    assert torch.all(got[sat] == ref[sat])
+
+
+def test_adam_matches_golden(golden_dir):
+    from tests.golden_util import SegmentFixture
+    fx = SegmentFixture("segment20_n2_128.npz")
+    z = np.load(f"{golden_dir}/adam_segment20.npz")
+    p = torch.cat([torch.as_tensor(fx.params[k], dtype=torch.float32).reshape(-1)
+                   for k in fx.param_names]).to(DEV)
+    g = torch.from_numpy(fx.z["grad32"].copy()).to(DEV)
+    live = torch.ones(p.numel(), dtype=torch.uint8)
+    for i, k in enumerate(fx.param_names):
+        if k in fx.grad_none:
+            live[fx.offsets[i]:fx.offsets[i + 1]] = 0
+    live = live.to(DEV)
+    m = torch.zeros_like(p)
+    v = torch.zeros_like(p)
+    for step, key in ((1, "step1"), (2, "step2")):
+        call("isg_adam", ptr(p), ptr(g), ptr(m), ptr(v), ptr(live), p.numel(), step, 1e-3, 0.9,
+             0.999, 1e-8, 0.0, stream())
+        ref = torch.from_numpy(z[key])
+        err = (p.cpu() - ref).abs().max().item()
+        assert err <= 2e-7, f"adam step {step}: {err}"
+
+
+def test_paste_and_nms_bit_exact():
+    from oracle import maskops_oracle as MO
+    rng = np.random.Generator(np.random.PCG64(5))
+    K, S, H, W = 12, 48, 97, 131
+    prob = rng.uniform(0, 1, (K, S, S)).astype(np.float32)
+    prob = np.where(prob > 0.35, prob, prob * 0.2).astype(np.float32)
+    boxes = []
+    for k in range(K):
+        x0, y0 = rng.integers(-20, W - 10), rng.integers(-20, H - 10)
+        boxes.append([x0, y0, x0 + rng.integers(8, 90), y0 + rng.integers(8, 90)])
+    boxes = np.asarray(boxes, np.int32)
+    ref = MO.paste_masks(prob, boxes, H, W)
+    P = torch.from_numpy(prob).to(DEV)
+    B = torch.from_numpy(boxes).to(DEV)
+    O = torch.empty((K, H, W), dtype=torch.uint8, device=DEV)
+    call("isg_mask_paste", ptr(P), K, S, ptr(B), H, W, ptr(O), stream())
+    assert np.array_equal(O.cpu().numpy(), ref)
+    keep_ref = MO.mask_nms(ref, 0.3)
+    ws = L.lib().isg_mask_nms_workspace(K, H, W)
+    work = torch.empty(ws, dtype=torch.uint8, device=DEV)
+    sc = torch.empty(K, dtype=torch.float32, device=DEV)
+    keep = torch.full((K,), -1, dtype=torch.int32, device=DEV)
+    nk = torch.zeros(1, dtype=torch.int32, device=DEV)
+    call("isg_mask_nms", ptr(O), K, H, W, 0.3, ptr(work), ptr(sc), ptr(keep), ptr(nk), stream())
+    _, _, sref = MO.mask_stats(ref)
+    assert np.array_equal(sc.cpu().numpy(), sref)
+    assert np.array_equal(keep.cpu().numpy()[:nk.item()], keep_ref)

@@ -1,0 +1,129 @@
+"""CPU-only checks: the C-ABI library loads and exports every symbol include/isg.h
+declares, the drop-in module matches the reference's state_dict/parameter layout,
+plans trace, and errors surface as the reference's exception types."""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+import torch
+
+from instancesegmentation_amd import _lib as L
+from instancesegmentation_amd.engine import Plan
+from instancesegmentation_amd.model.segment import Segment
+from oracle import maskops_oracle as MO
+from tests.golden_util import SEGMENT_FIXTURES, SegmentFixture
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    src = open(os.path.join(ROOT, "include", "isg.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:int32_t|int64_t|const char\*)\s+(isg_\w+)\s*\(",
+                                 src, re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = L.lib()  # also verifies every struct layout against isg_record_size
+    out = subprocess.run(["nm", "-D", "--defined-only", L.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r" T (isg_\w+)", out))
+    declared = header_symbols()
+    assert declared, "no declarations parsed"
+    missing = [s for s in declared if s not in exported]
+    assert not missing, missing
+    assert set(declared) <= set(L.SIGNATURES), set(declared) - set(L.SIGNATURES)
+    assert lib.isg_abi_version() == 1
+
+
+def test_library_error_path_without_gpu():
+    # an invalid geometry is rejected before any device work
+    g = L.Geom()
+    rc = L.lib().isg_conv_fwd(g, None, None, None, None)
+    assert rc == -1
+    assert b"geometry" in L.lib().isg_last_error()
+
+
+@pytest.mark.parametrize("name", SEGMENT_FIXTURES)
+def test_state_dict_layout_matches_reference(name):
+    fx = SegmentFixture(name)
+    m = Segment(fx.cin)
+    assert [(k, tuple(v.shape)) for k, v in m.state_dict().items()] == fx.shapes
+    assert [k for k, _ in m.named_parameters()] == fx.param_names
+    m.load_state_dict({k: torch.as_tensor(v).to(m.state_dict()[k].dtype)
+                       for k, v in fx.params.items()})
+
+
+@pytest.mark.parametrize("name", SEGMENT_FIXTURES)
+def test_plan_traces_and_unused_params_match_reference(name):
+    fx = SegmentFixture(name)
+    m = Segment(fx.cin)
+    shapes = [(fx.n, 3, fx.h, fx.w), (fx.n, 17, fx.h, fx.w)] if fx.cin == 20 \
+        else [(fx.n, fx.cin, fx.h, fx.w)]
+    p = Plan(m, shapes, True, True, tuple(False for _ in shapes))
+    unused = [k for k in p.graph.param_names if k not in p.used_params]
+    assert sorted(unused) == sorted(fx.grad_none)
+    assert p.fwd.recs and p.bwd.recs
+
+
+def test_weights_init_matches_reference_rules():
+    torch.manual_seed(0)
+    m = Segment(20)
+    for name, mod in m.named_modules():
+        if isinstance(mod, torch.nn.BatchNorm2d):
+            assert torch.all(mod.weight == 1) and torch.all(mod.bias == 0)
+        if type(mod) is torch.nn.Conv2d and mod.bias is not None:
+            assert torch.all(mod.bias == 0), name
+    # ConvTranspose2d keeps torch default init (not an nn.Conv2d subclass)
+    assert m.bottle6_1.bias.abs().sum() > 0
+
+
+def test_cpu_tensor_raises_runtime_error():
+    m = Segment(3)
+    with pytest.raises(RuntimeError):
+        m(torch.zeros(1, 3, 64, 64))
+
+
+def test_bad_channel_count_raises():
+    m = Segment(3)
+    with pytest.raises(RuntimeError):
+        Plan(m, [(1, 20, 64, 64)], True, True, (False,))
+
+
+def test_non_multiple_of_16_raises():
+    m = Segment(3)
+    with pytest.raises(RuntimeError):
+        Plan(m, [(1, 3, 72, 64)], True, True, (False,))
+
+
+# ---- oracle properties for the build-defined post-process (parity unpinned) ----------
+def test_paste_identity_window_reproduces_probability_truncation():
+    rng = np.random.Generator(np.random.PCG64(1))
+    S = 32
+    prob = rng.uniform(0, 1, (1, S, S)).astype(np.float32)
+    out = MO.paste_masks(prob, np.array([[0, 0, S, S]]), S, S)
+    assert np.array_equal(out[0], (prob[0] * np.float32(255)).astype(np.uint8))
+
+
+def test_paste_outside_window_is_zero():
+    prob = np.ones((1, 8, 8), np.float32)
+    out = MO.paste_masks(prob, np.array([[10, 10, 20, 20]]), 30, 30)
+    assert out[0, :10].sum() == 0 and out[0, :, :10].sum() == 0
+    assert np.all(out[0, 10:20, 10:20] == 255)
+
+
+def test_nms_suppresses_duplicates_and_keeps_disjoint():
+    m = np.zeros((4, 20, 20), np.uint8)
+    m[0, 2:10, 2:10] = 200
+    m[1, 2:10, 2:11] = 180   # near-duplicate of 0, lower score
+    m[2, 12:18, 12:18] = 250  # disjoint
+    m[3] = 0                 # empty mask
+    keep = MO.mask_nms(m, 0.5)
+    assert list(keep) == [2, 0, 3]
+
+
+def test_nms_ties_break_by_index():
+    m = np.zeros((3, 10, 10), np.uint8)
+    m[:, 0:5, 0:5] = 200
+    assert list(MO.mask_nms(m, 0.5)) == [0]
