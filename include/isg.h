@@ -44,9 +44,10 @@ enum { ISG_XF_PLAIN = 0, ISG_XF_BN_FWD = 1, ISG_XF_BN_BWD = 2 };
 enum { ISG_SINK_STORE = 0, ISG_SINK_ACCUM = 1, ISG_SINK_ACTBWD = 2, ISG_SINK_NONE = 3 };
 
 /* One BatchNorm2d layer (segment.py:41 `nn.BatchNorm2d(c2)`; eps 1e-5, momentum 0.1).
- * stats layout: [sum(C) | sumsq(C) | gsum(C) | gysum(C)] in double; sum/sumsq are of
- * the raw (pre-BN, bias included) conv output over N*H*W, gsum/gysum of the gradient
- * w.r.t. the BN output g and of g*y. train=0 uses the running statistics. */
+ * stats layout: [sum(C) | sumsq(C) | gsum(C) | gxsum(C)] in double; sum/sumsq are of
+ * the raw (pre-BN, bias included) conv output over N*H*W, gsum of the gradient g
+ * w.r.t. the BN output and gxsum of g*(y - mean), accumulated centred so the BN
+ * backward never cancels against mean*gsum. train=0 uses the running statistics. */
 typedef struct {
     const float* gamma;
     const float* beta;
@@ -87,7 +88,7 @@ typedef struct {
  *   STORE : p = v + bias; optional BN sum/sumsq into stats   (forward conv outputs)
  *   ACCUM : p += v                                            (gradient of a consumed tensor)
  *   ACTBWD: v is dL/dz for z = act(BN(y)); writes g = v*act'(BN(y)) into p and
- *           accumulates bn.stats gsum/gysum and the PReLU slope gradient. */
+ *           accumulates bn.stats gsum/gxsum and the PReLU slope gradient. */
 typedef struct {
     float* p;
     int64_t n_stride;
@@ -191,7 +192,7 @@ typedef struct {
 int32_t isg_bn_update_running(const isg_bn_update* items, int32_t nitems, isg_stream_t stream);
 
 /* Parameter-gradient finalisation (HOST item array, like isg_bn_update_running):
- *   dgamma = rstd*(gysum - mean*gsum), dbeta = gsum,
+ *   dgamma = rstd*gxsum, dbeta = gsum,
  *   dbias(conv before BN) = sum of rebuilt dy, dslope = double accumulator -> float. */
 typedef struct {
     const double* stats;       /* BN stats (4*C) or NULL */

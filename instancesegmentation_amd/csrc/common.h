@@ -58,9 +58,9 @@ ISG_DEV ChanCoef bwd_coef(const isg_bn& bn, int c) {
     if (bn.train) {
         double inv = 1.0 / (double)bn.count;
         double gs = bn.stats[2 * bn.C + c];
-        double gys = bn.stats[3 * bn.C + c];
+        double gxs = bn.stats[3 * bn.C + c];  // sum g*(y - mean), accumulated centred
         double mg = gs * inv;
-        double mgx = rstd * (gys - mean * gs) * inv;  // mean(g * xhat)
+        double mgx = rstd * gxs * inv;         // mean(g * xhat)
         k.c0 = (float)(gam * rstd);
         k.c1 = (float)(-gam * rstd * rstd * mgx);
         k.c2 = (float)mean;
@@ -170,7 +170,7 @@ ISG_DEV void load_sink_coefs(const isg_sinks& sk, SinkCoef* sc, int tid, int nth
 
 // Per-element sink application. Returns values to be reduced:
 //   STORE : r0 = value (for sum), r1 = value^2
-//   ACTBWD: r0 = g, r1 = g*y, r2 = prelu slope grad contribution
+//   ACTBWD: r0 = g, r1 = g*(y - mean), r2 = prelu slope grad contribution
 struct SinkRed {
     float r0, r1, r2;
 };
@@ -201,7 +201,7 @@ ISG_DEV SinkRed sink_apply(const isg_sink& k, const SinkCoef* sc, int cglob, int
         }
         k.p[off] = g;
         r.r0 = g;
-        r.r1 = g * y;
+        r.r1 = g * (y - f.mean);  // centred: no cancellation against mean*sum(g)
     }
     return r;
 }

@@ -194,119 +194,6 @@ __global__ __launch_bounds__(kThreads) void gemm_conv_kernel(GemmArgs a) {
     }
 }
 
-// ---------------------------------------------------------------------------------
-// Weight gradient: dW[row][col] += sum_p dy[row][p] * x_im2col[col][p]
-//   rows = channels of dy, col = ci*KH*KW + kh*KW + kw, p over the dy plane.
-// Operands are staged through LDS in 32-pixel chunks (pixels are the MFMA K dim,
-// contiguous in memory, so direct fragment loads would be 16-way strided).
-// Row stride 34 floats keeps ds_read_b32 conflict-free for the A/B fragment maps.
-constexpr int kPC = 32;
-constexpr int kLdsStride = kPC + 2;
-
-struct WgArgs {
-    isg_vtensor dy;    // rows
-    isg_vtensor x;     // gathered
-    float* dw;
-    float* dbias;
-    int N, TH, TW;     // dy plane
-    int H, W;          // x plane
-    int R, Ci, KH, KW, SH, SW, PH, PW, DH, DW;
-    int64_t pix_per_block;
-};
-
-template <int RT>
-__global__ __launch_bounds__(kThreads) void wgrad_kernel(WgArgs a) {
-    __shared__ float As[RT * 16][kLdsStride];
-    __shared__ float Bs[64][kLdsStride];
-    __shared__ ChanCoef cdy[ISG_MAX_CH];
-    __shared__ ChanCoef cx[ISG_MAX_CH];
-
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = tid >> 6;
-    const int kk = lane >> 4;
-    const int pl = lane & 15;
-    const int KK = a.KH * a.KW;
-    const int NCOL = a.Ci * KK;
-    const int cb = blockIdx.y * 64;
-
-    load_vt_coefs(a.dy, cdy, tid, kThreads);
-    load_vt_coefs(a.x, cx, tid, kThreads);
-    __syncthreads();
-
-    const int64_t tilePix = (int64_t)a.TH * a.TW;
-    const int64_t P = (int64_t)a.N * tilePix;
-    const int64_t pbeg = (int64_t)blockIdx.x * a.pix_per_block;
-    int64_t pend = pbeg + a.pix_per_block;
-    if (pend > P) pend = P;
-    const int64_t xHW = (int64_t)a.H * a.W;
-
-    f32x4 acc[RT];
-#pragma unroll
-    for (int m = 0; m < RT; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float bsum = 0.f;  // thread tid < R owns dbias[row = tid]
-
-    for (int64_t pc = pbeg; pc < pend; pc += kPC) {
-        // stage dy rows
-        for (int idx = tid; idx < RT * 16 * kPC; idx += kThreads) {
-            const int r = idx / kPC, q = idx - r * kPC;
-            const int64_t p = pc + q;
-            float v = 0.f;
-            if (r < a.R && p < pend) {
-                const int n = (int)(p / tilePix);
-                const int64_t pix = p - (int64_t)n * tilePix;
-                v = vt_load(a.dy, cdy, n, r, tilePix, pix);
-            }
-            As[r][q] = v;
-        }
-        // stage im2col columns [cb, cb+64)
-        for (int idx = tid; idx < 64 * kPC; idx += kThreads) {
-            const int cl = idx / kPC, q = idx - cl * kPC;
-            const int col = cb + cl;
-            const int64_t p = pc + q;
-            float v = 0.f;
-            if (col < NCOL && p < pend) {
-                const int n = (int)(p / tilePix);
-                const int pix = (int)(p - (int64_t)n * tilePix);
-                const int ty = pix / a.TW, tx = pix - ty * a.TW;
-                const int ci = col / KK, t = col - ci * KK;
-                const int kh = t / a.KW, kw = t - kh * a.KW;
-                const int sy = ty * a.SH - a.PH + kh * a.DH;
-                const int sxx = tx * a.SW - a.PW + kw * a.DW;
-                if (sy >= 0 && sy < a.H && sxx >= 0 && sxx < a.W)
-                    v = vt_load(a.x, cx, n, ci, xHW, (int64_t)sy * a.W + sxx);
-            }
-            Bs[cl][q] = v;
-        }
-        __syncthreads();
-        if (a.dbias && blockIdx.y == 0 && tid < a.R) {
-#pragma unroll 8
-            for (int q = 0; q < kPC; ++q) bsum += As[tid][q];
-        }
-#pragma unroll
-        for (int kq = 0; kq < kPC; kq += 4) {
-            const float bv = Bs[wave * 16 + pl][kq + kk];
-#pragma unroll
-            for (int m = 0; m < RT; ++m) {
-                const float av = As[m * 16 + pl][kq + kk];
-                acc[m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[m], 0, 0, 0);
-            }
-        }
-        __syncthreads();
-    }
-    const int col = cb + wave * 16 + pl;
-    if (col < NCOL) {
-#pragma unroll
-        for (int m = 0; m < RT; ++m)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int row = m * 16 + kk * 4 + r;
-                if (row < a.R) atomicAdd(&a.dw[(int64_t)row * NCOL + col], acc[m][r]);
-            }
-    }
-    if (a.dbias && blockIdx.y == 0 && tid < a.R) atomicAdd(&a.dbias[tid], bsum);
-}
-
 int vt_channels(const isg_vtensor* v) {
     int c = 0;
     for (int i = 0; i < v->nseg; ++i) c += v->s[i].C;
@@ -391,42 +278,4 @@ int32_t isg_dense_conv_dgrad(const isg_conv_geom* g, const isg_vtensor* dy, cons
     a.OH = g->OH; a.OW = g->OW;
     int64_t ntiles = ((int64_t)g->N * a.TH * a.TW + 15) / 16;
     return dispatch_gemm(a, dim3(num_blocks_for(ntiles), g->SH * g->SW), st);
-}
-
-int32_t isg_dense_conv_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x,
-                             float* dw, float* dbias, hipStream_t st) {
-    if (vt_channels(dy) != g->Co || vt_channels(x) != g->Ci)
-        return isg_set_error(ISG_ERR_INVALID, "conv wgrad: channel mismatch");
-    WgArgs a{};
-    a.dy = *dy; a.x = *x; a.dw = dw; a.dbias = dbias;
-    a.N = g->N; a.TH = g->OH; a.TW = g->OW; a.H = g->H; a.W = g->W;
-    a.R = g->Co; a.Ci = g->Ci; a.KH = g->KH; a.KW = g->KW; a.SH = g->SH; a.SW = g->SW;
-    a.PH = g->PH; a.PW = g->PW; a.DH = g->DH; a.DW = g->DW;
-    const int ncol = g->Ci * g->KH * g->KW;
-    const int ctiles = (ncol + 63) / 64;
-    const int64_t P = (int64_t)g->N * g->OH * g->OW;
-    int64_t want = 1024 / ctiles;
-    if (want < 1) want = 1;
-    int64_t splits = (P + 2047) / 2048;  // at least 2048 pixels per block
-    if (splits > want) splits = want;
-    if (splits < 1) splits = 1;
-    int64_t ppb = (P + splits - 1) / splits;
-    ppb = (ppb + kPC - 1) / kPC * kPC;
-    splits = (P + ppb - 1) / ppb;
-    a.pix_per_block = ppb;
-    dim3 grid((unsigned)splits, (unsigned)ctiles);
-    if (!dw) return isg_set_error(ISG_ERR_INVALID, "conv wgrad: dw is NULL");
-    const int rt = (g->Co + 15) / 16;
-    switch (rt) {
-        case 1: hipLaunchKernelGGL(wgrad_kernel<1>, grid, dim3(kThreads), 0, st, a); break;
-        case 2: hipLaunchKernelGGL(wgrad_kernel<2>, grid, dim3(kThreads), 0, st, a); break;
-        case 3: hipLaunchKernelGGL(wgrad_kernel<3>, grid, dim3(kThreads), 0, st, a); break;
-        case 4: hipLaunchKernelGGL(wgrad_kernel<4>, grid, dim3(kThreads), 0, st, a); break;
-        case 5: case 6: hipLaunchKernelGGL(wgrad_kernel<6>, grid, dim3(kThreads), 0, st, a); break;
-        case 7: case 8: hipLaunchKernelGGL(wgrad_kernel<8>, grid, dim3(kThreads), 0, st, a); break;
-        case 9: case 10: case 11: case 12:
-            hipLaunchKernelGGL(wgrad_kernel<12>, grid, dim3(kThreads), 0, st, a); break;
-        default: return isg_set_error(ISG_ERR_UNSUPPORTED, "conv wgrad: %d rows > 192", g->Co);
-    }
-    return isg_check_launch("wgrad_kernel");
 }

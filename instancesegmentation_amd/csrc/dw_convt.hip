@@ -93,7 +93,7 @@ ISG_DEV void sink1_apply(const isg_sink& k, const Sink1& f, int cl, int n, int64
         }
         k.p[off] = g;
         red[0] += g;
-        red[1] += g * y;
+        red[1] += g * (y - f.mean);
     }
 }
 

