@@ -188,6 +188,8 @@ ISG_DEV SinkRed sink_apply(const isg_sink& k, const SinkCoef* sc, int cglob, int
         r.r1 = v * v;
     } else if (k.mode == ISG_SINK_ACCUM) {
         k.p[off] += v;
+        r.r0 = v;  // per-channel sums for a bias gradient (when stats is set)
+        r.r1 = v * v;
     } else {
         float y = k.y[(int64_t)n * k.y_n_stride + (int64_t)cl * hw + pix];
         SinkCoef f = sc[cglob];
@@ -222,7 +224,7 @@ ISG_DEV void flush_sink_red(const isg_sinks& sk, const float* red0, const float*
         int s = sink_of(sk, c);
         const isg_sink& k = sk.s[s];
         int cl = c - k.c0;
-        if (k.mode == ISG_SINK_STORE) {
+        if (k.mode == ISG_SINK_STORE || k.mode == ISG_SINK_ACCUM) {
             if (k.stats) {
                 atomicAdd(&k.stats[cl], (double)red0[c]);
                 atomicAdd(&k.stats[k.C + cl], (double)red1[c]);
@@ -239,7 +241,8 @@ ISG_DEV void flush_sink_red(const isg_sinks& sk, const float* red0, const float*
 
 ISG_DEV bool sinks_need_red(const isg_sinks& sk) {
     for (int s = 0; s < sk.nsink; ++s) {
-        if (sk.s[s].mode == ISG_SINK_STORE && sk.s[s].stats) return true;
+        if ((sk.s[s].mode == ISG_SINK_STORE || sk.s[s].mode == ISG_SINK_ACCUM) && sk.s[s].stats)
+            return true;
         if (sk.s[s].mode == ISG_SINK_ACTBWD) return true;
     }
     return false;

@@ -242,9 +242,19 @@ int32_t check_sinks(const isg_sinks* s, int M, const char* what) {
 
 }  // namespace
 
+int32_t isg_halo_conv_fwd(const isg_conv_geom* g, const isg_vtensor* x, const float* w,
+                          const isg_sinks* out, hipStream_t st);
+
 int32_t isg_dense_conv_fwd(const isg_conv_geom* g, const isg_vtensor* x, const float* w,
                            const isg_sinks* out, hipStream_t st) {
     if (vt_channels(x) != g->Ci) return isg_set_error(ISG_ERR_INVALID, "conv fwd: Ci mismatch");
+    if (int32_t e = check_sinks(out, g->Co, "conv fwd")) return e;
+    // narrow outputs with spatial taps: LDS halo-tiled kernel (halo_conv.hip)
+    static const bool halo_off = getenv("ISG_NO_HALO_CONV") != nullptr;
+    if (!halo_off) {
+        const int32_t h = isg_halo_conv_fwd(g, x, w, out, st);
+        if (h != 0) return h < 0 ? h : 0;
+    }
     if (g->Ci * g->KH * g->KW > kKtabMax)
         return isg_set_error(ISG_ERR_UNSUPPORTED, "conv fwd: K=%d > %d", g->Ci * g->KH * g->KW, kKtabMax);
     if (int32_t e = check_sinks(out, g->Co, "conv fwd")) return e;

@@ -81,6 +81,8 @@ ISG_DEV void sink1_apply(const isg_sink& k, const Sink1& f, int cl, int n, int64
         red[1] += v * v;
     } else if (k.mode == ISG_SINK_ACCUM) {
         k.p[off] += v;
+        red[0] += v;
+        red[1] += v * v;
     } else {
         const float y = k.y[(int64_t)n * k.y_n_stride + (int64_t)cl * hw + pix];
         const float z = (y - f.mean) * f.scale + f.beta;
@@ -98,7 +100,7 @@ ISG_DEV void sink1_apply(const isg_sink& k, const Sink1& f, int cl, int n, int64
 }
 
 ISG_DEV void sink1_flush(const isg_sink& k, int cl, const float (&red)[3]) {
-    if (k.mode == ISG_SINK_STORE) {
+    if (k.mode == ISG_SINK_STORE || k.mode == ISG_SINK_ACCUM) {
         if (k.stats) {
             atomicAdd(&k.stats[cl], (double)red[0]);
             atomicAdd(&k.stats[k.C + cl], (double)red[1]);
@@ -113,7 +115,8 @@ ISG_DEV void sink1_flush(const isg_sink& k, int cl, const float (&red)[3]) {
 }
 
 ISG_DEV bool sink1_needs_red(const isg_sink& k) {
-    return (k.mode == ISG_SINK_STORE && k.stats) || k.mode == ISG_SINK_ACTBWD;
+    return ((k.mode == ISG_SINK_STORE || k.mode == ISG_SINK_ACCUM) && k.stats) ||
+           k.mode == ISG_SINK_ACTBWD;
 }
 
 struct DwArgs {

@@ -324,6 +324,10 @@ class Graph:
         geom = dict(N=self.N, Ci=ct.in_channels, H=H, W=W, Co=ct.out_channels, OH=OH, OW=OW,
                     KH=k[0], KW=k[1], SH=s[0], SW=s[1], PH=p[0], PW=p[1], DH=1, DW=1, groups=1)
         out = self.act_buf(ct.out_channels, OH, OW, name)
+        if bn is None and ct.bias is not None:
+            # the wgrad of a convT runs with swapped roles and cannot sum dY per output
+            # channel: consumers' gradient sinks accumulate it here instead
+            out.need_sum = self.stats_alloc(2 * ct.out_channels)
         bnr = self.bn_ref(bn, self.N * OH * OW) if bn is not None else None
         op = ConvOp(self, "convT", ct, geom, x, out, bnr)
         self.ops.append(op)
@@ -437,8 +441,13 @@ class GradState:
             return s
         d = self.dbuf(val.buf)
         first = self.mark(val.buf, val.c0, val.C)
-        return {"p": d.ptr(val.c0), "n_stride": d.n_stride, "c0": c0_glob, "C": val.C,
-                "mode": L.SINK_STORE if first else L.SINK_ACCUM}
+        s = {"p": d.ptr(val.c0), "n_stride": d.n_stride, "c0": c0_glob, "C": val.C,
+             "mode": L.SINK_STORE if first else L.SINK_ACCUM}
+        ns = getattr(val.buf, "need_sum", None)
+        if ns is not None:
+            assert val.c0 == 0 and val.C == val.buf.C
+            s["stats"] = Ptr(S_STATS, ns * 8)
+        return s
 
     def dy_seg(self, buf, bnr, train):
         """The gradient w.r.t. a conv's raw output `buf`, as a virtual segment, or None
@@ -616,6 +625,8 @@ class TailOp:
         dterm, dns, dacc = [None] * 3, [0] * 3, [0] * 3
         for i, (v, up) in enumerate(self.terms):
             if v.bn is None and v.grad:
+                if getattr(v.buf, "need_sum", None) is not None:
+                    raise NotImplementedError("tail term that needs a bias-gradient sum")
                 db = gs.dbuf(v.buf)
                 first = gs.mark(v.buf, v.c0, v.C)
                 dterm[i] = db.ptr(v.c0)
@@ -696,21 +707,14 @@ class Plan:
             bw.add(r)
         self.din_written = [v.grad and bool(gs.inited.get(id(v.segs[0].buf)))
                             for v in ins]
-        # bias of a conv(T) with no BN after it whose wgrad could not produce it
-        # (convT: the wgrad roles are swapped): sum of its output gradient, via the
-        # wgrad kernel's per-row sum with a throw-away 1x1 weight into scratch
-        for mod, out, dy in gs.bias_sums:
-            scratch = g.stats_alloc((out.C * out.C + 1) // 2)
-            ge = dict(N=g.N, Ci=out.C, H=out.H, W=out.W, Co=out.C, OH=out.H, OW=out.W, KH=1,
-                      KW=1, SH=1, SW=1, PH=0, PW=0, DH=1, DW=1, groups=1)
-            bw.add(Record(L.OP_CONV_WGRAD, L.WgradRec,
-                          {"g": ge, "dy": vtensor([dy], g.N, out.H, out.W),
-                           "x": vtensor([dy], g.N, out.H, out.W),
-                           "dw": Ptr(S_STATS, scratch * 8), "dbias": g.gptr(mod, "bias")},
-                          label="db_" + out.name))
         # finalisation of BN / PReLU / conv-bias-before-BN gradients
         conv_before = {id(bnr): mod for mod, bnr in gs.bias_from_bn}
         items = []
+        # bias of a convT with no BN after it (segment.py:435-436): the per-channel sum
+        # of its output gradient, accumulated by the consumers' gradient sinks
+        for mod, out, dy in gs.bias_sums:
+            items.append({"slope_acc": Ptr(S_STATS, out.need_sum * 8),
+                          "dslope": g.gptr(mod, "bias"), "C": out.C})
         for b in g.bns:
             it = {"stats": Ptr(S_STATS, b.stats_off * 8), "gamma": b.names["gamma"],
                   "running_mean": b.names["rm"], "running_var": b.names["rv"],
