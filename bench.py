@@ -36,6 +36,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--profile-ops", default="", help="write per-op timing table to this path")
+    ap.add_argument("--eager", action="store_true", help="no HIP graph capture")
     return ap.parse_args()
 
 
@@ -145,36 +146,21 @@ def main():
                             f"flops={r['flops']} bytes={r['nbytes']}\n")
         best = max(rows, key=lambda r: r["ms"])
         dom = (best["phase"], best["idx"])
+    trainer.step()  # restore a consistent state after the per-op pass
+    torch.cuda.synchronize()
+    # capture the step into HIP graphs; the dominant op gets its own graph so HIP events
+    # bracket it inside every timed step
+    dom_rec = None
+    if dom is not None:
+        ol = trainer.plan.fwd if dom[0] == "fwd" else trainer.plan.bwd
+        dom_rec = ol.recs[dom[1]]
+    if not args.eager:
+        trainer.capture(split=dom)
     for _ in range(args.warmup):
         trainer.step()
     torch.cuda.synchronize()
-
-    # split the dominant op's list so it can be bracketed by events inside the timed loop
-    ev_pairs = []
-    if dom is not None:
-        phase, idx = dom
-        ol = trainer.plan.fwd if phase == "fwd" else trainer.plan.bwd
-        pre, mid, post = ol.slice(0, idx), ol.slice(idx, idx + 1), ol.slice(idx + 1, len(ol.recs))
-        dom_rec = ol.recs[idx]
-        stream = torch.cuda.current_stream()
-
-        def timed_list(table, st, _pre=pre, _mid=mid, _post=post):
-            _pre.run(table, st)
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-            _mid.run(table, st)
-            e1.record(stream)
-            ev_pairs.append((e0, e1))
-            _post.run(table, st)
-
-        class _Wrap:
-            def __init__(self, f):
-                self.run = f
-                self.recs = ol.recs
-        if phase == "fwd":
-            trainer.plan.fwd = _Wrap(timed_list)
-        else:
-            trainer.plan.bwd = _Wrap(timed_list)
+    trainer.events = []
+    ev_pairs = trainer.events
 
     if world > 1:
         dist.barrier()
@@ -193,7 +179,7 @@ def main():
     loss = trainer.loss()
 
     roof = None
-    if ev_pairs:
+    if ev_pairs and dom_rec is not None:
         ms = sum(a.elapsed_time(b) for a, b in ev_pairs) / len(ev_pairs)
         roof = roofline_of(dom_rec, ms)
         roof["kernel"] = f"{dom[0]}:{dom_rec.label}"
@@ -209,7 +195,8 @@ def main():
         "data": "synthetic (seeded image/heatmaps/ellipse masks resident in HBM)",
         "config": {"workload": f"train_instance.py step, Segment({args.cin}), bs{args.batch}/GPU, "
                                f"{args.size}x{args.size}", "global_batch": world * args.batch,
-                   "image_size": args.size, "parallelism": f"dp{world}"},
+                   "image_size": args.size, "parallelism": f"dp{world}",
+                   "execution": "eager" if args.eager else "hip-graph"},
         "roofline": roof, "loss": round(loss, 6),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -228,6 +228,13 @@ int32_t isg_adam(float* param, const float* grad, float* exp_avg, float* exp_avg
                  const uint8_t* live, int64_t n, int32_t step, float lr, float beta1,
                  float beta2, float eps, float weight_decay, isg_stream_t stream);
 
+/* Same update with the step counter in device memory: *step is incremented on the
+ * stream first, then used — the launch sequence can be captured in a HIP graph and
+ * replayed (the host-side form bakes `step` into the kernel arguments). */
+int32_t isg_adam_dev(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                     const uint8_t* live, int64_t n, int32_t* step, float lr, float beta1,
+                     float beta2, float eps, float weight_decay, isg_stream_t stream);
+
 int32_t isg_fill_f64(double* p, int64_t n, double v, isg_stream_t stream);
 
 /* ---- infer post-process (build-defined; infer.py:32-36 is a stub) -------- */

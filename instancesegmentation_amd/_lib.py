@@ -133,6 +133,8 @@ SIGNATURES = {
     "isg_sigmoid_bwd": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
     "isg_adam": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32,
                            c_float, c_float, c_float, c_float, c_float, c_void_p]),
+    "isg_adam_dev": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
+                               c_void_p, c_float, c_float, c_float, c_float, c_float, c_void_p]),
     "isg_fill_f64": (c_int32, [c_void_p, c_int64, c_double, c_void_p]),
     "isg_mask_paste": (c_int32, [c_void_p, c_int32, c_int32, c_void_p, c_int32, c_int32, c_void_p,
                                  c_void_p]),

@@ -244,13 +244,22 @@ int32_t check_sinks(const isg_sinks* s, int M, const char* what) {
 
 int32_t isg_halo_conv_fwd(const isg_conv_geom* g, const isg_vtensor* x, const float* w,
                           const isg_sinks* out, hipStream_t st);
+int32_t isg_pw_gemm(const isg_conv_geom* g, const isg_vtensor* src, const float* w,
+                    const isg_sinks* out, bool dgrad, hipStream_t st);
+
+static bool is_pointwise(const isg_conv_geom* g) {
+    return g->KH == 1 && g->KW == 1 && g->SH == 1 && g->SW == 1 && g->PH == 0 && g->PW == 0 &&
+           g->groups == 1 && g->Ci <= 256 && g->Co <= 256;
+}
 
 int32_t isg_dense_conv_fwd(const isg_conv_geom* g, const isg_vtensor* x, const float* w,
                            const isg_sinks* out, hipStream_t st) {
     if (vt_channels(x) != g->Ci) return isg_set_error(ISG_ERR_INVALID, "conv fwd: Ci mismatch");
     if (int32_t e = check_sinks(out, g->Co, "conv fwd")) return e;
+    static const bool special_off = getenv("ISG_GENERIC_CONV") != nullptr;
+    if (!special_off && is_pointwise(g)) return isg_pw_gemm(g, x, w, out, false, st);
     // narrow outputs with spatial taps: LDS halo-tiled kernel (halo_conv.hip)
-    static const bool halo_off = getenv("ISG_NO_HALO_CONV") != nullptr;
+    static const bool halo_off = special_off || getenv("ISG_NO_HALO_CONV") != nullptr;
     if (!halo_off) {
         const int32_t h = isg_halo_conv_fwd(g, x, w, out, st);
         if (h != 0) return h < 0 ? h : 0;
@@ -273,6 +282,9 @@ int32_t isg_dense_conv_fwd(const isg_conv_geom* g, const isg_vtensor* x, const f
 int32_t isg_dense_conv_dgrad(const isg_conv_geom* g, const isg_vtensor* dy, const float* w,
                              const isg_sinks* dx, hipStream_t st) {
     if (vt_channels(dy) != g->Co) return isg_set_error(ISG_ERR_INVALID, "conv dgrad: Co mismatch");
+    if (int32_t e = check_sinks(dx, g->Ci, "conv dgrad")) return e;
+    static const bool special_off = getenv("ISG_GENERIC_CONV") != nullptr;
+    if (!special_off && is_pointwise(g)) return isg_pw_gemm(g, dy, w, dx, true, st);
     if (g->KH > 16 || g->KW > 16) return isg_set_error(ISG_ERR_UNSUPPORTED, "conv dgrad: kernel > 16");
     const int maxk = g->Co * ((g->KH + g->SH - 1) / g->SH) * ((g->KW + g->SW - 1) / g->SW);
     if (maxk > kKtabMax) return isg_set_error(ISG_ERR_UNSUPPORTED, "conv dgrad: K=%d too large", maxk);

@@ -415,6 +415,39 @@ __global__ void adam_kernel(float* p, const float* g, float* m, float* v, const 
     }
 }
 
+// Graph-replayable form: the 1-based step lives in device memory (incremented by
+// step_inc_kernel earlier in the same stream), bias corrections are formed in double
+// exactly like torch's host-side python floats, then rounded to f32.
+__global__ void adam_dev_kernel(float* p, const float* g, float* m, float* v, const uint8_t* live,
+                                int64_t n, const int32_t* step, float lr, float b1, float b2,
+                                float eps, float wd) {
+#pragma clang fp contract(off)
+    const double st = (double)*step;
+    const double bc1 = 1.0 - pow((double)b1, st);
+    const double bc2 = 1.0 - pow((double)b2, st);
+    const float neg_step = (float)(-((double)lr / bc1));
+    const float bc2_sqrt = (float)sqrt(bc2);
+    const float w1 = (float)(1.0 - (double)b1);
+    const float one_m_b2 = (float)(1.0 - (double)b2);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        if (live && !live[i]) continue;
+        float gi = g[i];
+        const float pi = p[i];
+        if (wd != 0.f) gi = gi + wd * pi;
+        float mi = m[i];
+        mi = mi + w1 * (gi - mi);
+        float vi = v[i] * b2;
+        vi = vi + one_m_b2 * gi * gi;
+        const float denom = sqrtf(vi) / bc2_sqrt + eps;
+        m[i] = mi;
+        v[i] = vi;
+        p[i] = pi + neg_step * mi / denom;
+    }
+}
+
+__global__ void step_inc_kernel(int32_t* c) { *c += 1; }
+
 __global__ void fill_f64_kernel(double* p, int64_t n, double v) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x)
@@ -528,6 +561,15 @@ int32_t isg_adam(float* param, const float* grad, float* exp_avg, float* exp_avg
                        exp_avg_sq, live, n, (float)(1.0 - (double)beta1), beta2,
                        (float)(1.0 - (double)beta2), bc2_sqrt, neg_step, eps, weight_decay);
     return isg_check_launch("adam_kernel");
+}
+
+int32_t isg_adam_dev(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                     const uint8_t* live, int64_t n, int32_t* step, float lr, float beta1,
+                     float beta2, float eps, float weight_decay, isg_stream_t st) {
+    hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, st, step);
+    hipLaunchKernelGGL(adam_dev_kernel, dim3(grid_for(n)), dim3(kThreads), 0, st, param, grad,
+                       exp_avg, exp_avg_sq, live, n, step, lr, beta1, beta2, eps, weight_decay);
+    return isg_check_launch("adam_dev_kernel");
 }
 
 int32_t isg_fill_f64(double* p, int64_t n, double v, isg_stream_t st) {

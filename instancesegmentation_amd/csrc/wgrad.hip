@@ -56,12 +56,19 @@ __global__ __launch_bounds__(kThreads) void wgrad_tiled_kernel(WgArgs a) {
     load_vt_coefs(a.dy, cdy, tid, kThreads);
     load_vt_coefs(a.x, cx, tid, kThreads);
 
-    // per-lane tile descriptors (tile t = wave + 4*i)
+    // per-lane tile descriptors (tile t = wave + 4*i). With fewer than 4 output tiles
+    // (narrow layers) the waves split the 64 pixels of each tile instead (k-split) and
+    // combine their partial sums through LDS before the atomics.
     const int ntile_blk = a.RT * a.CTB;
+    const bool ksplit = ntile_blk < 4;
+    const int ks = ksplit ? 4 / ntile_blk : 1;          // waves per tile
+    const int kpart = ksplit ? wave / ntile_blk : 0;    // this wave's pixel quarter/half
+    const bool kactive = !ksplit || kpart < ks;
+    const int kq_lo = kpart * (kTP / ks), kq_hi = kq_lo + kTP / ks;
     int arow[kMaxTiles], xoff[kMaxTiles];
 #pragma unroll
     for (int i = 0; i < kMaxTiles; ++i) {
-        const int t = wave + 4 * i;
+        const int t = ksplit ? (i == 0 ? wave % ntile_blk : 1 << 20) : wave + 4 * i;
         const int rt = t / a.CTB, ct = t - rt * a.CTB;
         arow[i] = (rt * 16 + pl) * kAStride;
         const int col = c_lo + ct * 16 + pl;
@@ -116,12 +123,13 @@ __global__ __launch_bounds__(kThreads) void wgrad_tiled_kernel(WgArgs a) {
             for (int p = 0; p < kTP; ++p) bsum += rowp[p];
         }
 #pragma unroll 4
-        for (int kq = 0; kq < kTP; kq += 4) {
+        for (int kq = kq_lo; kq < kq_hi; kq += 4) {
+            if (!kactive) break;
             const int p = kq + kk;
             const int poff = (p >> 4) * a.SH * a.HC + (p & 15) * a.SW;
 #pragma unroll
             for (int i = 0; i < kMaxTiles; ++i) {
-                if (wave + 4 * i < ntile_blk) {  // wave-uniform
+                if (ksplit ? i == 0 : wave + 4 * i < ntile_blk) {  // wave-uniform
                     const float av = As[arow[i] + p];
                     const float bv = xoff[i] >= 0 ? Xs[xoff[i] + poff] : 0.f;
                     acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[i], 0, 0, 0);
@@ -130,10 +138,23 @@ __global__ __launch_bounds__(kThreads) void wgrad_tiled_kernel(WgArgs a) {
         }
         __syncthreads();
     }
+    // k-split: waves kpart>0 hand their partial tile to wave (wave % ntile_blk) via LDS
+    if (ksplit) {
+        float* part = smem;  // the staging buffers are free now (loop ended on a barrier)
+        if (kactive && kpart > 0)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) part[((wave - ntile_blk) * 4 + r) * 64 + lane] = acc[0][r];
+        __syncthreads();
+        if (kpart == 0)
+            for (int j = 1; j < ks; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    acc[0][r] += part[((wave + (j - 1) * ntile_blk) * 4 + r) * 64 + lane];
+    }
     // flush: lane holds D[row = rt*16 + kk*4 + r][col = c_lo + ct*16 + pl]
 #pragma unroll
     for (int i = 0; i < kMaxTiles; ++i) {
-        const int t = wave + 4 * i;
+        const int t = ksplit ? (i == 0 && kpart == 0 ? wave : 1 << 20) : wave + 4 * i;
         if (t >= ntile_blk) continue;
         const int rt = t / a.CTB, ct = t - rt * a.CTB;
         const int col = c_lo + ct * 16 + pl;
@@ -190,7 +211,11 @@ int32_t isg_dense_conv_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, cons
     a.tiles_x = (g->OW + kTC - 1) / kTC;
     a.tiles_y = (g->OH + kTR - 1) / kTR;
     a.ntiles = (int64_t)g->N * a.tiles_x * a.tiles_y;
+    // blocks along pixels: enough to fill the chip, but every block adds its partial dW
+    // with f32 atomics — cap the adders per address (contention) and the atomic bytes
     int64_t gx = (2048 + gy - 1) / gy;
+    const int64_t nout = (int64_t)g->Co * ncol;
+    gx = std::min<int64_t>(gx, nout < 1024 ? 128 : 512);
     if (gx > a.ntiles) gx = a.ntiles;
     if (gx < 1) gx = 1;
     a.tiles_per_block = (a.ntiles + gx - 1) / gx;

@@ -94,10 +94,13 @@ class Trainer:
         self.exp_avg = torch.zeros_like(self.flat)
         self.exp_avg_sq = torch.zeros_like(self.flat)
         self.step_count = 0
+        self.step_dev = torch.zeros(1, dtype=torch.int32, device=dev)  # Adam's step, on device
         self.inputs = [torch.empty(s, dtype=torch.float32, device=dev) for s in self.in_shapes]
         self.target = torch.empty(self.plan.out_shapes[0], dtype=torch.float32, device=dev)
         self.table = self._make_table()
-        self.graph = None
+        self.graphs = None
+        self.events = []
+        self.split = None
 
     def _make_table(self):
         g = self.plan.graph
@@ -117,11 +120,10 @@ class Trainer:
         return tab
 
     # ---- the step body -------------------------------------------------------------
-    def _body(self):
+    def _fwd_bwd(self):
+        """forward -> sigmoid+BCE (loss, dlogits) -> backward; HIP work only."""
         lib = L.lib()
         st = L.stream_ptr(self.device)
-        if self.world > 1:
-            dist.broadcast(self.flatb, 0, group=self.pg)
         self.plan.fwd.run(self.table, st)
         n = self.logits.numel()
         L.check(lib.isg_fill_f64(self.loss_acc.data_ptr(), 1, 0.0, st), "fill")
@@ -129,16 +131,87 @@ class Trainer:
                                     self.loss_acc.data_ptr(), self.dlogits.data_ptr(),
                                     1.0 / n, st), "bce")
         self.plan.bwd.run(self.table, st)
-        if self.world > 1:
-            dist.all_reduce(self.grad_flat, op=dist.ReduceOp.AVG, group=self.pg)
 
     def _adam(self):
-        self.step_count += 1
-        L.check(L.lib().isg_adam(self.flat.data_ptr(), self.grad_flat.data_ptr(),
-                                 self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(),
-                                 self.live.data_ptr(), self.flat.numel(), self.step_count,
-                                 self.lr, self.betas[0], self.betas[1], self.eps, self.wd,
-                                 L.stream_ptr(self.device)), "adam")
+        L.check(L.lib().isg_adam_dev(self.flat.data_ptr(), self.grad_flat.data_ptr(),
+                                     self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(),
+                                     self.live.data_ptr(), self.flat.numel(),
+                                     self.step_dev.data_ptr(), self.lr, self.betas[0],
+                                     self.betas[1], self.eps, self.wd,
+                                     L.stream_ptr(self.device)), "adam")
+
+    def _loss(self):
+        lib = L.lib()
+        st = L.stream_ptr(self.device)
+        n = self.logits.numel()
+        L.check(lib.isg_fill_f64(self.loss_acc.data_ptr(), 1, 0.0, st), "fill")
+        L.check(lib.isg_bce_sigmoid(self.logits.data_ptr(), self.target.data_ptr(), n,
+                                    self.loss_acc.data_ptr(), self.dlogits.data_ptr(),
+                                    1.0 / n, st), "bce")
+
+    def _schedule(self, split=None):
+        """The step as a list of units: callables issuing HIP work, or the markers
+        'coll' (eager RCCL all-reduce), 'tic'/'toc' (timing events around one op).
+        split=(phase, idx) isolates op `idx` of the forward/backward list."""
+        def run_list(ol):
+            return lambda: ol.run(self.table, L.stream_ptr(self.device))
+        units = []
+        for phase, ol in (("fwd", self.plan.fwd), ("bwd", self.plan.bwd)):
+            if split and split[0] == phase:
+                i = split[1]
+                if i > 0:
+                    units.append(run_list(ol.slice(0, i)))
+                units += ["tic", run_list(ol.slice(i, i + 1)), "toc"]
+                if i + 1 < len(ol.recs):
+                    units.append(run_list(ol.slice(i + 1, len(ol.recs))))
+            else:
+                units.append(run_list(ol))
+            if phase == "fwd":
+                units.append(self._loss)
+        if self.world > 1:
+            units.append("coll")
+        units.append(self._adam)
+        return units
+
+    def capture(self, split=None):
+        """Record the step into HIP graphs: every run of consecutive HIP units becomes one
+        graph; markers between them stay eager (RCCL collectives, timing events)."""
+        torch.cuda.synchronize(self.device)
+        plan = []
+        cur = []
+        for u in self._schedule(split) + ["end"]:
+            if callable(u):
+                cur.append(u)
+                continue
+            if cur:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    for f in cur:
+                        f()
+                plan.append(g)
+                cur = []
+            if u != "end":
+                plan.append(u)
+        self.graphs = plan
+        self.events = []
+        return self
+
+    def _run(self, units):
+        ev = None
+        for u in units:
+            if isinstance(u, torch.cuda.CUDAGraph):
+                u.replay()
+            elif callable(u):
+                u()
+            elif u == "coll":
+                dist.all_reduce(self.grad_flat, op=dist.ReduceOp.AVG, group=self.pg)
+            elif u == "tic":
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record()
+            elif u == "toc":
+                e1 = torch.cuda.Event(enable_timing=True)
+                e1.record()
+                self.events.append((ev, e1))
 
     def step(self, x=None, target=None):
         """One optimisation step. x: list of input tensors (copied into the static input
@@ -148,8 +221,10 @@ class Trainer:
                 dst.copy_(src, non_blocking=True)
         if target is not None:
             self.target.copy_(target, non_blocking=True)
-        self._body()
-        self._adam()
+        self.step_count += 1
+        if self.world > 1:  # DDP broadcast_buffers: rank 0's BN running stats
+            dist.broadcast(self.flatb, 0, group=self.pg)
+        self._run(self.graphs if self.graphs else self._schedule(self.split))
         return self.loss_acc / self.logits.numel()
 
     def loss(self):
