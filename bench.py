@@ -50,21 +50,28 @@ def setup_dist():
     return world, rank, local
 
 
-def op_timing(trainer, reps=3):
-    """Time every recorded op alone (HIP events on the launch stream)."""
+def op_timing(trainer, reps=20):
+    """Device time of every recorded op alone: the op repeated `reps` times inside one
+    captured HIP graph, bracketed by HIP events (host launch latency excluded)."""
     from instancesegmentation_amd import _lib as L
-    stream = torch.cuda.current_stream()
     rows = []
     for phase, ol in (("fwd", trainer.plan.fwd), ("bwd", trainer.plan.bwd)):
         for i, r in enumerate(ol.recs):
             sub = ol.slice(i, i + 1)
             sub.run(trainer.table, L.stream_ptr())
+            torch.cuda.synchronize()
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                for _ in range(reps):
+                    sub.run(trainer.table, L.stream_ptr())
+            graph.replay()
+            stream = torch.cuda.current_stream()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-            for _ in range(reps):
-                sub.run(trainer.table, L.stream_ptr())
+            graph.replay()
             e1.record(stream)
             e1.synchronize()
+            del graph
             rows.append(dict(phase=phase, idx=i, label=r.label, kind=r.kind,
                              ms=e0.elapsed_time(e1) / reps, flops=r.flops, nbytes=r.nbytes))
     # leave the trainer's arenas consistent: rerun a full fwd/bwd afterwards

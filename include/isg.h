@@ -38,6 +38,12 @@ typedef struct ihipStream_t* isg_stream_t; /* == hipStream_t */
 #define ISG_MAX_SEGS 3
 #define ISG_MAX_CH 512
 #define ISG_LIST_CHUNK 32
+/* Every cross-workgroup accumulator (BN statistics, PReLU slope and bias sums) is kept
+ * in ISG_STAT_REP replicas, each workgroup adding into one chosen by its block index,
+ * so at most (workgroups / ISG_STAT_REP) atomics contend on an address; readers sum the
+ * replicas. An accumulator "of n values" therefore occupies ISG_STAT_REP*n doubles,
+ * replica r at offset r*n. */
+#define ISG_STAT_REP 16
 
 enum { ISG_ACT_NONE = 0, ISG_ACT_RELU = 1, ISG_ACT_PRELU = 2 };
 enum { ISG_XF_PLAIN = 0, ISG_XF_BN_FWD = 1, ISG_XF_BN_BWD = 2 };
@@ -47,7 +53,8 @@ enum { ISG_SINK_STORE = 0, ISG_SINK_ACCUM = 1, ISG_SINK_ACTBWD = 2, ISG_SINK_NON
  * stats layout: [sum(C) | sumsq(C) | gsum(C) | gxsum(C)] in double; sum/sumsq are of
  * the raw (pre-BN, bias included) conv output over N*H*W, gsum of the gradient g
  * w.r.t. the BN output and gxsum of g*(y - mean), accumulated centred so the BN
- * backward never cancels against mean*gsum. train=0 uses the running statistics. */
+ * backward never cancels against mean*gsum. train=0 uses the running statistics.
+ * The 4*C block is replicated ISG_STAT_REP times (4*C*ISG_STAT_REP doubles). */
 typedef struct {
     const float* gamma;
     const float* beta;
@@ -96,11 +103,12 @@ typedef struct {
     int32_t mode;
     int32_t act;
     const float* bias;
-    double* stats;         /* STORE: 2*C doubles (sum, sumsq) or NULL */
+    double* stats;         /* STORE/ACCUM: a BN-layout block (4*C per replica) whose
+                              sum/sumsq halves receive the output sums, or NULL */
     const float* y;        /* ACTBWD */
     int64_t y_n_stride;
     const float* slope;    /* ACTBWD + PRELU */
-    double* slope_grad;    /* ACTBWD + PRELU, C doubles */
+    double* slope_grad;    /* ACTBWD + PRELU, C doubles per replica */
     isg_bn bn;             /* ACTBWD; bn.stats==NULL means "no BN" (identity) */
 } isg_sink;
 
@@ -195,7 +203,7 @@ int32_t isg_bn_update_running(const isg_bn_update* items, int32_t nitems, isg_st
  *   dgamma = rstd*gxsum, dbeta = gsum,
  *   dbias(conv before BN) = sum of rebuilt dy, dslope = double accumulator -> float. */
 typedef struct {
-    const double* stats;       /* BN stats (4*C) or NULL */
+    const double* stats;       /* BN stats (4*C per replica) or NULL */
     const float* gamma;
     const float* running_mean; /* eval-mode backward */
     const float* running_var;
@@ -208,6 +216,9 @@ typedef struct {
     int32_t train;
     float count;
     float eps;
+    int32_t slope_stride;      /* replica stride of slope_acc in doubles: C for a PReLU
+                                  slope, 4*C for the sum half of a sink's stats block */
+    int32_t pad_;
 } isg_grad_final;
 int32_t isg_grad_finalize(const isg_grad_final* items, int32_t nitems, isg_stream_t stream);
 
@@ -272,6 +283,8 @@ int32_t isg_record_size(int32_t which);
 
 const char* isg_last_error(void);
 int32_t isg_abi_version(void);
+/* ISG_STAT_REP the library was built with (accumulator replica count). */
+int32_t isg_stat_replicas(void);
 
 #ifdef __cplusplus
 }

@@ -18,6 +18,8 @@ XF_PLAIN, XF_BN_FWD, XF_BN_BWD = 0, 1, 2
 SINK_STORE, SINK_ACCUM, SINK_ACTBWD, SINK_NONE = 0, 1, 2, 3
 MAX_SEGS = 3
 LIST_CHUNK = 32
+STAT_REP = 16     # ISG_STAT_REP: accumulator replicas (isg.h)
+ABI_VERSION = 2
 
 
 class Bn(Structure):
@@ -76,7 +78,8 @@ class GradFinal(Structure):
     _fields_ = [("stats", c_void_p), ("gamma", c_void_p), ("running_mean", c_void_p),
                 ("running_var", c_void_p), ("dgamma", c_void_p), ("dbeta", c_void_p),
                 ("dconv_bias", c_void_p), ("slope_acc", c_void_p), ("dslope", c_void_p),
-                ("C", c_int32), ("train", c_int32), ("count", c_float), ("eps", c_float)]
+                ("C", c_int32), ("train", c_int32), ("count", c_float), ("eps", c_float),
+                ("slope_stride", c_int32), ("pad_", c_int32)]
 
 
 # executor records (api.cpp)
@@ -144,6 +147,7 @@ SIGNATURES = {
     "isg_exec": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p]),
     "isg_last_error": (c_char_p, []),
     "isg_abi_version": (c_int32, []),
+    "isg_stat_replicas": (c_int32, []),
     "isg_record_size": (c_int32, [c_int32]),
 }
 
@@ -163,6 +167,10 @@ def lib():
             fn = getattr(h, name)
             fn.restype = res
             fn.argtypes = args
+        if h.isg_abi_version() != ABI_VERSION or h.isg_stat_replicas() != STAT_REP:
+            raise RuntimeError(f"ABI mismatch: libisg.so is version {h.isg_abi_version()} "
+                               f"with {h.isg_stat_replicas()} stat replicas, expected "
+                               f"{ABI_VERSION} / {STAT_REP}; rebuild it")
         for which, cls in _RECORD_CHECK:
             n = h.isg_record_size(which)
             if n != ctypes.sizeof(cls):

@@ -24,11 +24,26 @@ struct ChanCoef {
     float c0, c1, c2, c3;
 };
 
+// ---- replicated accumulators (ISG_STAT_REP copies, include/isg.h) ---------------------
+// replica chosen by the workgroup; spreads same-address atomics over the copies
+ISG_DEV int rep_of_block() {
+    return (int)((blockIdx.x + 7u * blockIdx.y + 13u * blockIdx.z) % ISG_STAT_REP);
+}
+// pointer to this workgroup's replica of an accumulator of n values
+ISG_DEV double* rep_ptr(double* base, int n) { return base + (int64_t)rep_of_block() * n; }
+// sum over replicas of element i of an accumulator of n values
+ISG_DEV double rep_sum(const double* base, int n, int i) {
+    double s = 0.0;
+#pragma unroll
+    for (int r = 0; r < ISG_STAT_REP; ++r) s += base[(int64_t)r * n + i];
+    return s;
+}
+
 ISG_DEV void bn_mean_rstd(const isg_bn& bn, int c, double& mean, double& rstd) {
     if (bn.train) {
         double inv = 1.0 / (double)bn.count;
-        mean = bn.stats[c] * inv;
-        double var = bn.stats[bn.C + c] * inv - mean * mean;
+        mean = rep_sum(bn.stats, 4 * bn.C, c) * inv;
+        double var = rep_sum(bn.stats, 4 * bn.C, bn.C + c) * inv - mean * mean;
         if (var < 0.0) var = 0.0;
         rstd = 1.0 / sqrt(var + (double)bn.eps);
     } else {
@@ -57,8 +72,8 @@ ISG_DEV ChanCoef bwd_coef(const isg_bn& bn, int c) {
     ChanCoef k;
     if (bn.train) {
         double inv = 1.0 / (double)bn.count;
-        double gs = bn.stats[2 * bn.C + c];
-        double gxs = bn.stats[3 * bn.C + c];  // sum g*(y - mean), accumulated centred
+        double gs = rep_sum(bn.stats, 4 * bn.C, 2 * bn.C + c);
+        double gxs = rep_sum(bn.stats, 4 * bn.C, 3 * bn.C + c);  // sum g*(y - mean), centred
         double mg = gs * inv;
         double mgx = rstd * gxs * inv;         // mean(g * xhat)
         k.c0 = (float)(gam * rstd);
@@ -226,15 +241,18 @@ ISG_DEV void flush_sink_red(const isg_sinks& sk, const float* red0, const float*
         int cl = c - k.c0;
         if (k.mode == ISG_SINK_STORE || k.mode == ISG_SINK_ACCUM) {
             if (k.stats) {
-                atomicAdd(&k.stats[cl], (double)red0[c]);
-                atomicAdd(&k.stats[k.C + cl], (double)red1[c]);
+                double* st = rep_ptr(k.stats, 4 * k.C);
+                atomicAdd(&st[cl], (double)red0[c]);
+                atomicAdd(&st[k.C + cl], (double)red1[c]);
             }
         } else if (k.mode == ISG_SINK_ACTBWD) {
             if (k.bn.stats) {
-                atomicAdd(&k.bn.stats[2 * k.C + cl], (double)red0[c]);
-                atomicAdd(&k.bn.stats[3 * k.C + cl], (double)red1[c]);
+                double* st = rep_ptr(k.bn.stats, 4 * k.C);
+                atomicAdd(&st[2 * k.C + cl], (double)red0[c]);
+                atomicAdd(&st[3 * k.C + cl], (double)red1[c]);
             }
-            if (k.slope_grad && k.act == ISG_ACT_PRELU) atomicAdd(&k.slope_grad[cl], (double)red2[c]);
+            if (k.slope_grad && k.act == ISG_ACT_PRELU)
+                atomicAdd(&rep_ptr(k.slope_grad, k.C)[cl], (double)red2[c]);
         }
     }
 }

@@ -102,15 +102,18 @@ ISG_DEV void sink1_apply(const isg_sink& k, const Sink1& f, int cl, int n, int64
 ISG_DEV void sink1_flush(const isg_sink& k, int cl, const float (&red)[3]) {
     if (k.mode == ISG_SINK_STORE || k.mode == ISG_SINK_ACCUM) {
         if (k.stats) {
-            atomicAdd(&k.stats[cl], (double)red[0]);
-            atomicAdd(&k.stats[k.C + cl], (double)red[1]);
+            double* sp = rep_ptr(k.stats, 4 * k.C);
+            atomicAdd(&sp[cl], (double)red[0]);
+            atomicAdd(&sp[k.C + cl], (double)red[1]);
         }
     } else if (k.mode == ISG_SINK_ACTBWD) {
         if (k.bn.stats) {
-            atomicAdd(&k.bn.stats[2 * k.C + cl], (double)red[0]);
-            atomicAdd(&k.bn.stats[3 * k.C + cl], (double)red[1]);
+            double* sp = rep_ptr(k.bn.stats, 4 * k.C);
+            atomicAdd(&sp[2 * k.C + cl], (double)red[0]);
+            atomicAdd(&sp[3 * k.C + cl], (double)red[1]);
         }
-        if (k.slope_grad && k.act == ISG_ACT_PRELU) atomicAdd(&k.slope_grad[cl], (double)red[2]);
+        if (k.slope_grad && k.act == ISG_ACT_PRELU)
+            atomicAdd(&rep_ptr(k.slope_grad, k.C)[cl], (double)red[2]);
     }
 }
 
@@ -317,8 +320,9 @@ __global__ __launch_bounds__(kThreads) void convT_kernel(CtArgs a) {
             const int co = threadIdx.x;
             const float t0 = sh[co][0][0] + sh[co][0][1] + sh[co][0][2] + sh[co][0][3];
             const float t1 = sh[co][1][0] + sh[co][1][1] + sh[co][1][2] + sh[co][1][3];
-            atomicAdd(&o.stats[co], (double)t0);
-            atomicAdd(&o.stats[o.C + co], (double)t1);
+            double* sp = rep_ptr(o.stats, 4 * o.C);
+            atomicAdd(&sp[co], (double)t0);
+            atomicAdd(&sp[o.C + co], (double)t1);
         }
     }
 }

@@ -211,11 +211,13 @@ __global__ __launch_bounds__(kThreads) void tail_bwd_kernel(isg_tail_grad tg) {
         for (int i = 0; i < t.nterm; ++i) {
             const isg_vseg& tm = t.term[i];
             if (tm.xform == ISG_XF_BN_FWD && tm.bn.stats) {
-                atomicAdd(&tm.bn.stats[2 * tm.bn.C + c], (double)rv[i]);
-                atomicAdd(&tm.bn.stats[3 * tm.bn.C + c], (double)rv[3 + i]);
+                double* sp = rep_ptr(tm.bn.stats, 4 * tm.bn.C);
+                atomicAdd(&sp[2 * tm.bn.C + c], (double)rv[i]);
+                atomicAdd(&sp[3 * tm.bn.C + c], (double)rv[3 + i]);
             }
         }
-        if (t.act == ISG_ACT_PRELU && tg.slope_grad) atomicAdd(&tg.slope_grad[c], (double)rv[6]);
+        if (t.act == ISG_ACT_PRELU && tg.slope_grad)
+            atomicAdd(&rep_ptr(tg.slope_grad, t.C)[c], (double)rv[6]);
     }
 }
 
@@ -291,8 +293,8 @@ __global__ void bn_update_kernel(BnUpdateList items, int nitems) {
     const isg_bn_update& u = items.it[it];
     for (int c = threadIdx.x; c < u.C; c += blockDim.x) {
         const double M = (double)u.count;
-        const double mean = u.stats[c] / M;
-        double var = u.stats[u.C + c] / M - mean * mean;
+        const double mean = rep_sum(u.stats, 4 * u.C, c) / M;
+        double var = rep_sum(u.stats, 4 * u.C, u.C + c) / M - mean * mean;
         if (var < 0.0) var = 0.0;
         const double unb = M > 1.0 ? var * M / (M - 1.0) : var;
         const float m = u.momentum;
@@ -308,22 +310,22 @@ __global__ void grad_final_kernel(GradFinalList items, int nitems) {
     const isg_grad_final& f = items.it[it];
     for (int c = threadIdx.x; c < f.C; c += blockDim.x) {
         if (f.slope_acc) {
-            f.dslope[c] = (float)f.slope_acc[c];
+            f.dslope[c] = (float)rep_sum(f.slope_acc, f.slope_stride, c);
             continue;
         }
         const double M = (double)f.count;
         double mean, rstd;
         if (f.train) {
-            mean = f.stats[c] / M;
-            double var = f.stats[f.C + c] / M - mean * mean;
+            mean = rep_sum(f.stats, 4 * f.C, c) / M;
+            double var = rep_sum(f.stats, 4 * f.C, f.C + c) / M - mean * mean;
             if (var < 0.0) var = 0.0;
             rstd = 1.0 / sqrt(var + (double)f.eps);
         } else {
             mean = (double)f.running_mean[c];
             rstd = 1.0 / sqrt((double)f.running_var[c] + (double)f.eps);
         }
-        const double gs = f.stats[2 * f.C + c];
-        const double gxs = f.stats[3 * f.C + c];  // sum g*(y - mean), centred
+        const double gs = rep_sum(f.stats, 4 * f.C, 2 * f.C + c);
+        const double gxs = rep_sum(f.stats, 4 * f.C, 3 * f.C + c);  // sum g*(y - mean), centred
         const double dgamma = rstd * gxs;
         if (f.dgamma) f.dgamma[c] = (float)dgamma;
         if (f.dbeta) f.dbeta[c] = (float)gs;
@@ -332,7 +334,7 @@ __global__ void grad_final_kernel(GradFinalList items, int nitems) {
             const double gam = (double)f.gamma[c];
             double db;
             if (f.train) {
-                const double sy = f.stats[c];
+                const double sy = rep_sum(f.stats, 4 * f.C, c);
                 const double mg = gs / M, mgx = rstd * gxs / M;
                 db = gam * rstd * (gs - M * mg) - gam * rstd * rstd * mgx * (sy - M * mean);
             } else {

@@ -167,9 +167,10 @@ __global__ __launch_bounds__(kThreads) void halo_conv_kernel(HaloArgs a) {
                 }
             }
         __syncthreads();
+        double* sp = rep_ptr(o.stats, 4 * o.C);
         for (int co = tid; co < a.Co; co += kThreads) {
-            atomicAdd(&o.stats[co], (double)red[0][co]);
-            atomicAdd(&o.stats[o.C + co], (double)red[1][co]);
+            atomicAdd(&sp[co], (double)red[0][co]);
+            atomicAdd(&sp[o.C + co], (double)red[1][co]);
         }
     }
 }

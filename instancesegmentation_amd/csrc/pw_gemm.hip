@@ -212,16 +212,18 @@ __global__ __launch_bounds__(kThreads) void pw_kernel(PwArgs a) {
             const int cl = m - k.c0;
             if (k.mode == ISG_SINK_STORE || k.mode == ISG_SINK_ACCUM) {
                 if (k.stats) {
-                    atomicAdd(&k.stats[cl], (double)red[0][rl]);
-                    atomicAdd(&k.stats[k.C + cl], (double)red[1][rl]);
+                    double* sp = rep_ptr(k.stats, 4 * k.C);
+                    atomicAdd(&sp[cl], (double)red[0][rl]);
+                    atomicAdd(&sp[k.C + cl], (double)red[1][rl]);
                 }
             } else if (k.mode == ISG_SINK_ACTBWD) {
                 if (k.bn.stats) {
-                    atomicAdd(&k.bn.stats[2 * k.C + cl], (double)red[0][rl]);
-                    atomicAdd(&k.bn.stats[3 * k.C + cl], (double)red[1][rl]);
+                    double* sp = rep_ptr(k.bn.stats, 4 * k.C);
+                    atomicAdd(&sp[2 * k.C + cl], (double)red[0][rl]);
+                    atomicAdd(&sp[3 * k.C + cl], (double)red[1][rl]);
                 }
                 if (k.slope_grad && k.act == ISG_ACT_PRELU)
-                    atomicAdd(&k.slope_grad[cl], (double)red[2][rl]);
+                    atomicAdd(&rep_ptr(k.slope_grad, k.C)[cl], (double)red[2][rl]);
             }
         }
     }

@@ -249,8 +249,9 @@ class Graph:
         return b
 
     def stats_alloc(self, ndouble):
+        """An accumulator of `ndouble` values, replicated L.STAT_REP times (isg.h)."""
         off = self.stats_size
-        self.stats_size += (ndouble + 7) // 8 * 8
+        self.stats_size += (ndouble * L.STAT_REP + 7) // 8 * 8
         return off
 
     def bn_ref(self, bn, count):
@@ -327,7 +328,8 @@ class Graph:
         if bn is None and ct.bias is not None:
             # the wgrad of a convT runs with swapped roles and cannot sum dY per output
             # channel: consumers' gradient sinks accumulate it here instead
-            out.need_sum = self.stats_alloc(2 * ct.out_channels)
+            # (a BN-layout block: sinks add into its sum half, replica stride 4*C)
+            out.need_sum = self.stats_alloc(4 * ct.out_channels)
         bnr = self.bn_ref(bn, self.N * OH * OW) if bn is not None else None
         op = ConvOp(self, "convT", ct, geom, x, out, bnr)
         self.ops.append(op)
@@ -714,7 +716,8 @@ class Plan:
         # of its output gradient, accumulated by the consumers' gradient sinks
         for mod, out, dy in gs.bias_sums:
             items.append({"slope_acc": Ptr(S_STATS, out.need_sum * 8),
-                          "dslope": g.gptr(mod, "bias"), "C": out.C})
+                          "dslope": g.gptr(mod, "bias"), "C": out.C,
+                          "slope_stride": 4 * out.C})
         for b in g.bns:
             it = {"stats": Ptr(S_STATS, b.stats_off * 8), "gamma": b.names["gamma"],
                   "running_mean": b.names["rm"], "running_var": b.names["rv"],
@@ -727,7 +730,8 @@ class Plan:
         for sl in g.slopes.values():
             if sl.used_in_bwd:
                 items.append({"slope_acc": Ptr(S_STATS, sl.acc_off * 8),
-                              "dslope": g.gptr(sl.mod, "weight"), "C": sl.C})
+                              "dslope": g.gptr(sl.mod, "weight"), "C": sl.C,
+                              "slope_stride": sl.C})
         for i in range(0, len(items), L.LIST_CHUNK):
             chunk = items[i:i + L.LIST_CHUNK]
             bw.add(Record(L.OP_GRAD_FINAL, L.ListRec, {"n": len(chunk)}, L.GradFinal, chunk))

@@ -19,6 +19,23 @@ def ptr(t):
     return t.data_ptr() if t is not None else None
 
 
+def rep_zeros(n, device="cuda"):
+    """An accumulator of n doubles in its ISG_STAT_REP replicas (isg.h)."""
+    return torch.zeros(L.STAT_REP * n, dtype=torch.float64, device=device)
+
+
+def rep_from(vals, device="cuda"):
+    """Replicated accumulator holding `vals` (replica 0) — precomputed stats input."""
+    out = rep_zeros(vals.numel(), device)
+    out[:vals.numel()] = vals.to(device=device, dtype=torch.float64)
+    return out
+
+
+def rep_fold(t, n):
+    """Sum of the replicas of an accumulator of n values."""
+    return t.view(L.STAT_REP, n).sum(0)
+
+
 def bn_spec_eval(gamma, beta, rm, rv, eps=1e-5):
     return {"gamma": ptr(gamma), "beta": ptr(beta), "running_mean": ptr(rm),
             "running_var": ptr(rv), "C": gamma.numel(), "train": 0, "count": 1.0, "eps": eps}

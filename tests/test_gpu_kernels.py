@@ -6,7 +6,8 @@ import torch
 import torch.nn.functional as F
 
 from instancesegmentation_amd import _lib as L
-from tests.isg_helpers import bn_spec_eval, bn_spec_train, call, geom, ptr, sinks, stream, vt
+from tests.isg_helpers import (bn_spec_eval, bn_spec_train, call, geom, ptr, rep_fold, rep_from,
+                               rep_zeros, sinks, stream, vt)
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -94,13 +95,14 @@ def test_conv_fwd_dense(cfg):
                      "xform": L.XF_PLAIN})
     Wt, B = cuda32(w), cuda32(b)
     Y = torch.full((N, Co, OH, OW), float("nan"), device=DEV)
-    stats = torch.zeros(2 * Co, dtype=torch.float64, device=DEV)
+    stats = rep_zeros(4 * Co)
     sk = sinks([{"p": ptr(Y), "n_stride": Co * OH * OW, "c0": 0, "C": Co,
                  "mode": L.SINK_STORE, "bias": ptr(B), "stats": ptr(stats)}])
     call("isg_conv_fwd", geom(**ge), vt(segs, N, H, W), ptr(Wt), sk, stream())
     close(Y, ref, what="conv fwd")
+    stats = rep_fold(stats, 4 * Co)
     close(stats[:Co], ref.sum((0, 2, 3)), what="sum")
-    close(stats[Co:], (ref * ref).sum((0, 2, 3)), what="sumsq")
+    close(stats[Co:2 * Co], (ref * ref).sum((0, 2, 3)), what="sumsq")
 
 
 def _bn_train_state(y, g, seed):
@@ -141,15 +143,14 @@ def test_conv_dgrad_dense(cfg):
     z = fwd_xform_ref(xin, ig, ib, irm, irv, islope, "none")
     gref = torch.where(z > 0, ref, ref * islope[None, :, None, None])
     sref = torch.where(z > 0, torch.zeros_like(z), z * ref).sum((0, 2, 3))
-    Yr, Gb, GA, BE, ST = cuda32(yraw), cuda32(gbn), cuda32(gamma), cuda32(beta), \
-        st.to(DEV).contiguous()
+    Yr, Gb, GA, BE, ST = cuda32(yraw), cuda32(gbn), cuda32(gamma), cuda32(beta), rep_from(st)
     dyseg = {"p": ptr(Gb), "y": ptr(Yr), "n_stride": Co * OH * OW, "y_n_stride": Co * OH * OW,
              "C": Co, "xform": L.XF_BN_BWD, "bn": bn_spec_train(GA, BE, ST, N * OH * OW)}
     DX = torch.full((N, Ci, H, W), float("nan"), device=DEV)
     XI = cuda32(xin)
     IG = [cuda32(t) for t in (ig, ib, irm, irv, islope)]
-    istats = torch.zeros(4 * Ci, dtype=torch.float64, device=DEV)
-    sgrad = torch.zeros(Ci, dtype=torch.float64, device=DEV)
+    istats = rep_zeros(4 * Ci)
+    sgrad = rep_zeros(Ci)
     bn_in = bn_spec_eval(*IG[:4])
     bn_in["stats"] = ptr(istats)
     sk = sinks([{"p": ptr(DX), "n_stride": Ci * H * W, "c0": 0, "C": Ci, "mode": L.SINK_ACTBWD,
@@ -157,6 +158,7 @@ def test_conv_dgrad_dense(cfg):
                  "slope": ptr(IG[4]), "slope_grad": ptr(sgrad), "bn": bn_in}])
     call("isg_conv_dgrad", geom(**ge), vt([dyseg], N, OH, OW), ptr(cuda32(w)), sk, stream())
     close(DX, gref, what="dgrad g")
+    istats, sgrad = rep_fold(istats, 4 * Ci), rep_fold(sgrad, Ci)
     close(istats[2 * Ci:3 * Ci], gref.sum((0, 2, 3)), what="gsum")
     close(istats[3 * Ci:], (gref * (xin - irm[None, :, None, None])).sum((0, 2, 3)),
           what="gxsum")
@@ -212,11 +214,12 @@ def test_depthwise(cfg):
     xseg = {"p": ptr(X), "n_stride": C * H * W, "C": C, "xform": L.XF_BN_FWD,
             "act": L.ACT["prelu"], "slope": ptr(G[4]), "bn": bn_spec_eval(*G[:4])}
     Y = torch.full((N, C, H, W), float("nan"), device=DEV)
-    stats = torch.zeros(2 * C, dtype=torch.float64, device=DEV)
+    stats = rep_zeros(4 * C)
     sk = sinks([{"p": ptr(Y), "n_stride": C * H * W, "c0": 0, "C": C, "mode": L.SINK_STORE,
                  "bias": ptr(B), "stats": ptr(stats)}])
     call("isg_conv_fwd", geom(**ge), vt([xseg], N, H, W), ptr(Wt), sk, stream())
     close(Y, ref, what="dw fwd")
+    stats = rep_fold(stats, 4 * C)
     close(stats[:C], ref.sum((0, 2, 3)), what="dw sum")
     # dgrad (plain dy -> plain store)
     dy = rnd(N, C, H, W, seed=25)
@@ -257,15 +260,16 @@ def test_convT_fwd(cfg):
     xseg = {"p": ptr(X), "n_stride": Ci * H * W, "C": Ci, "xform": L.XF_BN_FWD,
             "act": L.ACT["relu"], "bn": bn_spec_eval(*G[:4])}
     Y = torch.full((N, Co, OH, OW), float("nan"), device=DEV)
-    stats = torch.zeros(2 * Co, dtype=torch.float64, device=DEV)
+    stats = rep_zeros(4 * Co)
     sk = sinks([{"p": ptr(Y), "n_stride": Co * OH * OW, "c0": 0, "C": Co, "mode": L.SINK_STORE,
                  "bias": ptr(B), "stats": ptr(stats)}])
     ge = dict(N=N, Ci=Ci, H=H, W=W, Co=Co, OH=OH, OW=OW, KH=K, KW=K, SH=S, SW=S, PH=P, PW=P,
               DH=1, DW=1, groups=1)
     call("isg_convT_fwd", geom(**ge), vt([xseg], N, H, W), ptr(Wt), sk, stream())
     close(Y, ref, what="convT")
+    stats = rep_fold(stats, 4 * Co)
     close(stats[:Co], ref.sum((0, 2, 3)), what="convT sum")
-    close(stats[Co:], (ref * ref).sum((0, 2, 3)), what="convT sumsq")
+    close(stats[Co:2 * Co], (ref * ref).sum((0, 2, 3)), what="convT sumsq")
 
 
 @pytest.mark.parametrize("k", [2, 4])
@@ -304,7 +308,7 @@ def test_tail(act, up):
     out = torch.where(pre > 0, pre, pre * slope[None, :, None, None]) if act == "prelu" \
         else pre.clamp_min(0)
     Y, R, GA, BE, SL = cuda32(y), cuda32(r), cuda32(gamma), cuda32(beta), cuda32(slope)
-    ST = st0.to(DEV).contiguous()
+    ST = rep_from(st0)
     bnt = bn_spec_train(GA, BE, ST, N * H * W)
     t = {"term": [{"p": ptr(Y), "n_stride": C * H * W, "C": C, "xform": L.XF_BN_FWD,
                    "act": 0, "bn": bnt},
@@ -325,7 +329,7 @@ def test_tail(act, up):
     dr = F.avg_pool2d(g, 2) * 4 if up else g
     Gt = torch.full((N, C, H, W), float("nan"), device=DEV)
     DR = torch.full(tuple(r.shape), float("nan"), device=DEV)
-    sg = torch.zeros(C, dtype=torch.float64, device=DEV)
+    sg = rep_zeros(C)
     tg = {"f": t, "dout": ptr(cuda32(dout)), "dout_n_stride": C * H * W, "g": ptr(Gt),
           "g_n_stride": C * H * W, "dterm": [None, ptr(DR), None],
           "dterm_n_stride": [0, R[0].numel(), 0], "dterm_accum": [0, 0, 0],
@@ -333,6 +337,7 @@ def test_tail(act, up):
     call("isg_tail_bwd", struct(LL.TailGrad, tg), stream())
     close(Gt, g, what="tail g")
     close(DR, dr, what="tail dterm")
+    ST, sg = rep_fold(ST, 4 * C), rep_fold(sg, C)
     close(ST[2 * C:3 * C], g.sum((0, 2, 3)), what="tail gsum")
     close(ST[3 * C:], (g * (y - mean)).sum((0, 2, 3)), what="tail gxsum")
     if act == "prelu":

@@ -34,7 +34,8 @@ def test_library_exports_every_declared_symbol():
     missing = [s for s in declared if s not in exported]
     assert not missing, missing
     assert set(declared) <= set(L.SIGNATURES), set(declared) - set(L.SIGNATURES)
-    assert lib.isg_abi_version() == 1
+    assert lib.isg_abi_version() == L.ABI_VERSION
+    assert lib.isg_stat_replicas() == L.STAT_REP
 
 
 def test_library_error_path_without_gpu():
