@@ -738,4 +738,5 @@ class Plan:
         self.stats_size = max(g.stats_size, 8)
         self.bwd = bw.compile()
         self.grad_size = gs.size
+        self.grad_bufs = list(gs.D.values()) + list(gs.G.values())  # for debugging tools
         self.used_params = set(g.used_params)
