@@ -11,7 +11,7 @@ import sys
 def rows_from(path):
     if path.endswith(".db"):
         c = sqlite3.connect(path)
-        return [(r[0], int(r[1]), float(r[2]) / 1e3, float(r[3]) / 1e3, float(r[4]))
+        return [(r[0], int(r[1]), float(r[2]), float(r[3]), float(r[4]))  # view is in us
                 for r in c.execute("select name,total_calls,total_duration,average,percentage "
                                    "from top_kernels")]
     out = []
