@@ -65,6 +65,12 @@ typedef struct {
     int32_t train;
     float count; /* N*H*W */
     float eps;
+    /* Finalised per-channel coefficients (8*C floats), or NULL: forward [C][4] =
+     * (mean, gamma*rstd, beta, 0) then backward [C][4] = (A, B, mean, C) of
+     * dy = A*g + B*(y - mean) + C. Written by isg_bn_finalize once per layer and step
+     * so consumers read 16 bytes per channel instead of reducing the fp64 replicas;
+     * NULL makes every consumer derive them from `stats` (or the running stats). */
+    float* coef;
 } isg_bn;
 
 /* A channel segment of a virtual tensor.
@@ -168,6 +174,19 @@ int32_t isg_conv_dgrad(const isg_conv_geom* g, const isg_vtensor* dy, const floa
 int32_t isg_conv_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x,
                        float* dw, float* dbias, isg_stream_t stream);
 
+/* Weight-gradient replicas. A dW element receives one f32 atomic from every workgroup
+ * along the pixel dimension (hundreds); same-address atomics serialise at the memory
+ * side (~40 ns each), so the wgrad kernels add into one of `nrep` replicas of dw/dbias
+ * (replica r at dw + r*rep_stride floats), chosen per workgroup, and one
+ * isg_sum_replicas pass folds them at the end of the backward. */
+#define ISG_WREP 16
+int32_t isg_conv_wgrad_rep(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x,
+                           float* dw, float* dbias, int64_t rep_stride, int32_t nrep,
+                           isg_stream_t stream);
+/* dst[i] = sum_{r<nrep} src[r*stride + i] for i < n (fixed order: deterministic). */
+int32_t isg_sum_replicas(float* dst, const float* src, int64_t n, int32_t nrep, int64_t stride,
+                         isg_stream_t stream);
+
 /* ConvTranspose2d forward (segment.py:305-306, 435-436) with kernel = 2*stride,
  * weight [Ci][Co][K][K], as a sub-pixel direct kernel. geom describes the transposed
  * conv: input (N,Ci,H,W) -> output (N,Co,OH,OW), KH=KW=K, SH=SW=s, PH=PW=p. */
@@ -198,6 +217,13 @@ typedef struct {
     int32_t pad_;
 } isg_bn_update;
 int32_t isg_bn_update_running(const isg_bn_update* items, int32_t nitems, isg_stream_t stream);
+
+/* Coefficient finalisation for `nitems` BatchNorm layers (HOST array, chunked like
+ * isg_bn_update_running): from the replicated fp64 statistics write items[i].coef's
+ * forward half (bwd == 0, after the forward statistics are complete) or backward half
+ * (bwd == 1, after the gsum/gxsum statistics are complete). Same fp64 formulas the
+ * consumers would evaluate (BatchNorm2d train: biased variance, eps). */
+int32_t isg_bn_finalize(const isg_bn* items, int32_t nitems, int32_t bwd, isg_stream_t stream);
 
 /* Parameter-gradient finalisation (HOST item array, like isg_bn_update_running):
  *   dgamma = rstd*gxsum, dbeta = gsum,

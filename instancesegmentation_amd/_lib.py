@@ -19,13 +19,14 @@ SINK_STORE, SINK_ACCUM, SINK_ACTBWD, SINK_NONE = 0, 1, 2, 3
 MAX_SEGS = 3
 LIST_CHUNK = 32
 STAT_REP = 16     # ISG_STAT_REP: accumulator replicas (isg.h)
-ABI_VERSION = 2
+ABI_VERSION = 4
+WREP = 16         # ISG_WREP: weight-gradient replicas (isg.h)
 
 
 class Bn(Structure):
     _fields_ = [("gamma", c_void_p), ("beta", c_void_p), ("running_mean", c_void_p),
                 ("running_var", c_void_p), ("stats", c_void_p), ("C", c_int32),
-                ("train", c_int32), ("count", c_float), ("eps", c_float)]
+                ("train", c_int32), ("count", c_float), ("eps", c_float), ("coef", c_void_p)]
 
 
 class VSeg(Structure):
@@ -88,7 +89,13 @@ class ConvRec(Structure):
 
 
 class WgradRec(Structure):
-    _fields_ = [("g", Geom), ("dy", VTensor), ("x", VTensor), ("dw", c_void_p), ("dbias", c_void_p)]
+    _fields_ = [("g", Geom), ("dy", VTensor), ("x", VTensor), ("dw", c_void_p), ("dbias", c_void_p),
+                ("rep_stride", c_int64), ("nrep", c_int32), ("pad_", c_int32)]
+
+
+class SumRepRec(Structure):
+    _fields_ = [("dst", c_void_p), ("src", c_void_p), ("n", c_int64), ("stride", c_int64),
+                ("nrep", c_int32), ("pad_", c_int32)]
 
 
 class PoolRec(Structure):
@@ -112,10 +119,11 @@ class MemsetRec(Structure):
 OP_CONV_FWD, OP_CONV_DGRAD, OP_CONV_WGRAD, OP_CONVT_FWD = 1, 2, 3, 4
 OP_MAXPOOL_FWD, OP_MAXPOOL_BWD, OP_TAIL_FWD, OP_TAIL_BWD = 5, 6, 7, 8
 OP_BN_UPDATE, OP_GRAD_FINAL, OP_BCE, OP_MEMSET = 9, 10, 11, 12
+OP_SUM_REP, OP_BN_FINAL = 13, 14
 
 _RECORD_CHECK = [(0, VTensor), (1, Sinks), (2, ConvRec), (3, WgradRec), (4, PoolRec), (5, Tail),
                  (6, TailGrad), (7, BnUpdate), (8, GradFinal), (9, BceRec), (10, Geom), (11, Bn),
-                 (12, VSeg), (13, Sink)]
+                 (12, VSeg), (13, Sink), (14, SumRepRec)]
 
 # exported symbol -> (restype, argtypes)
 SIGNATURES = {
@@ -123,6 +131,9 @@ SIGNATURES = {
     "isg_conv_dgrad": (c_int32, [POINTER(Geom), POINTER(VTensor), c_void_p, POINTER(Sinks), c_void_p]),
     "isg_conv_wgrad": (c_int32, [POINTER(Geom), POINTER(VTensor), POINTER(VTensor), c_void_p,
                                  c_void_p, c_void_p]),
+    "isg_conv_wgrad_rep": (c_int32, [POINTER(Geom), POINTER(VTensor), POINTER(VTensor), c_void_p,
+                                     c_void_p, c_int64, c_int32, c_void_p]),
+    "isg_sum_replicas": (c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_int64, c_void_p]),
     "isg_convT_fwd": (c_int32, [POINTER(Geom), POINTER(VTensor), c_void_p, POINTER(Sinks), c_void_p]),
     "isg_maxpool_fwd": (c_int32, [POINTER(VTensor), c_int32, c_void_p, c_int64, c_void_p]),
     "isg_maxpool_bwd": (c_int32, [POINTER(VTensor), c_int32, c_void_p, c_int64, POINTER(Sinks),
@@ -131,6 +142,7 @@ SIGNATURES = {
     "isg_tail_bwd": (c_int32, [POINTER(TailGrad), c_void_p]),
     "isg_bn_update_running": (c_int32, [POINTER(BnUpdate), c_int32, c_void_p]),
     "isg_grad_finalize": (c_int32, [POINTER(GradFinal), c_int32, c_void_p]),
+    "isg_bn_finalize": (c_int32, [POINTER(Bn), c_int32, c_int32, c_void_p]),
     "isg_bce_sigmoid": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_float, c_void_p]),
     "isg_sigmoid_fwd": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p]),
     "isg_sigmoid_bwd": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),

@@ -11,6 +11,7 @@
 
 static thread_local std::string g_last_error;
 
+
 int32_t isg_set_error(int32_t code, const char* fmt, ...) {
     char buf[512];
     va_list ap;
@@ -33,13 +34,13 @@ int32_t isg_dense_conv_fwd(const isg_conv_geom*, const isg_vtensor*, const float
 int32_t isg_dense_conv_dgrad(const isg_conv_geom*, const isg_vtensor*, const float*, const isg_sinks*,
                              hipStream_t);
 int32_t isg_dense_conv_wgrad(const isg_conv_geom*, const isg_vtensor*, const isg_vtensor*, float*,
-                             float*, hipStream_t);
+                             float*, int64_t, int32_t, hipStream_t);
 int32_t isg_depthwise_fwd(const isg_conv_geom*, const isg_vtensor*, const float*, const isg_sinks*,
                           hipStream_t);
 int32_t isg_depthwise_dgrad(const isg_conv_geom*, const isg_vtensor*, const float*, const isg_sinks*,
                             hipStream_t);
 int32_t isg_depthwise_wgrad(const isg_conv_geom*, const isg_vtensor*, const isg_vtensor*, float*,
-                            float*, hipStream_t);
+                            float*, int64_t, int32_t, hipStream_t);
 
 static int32_t check_geom(const isg_conv_geom* g) {
     if (!g) return isg_set_error(ISG_ERR_INVALID, "conv: NULL geometry");
@@ -60,7 +61,7 @@ static int32_t check_geom(const isg_conv_geom* g) {
 extern "C" {
 
 const char* isg_last_error(void) { return g_last_error.c_str(); }
-int32_t isg_abi_version(void) { return 2; }
+int32_t isg_abi_version(void) { return 4; }
 int32_t isg_stat_replicas(void) { return ISG_STAT_REP; }
 
 int32_t isg_conv_fwd(const isg_conv_geom* g, const isg_vtensor* x, const float* w,
@@ -77,11 +78,20 @@ int32_t isg_conv_dgrad(const isg_conv_geom* g, const isg_vtensor* dy, const floa
     return isg_depthwise_dgrad(g, dy, w, dx, st);
 }
 
+int32_t isg_conv_wgrad_rep(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x,
+                           float* dw, float* dbias, int64_t rep_stride, int32_t nrep,
+                           isg_stream_t st) {
+    if (int32_t e = check_geom(g)) return e;
+    if (nrep < 1 || (nrep > 1 && rep_stride <= 0))
+        return isg_set_error(ISG_ERR_INVALID, "conv wgrad: bad replicas %d / stride %lld", nrep,
+                             (long long)rep_stride);
+    if (g->groups == 1) return isg_dense_conv_wgrad(g, dy, x, dw, dbias, rep_stride, nrep, st);
+    return isg_depthwise_wgrad(g, dy, x, dw, dbias, rep_stride, nrep, st);
+}
+
 int32_t isg_conv_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x,
                        float* dw, float* dbias, isg_stream_t st) {
-    if (int32_t e = check_geom(g)) return e;
-    if (g->groups == 1) return isg_dense_conv_wgrad(g, dy, x, dw, dbias, st);
-    return isg_depthwise_wgrad(g, dy, x, dw, dbias, st);
+    return isg_conv_wgrad_rep(g, dy, x, dw, dbias, 0, 1, st);
 }
 
 // ---- plan executor ----------------------------------------------------------------
@@ -102,6 +112,8 @@ enum {
     OP_GRAD_FINAL = 10,
     OP_BCE = 11,
     OP_MEMSET = 12,
+    OP_SUM_REP = 13,
+    OP_BN_FINAL = 14,
 };
 
 struct ConvRec {
@@ -116,6 +128,17 @@ struct WgradRec {
     isg_vtensor x;
     float* dw;
     float* dbias;
+    int64_t rep_stride;
+    int32_t nrep;
+    int32_t pad_;
+};
+struct SumRepRec {
+    float* dst;
+    const float* src;
+    int64_t n;
+    int64_t stride;
+    int32_t nrep;
+    int32_t pad_;
 };
 struct PoolRec {
     isg_vtensor x;
@@ -129,7 +152,7 @@ struct PoolRec {
 };
 struct ListRec {  // followed in the record by n items (host memory)
     int32_t n;
-    int32_t pad_;
+    int32_t pad_;  // OP_BN_FINAL: 0 forward / 1 backward coefficients
 };
 struct BceRec {
     const float* logits;
@@ -186,7 +209,8 @@ int32_t isg_exec(const void* ops, int32_t nops, void* const* table, isg_stream_t
             }
             case OP_CONV_WGRAD: {
                 auto* r = (WgradRec*)buf;
-                rc = isg_conv_wgrad(&r->g, &r->dy, &r->x, r->dw, r->dbias, st);
+                rc = isg_conv_wgrad_rep(&r->g, &r->dy, &r->x, r->dw, r->dbias, r->rep_stride,
+                                        r->nrep < 1 ? 1 : r->nrep, st);
                 break;
             }
             case OP_CONVT_FWD: {
@@ -215,6 +239,11 @@ int32_t isg_exec(const void* ops, int32_t nops, void* const* table, isg_stream_t
                 rc = isg_bn_update_running((const isg_bn_update*)(buf + sizeof(ListRec)), r->n, st);
                 break;
             }
+            case OP_BN_FINAL: {
+                auto* r = (ListRec*)buf;
+                rc = isg_bn_finalize((const isg_bn*)(buf + sizeof(ListRec)), r->n, r->pad_, st);
+                break;
+            }
             case OP_GRAD_FINAL: {
                 auto* r = (ListRec*)buf;
                 rc = isg_grad_finalize((const isg_grad_final*)(buf + sizeof(ListRec)), r->n, st);
@@ -223,6 +252,11 @@ int32_t isg_exec(const void* ops, int32_t nops, void* const* table, isg_stream_t
             case OP_BCE: {
                 auto* r = (BceRec*)buf;
                 rc = isg_bce_sigmoid(r->logits, r->target, r->n, r->loss, r->dlogits, r->grad_scale, st);
+                break;
+            }
+            case OP_SUM_REP: {
+                auto* r = (SumRepRec*)buf;
+                rc = isg_sum_replicas(r->dst, r->src, r->n, r->nrep, r->stride, st);
                 break;
             }
             case OP_MEMSET: {
@@ -259,6 +293,7 @@ int32_t isg_record_size(int32_t which) {
         case 11: return (int32_t)sizeof(isg_bn);
         case 12: return (int32_t)sizeof(isg_vseg);
         case 13: return (int32_t)sizeof(isg_sink);
+        case 14: return (int32_t)sizeof(SumRepRec);
         default: return -1;
     }
 }

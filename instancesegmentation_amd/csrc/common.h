@@ -16,6 +16,15 @@
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// Global-address-space access through a generic pointer. Pointers that come out of LDS
+// tables (or any memory the compiler cannot trace to a kernel argument) otherwise turn
+// into flat_load/flat_store, which count on lgkmcnt as well as vmcnt: every later LDS
+// wait then drains all outstanding global loads and the loads serialise.
+typedef const float __attribute__((address_space(1)))* gcfloat_p;
+typedef float __attribute__((address_space(1)))* gfloat_p;
+ISG_DEV float gld(const float* p, int64_t i) { return ((gcfloat_p)p)[i]; }
+ISG_DEV void gst(float* p, int64_t i, float v) { ((gfloat_p)p)[i] = v; }
+
 // ---- per-channel coefficient table (LDS) -------------------------------------
 // BN_FWD : v = act((x - c0) * c1 + c2)          c0=mean  c1=gamma*rstd  c2=beta, c3=slope
 // BN_BWD : v = c0*g + c1*(y - c2) + c3          (BatchNorm2d backward)
@@ -54,6 +63,10 @@ ISG_DEV void bn_mean_rstd(const isg_bn& bn, int c, double& mean, double& rstd) {
 
 // forward coefficients of a BN_FWD segment channel
 ISG_DEV ChanCoef fwd_coef(const isg_bn& bn, const float* slope, int c) {
+    if (bn.coef) {  // finalised once per layer (isg_bn_finalize)
+        const f32x4 f = reinterpret_cast<const f32x4*>(bn.coef)[c];
+        return ChanCoef{f[0], f[1], f[2], slope ? slope[c] : 0.f};
+    }
     double mean, rstd;
     bn_mean_rstd(bn, c, mean, rstd);
     ChanCoef k;
@@ -66,6 +79,10 @@ ISG_DEV ChanCoef fwd_coef(const isg_bn& bn, const float* slope, int c) {
 
 // backward coefficients: dy = A*g + B*(y-mean) + C
 ISG_DEV ChanCoef bwd_coef(const isg_bn& bn, int c) {
+    if (bn.coef) {
+        const f32x4 f = reinterpret_cast<const f32x4*>(bn.coef)[bn.C + c];
+        return ChanCoef{f[0], f[1], f[2], f[3]};
+    }
     double mean, rstd;
     bn_mean_rstd(bn, c, mean, rstd);
     double gam = (double)bn.gamma[c];
@@ -265,6 +282,32 @@ ISG_DEV bool sinks_need_red(const isg_sinks& sk) {
     }
     return false;
 }
+
+// ---- diagnostic stamps (built only into the tools/kbench harness library) -------------
+// STAMP(i): thread 0 of each workgroup records s_memrealtime (100 MHz, chip-global) in
+// slot i of its 8-slot record. Compiled out of libisg.so.
+#ifdef ISG_STAMPS
+#define ISG_STAMP_MAXBLK 65536
+// one buffer per translation unit (no relocatable device code); each .hip exposes it
+// through isg_dbg_stamps_<file>() in the stamp build
+static __device__ unsigned long long isg_stamps[ISG_STAMP_MAXBLK * 8];
+#define ISG_STAMP_ACCESSOR(name)                                          \
+    extern "C" void* name(void) {                                          \
+        void* p = nullptr;                                                 \
+        (void)hipGetSymbolAddress(&p, HIP_SYMBOL(isg_stamps));             \
+        return p;                                                          \
+    }
+#define STAMP(i)                                                                          \
+    do {                                                                                  \
+        if (threadIdx.x == 0) {                                                           \
+            const unsigned b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z); \
+            if (b < ISG_STAMP_MAXBLK) isg_stamps[b * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+        }                                                                                 \
+    } while (0)
+#else
+#define STAMP(i) do {} while (0)
+#define ISG_STAMP_ACCESSOR(name)
+#endif
 
 // ---- error plumbing (host) -----------------------------------------------------
 int32_t isg_set_error(int32_t code, const char* fmt, ...);

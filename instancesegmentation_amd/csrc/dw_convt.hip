@@ -164,12 +164,19 @@ __global__ __launch_bounds__(kThreads) void dw_kernel(DwArgs a) {
     }
 }
 
-// weight gradient: dw[c,t] += sum_p dy[c,p] * x[c, p + tap_t]; dbias[c] += sum_p dy
+// weight gradient: dw[c,t] += sum_p dy[c,p] * x[c, p + tap_t]; dbias[c] += sum_p dy.
+// grid (splits, C): a block reduces ~kDwPix pixels of one channel, each lane kDwU pixels
+// per pass with all their loads issued together, then adds its partials into one of
+// nrep replicas of dw (include/isg.h ISG_WREP) so few atomics meet on one address.
 constexpr int kMaxTaps = 9;
+constexpr int kDwU = 4;
+constexpr int kDwPix = kThreads * kDwU;
 struct DwWgArgs {
     isg_vseg dy, x;
     float* dw;
     float* dbias;
+    int64_t rep_stride;
+    int nrep;
     int N, C, H, W, OH, OW, KH, KW, PH, PW, DH, DW;
     int64_t pix_per_block;
 };
@@ -185,29 +192,46 @@ __global__ __launch_bounds__(kThreads) void dw_wgrad_kernel(DwWgArgs a) {
     int64_t pe = pb + a.pix_per_block;
     if (pe > P) pe = P;
     const int KK = a.KH * a.KW;
+    int tdy[kMaxTaps], tdx[kMaxTaps];
+#pragma unroll
+    for (int t = 0; t < kMaxTaps; ++t) {
+        const int kh = t < KK ? t / a.KW : 0, kw = t < KK ? t - kh * a.KW : 0;
+        tdy[t] = kh * a.DH - a.PH;
+        tdx[t] = kw * a.DW - a.PW;
+    }
     float acc[kMaxTaps + 1];
 #pragma unroll
     for (int t = 0; t <= kMaxTaps; ++t) acc[t] = 0.f;
-    for (int64_t p = pb + threadIdx.x; p < pe; p += kThreads) {
-        const int n = (int)(p / ohw);
-        const int64_t pix = p - (int64_t)n * ohw;
-        const int oy = (int)(pix / a.OW), ox = (int)(pix - (int64_t)oy * a.OW);
-        const float d = seg_load(a.dy, kd, n, c, ohw, pix);
-        acc[kMaxTaps] += d;
+    for (int64_t p0 = pb + threadIdx.x; p0 < pe; p0 += kDwPix) {
+        float d[kDwU], xv[kDwU][kMaxTaps];
 #pragma unroll
-        for (int t = 0; t < kMaxTaps; ++t) {
-            if (t < KK) {
-                const int kh = t / a.KW, kw = t - kh * a.KW;
-                const int iy = oy - a.PH + kh * a.DH, ix = ox - a.PW + kw * a.DW;
-                if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
-                    acc[t] += d * seg_load(a.x, kx, n, c, xhw, (int64_t)iy * a.W + ix);
+        for (int u = 0; u < kDwU; ++u) {
+            const int64_t p = p0 + (int64_t)u * kThreads;
+            const bool pv = p < pe;
+            const int n = pv ? (int)(p / ohw) : 0;
+            const int64_t pix = pv ? p - (int64_t)n * ohw : 0;
+            const int oy = (int)(pix / a.OW), ox = (int)(pix - (int64_t)oy * a.OW);
+            d[u] = pv ? seg_load(a.dy, kd, n, c, ohw, pix) : 0.f;
+#pragma unroll
+            for (int t = 0; t < kMaxTaps; ++t) {
+                const int iy = oy + tdy[t], ix = ox + tdx[t];
+                xv[u][t] = (pv && t < KK && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
+                               ? seg_load(a.x, kx, n, c, xhw, (int64_t)iy * a.W + ix)
+                               : 0.f;
             }
+        }
+#pragma unroll
+        for (int u = 0; u < kDwU; ++u) {
+            acc[kMaxTaps] += d[u];
+#pragma unroll
+            for (int t = 0; t < kMaxTaps; ++t) acc[t] = fmaf(d[u], xv[u][t], acc[t]);
         }
     }
     block_reduce<kMaxTaps + 1>(acc, sh);
     if (threadIdx.x == 0) {
-        for (int t = 0; t < KK; ++t) atomicAdd(&a.dw[c * KK + t], acc[t]);
-        if (a.dbias) atomicAdd(&a.dbias[c], acc[kMaxTaps]);
+        const int64_t ro = (int64_t)((blockIdx.x + 7u * blockIdx.y) % (unsigned)a.nrep) * a.rep_stride;
+        for (int t = 0; t < KK; ++t) atomicAdd(&a.dw[ro + c * KK + t], acc[t]);
+        if (a.dbias) atomicAdd(&a.dbias[ro + c], acc[kMaxTaps]);
     }
 }
 
@@ -352,16 +376,19 @@ int32_t isg_depthwise_dgrad(const isg_conv_geom* g, const isg_vtensor* dy, const
 }
 
 int32_t isg_depthwise_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x,
-                            float* dw, float* dbias, hipStream_t st) {
+                            float* dw, float* dbias, int64_t rep_stride, int32_t nrep,
+                            hipStream_t st) {
     if (dy->nseg != 1 || x->nseg != 1 || g->KH * g->KW > kMaxTaps)
         return isg_set_error(ISG_ERR_UNSUPPORTED, "depthwise wgrad: need 1 seg, <= 9 taps");
     DwWgArgs a{};
     a.dy = dy->s[0]; a.x = x->s[0]; a.dw = dw; a.dbias = dbias;
+    a.rep_stride = rep_stride; a.nrep = nrep;
     a.N = g->N; a.C = g->Ci; a.H = g->H; a.W = g->W; a.OH = g->OH; a.OW = g->OW;
     a.KH = g->KH; a.KW = g->KW; a.PH = g->PH; a.PW = g->PW; a.DH = g->DH; a.DW = g->DW;
     const int64_t P = (int64_t)g->N * g->OH * g->OW;
-    int64_t splits = (P + 4095) / 4096;
-    const int64_t maxsplit = (2048 + g->Ci - 1) / g->Ci;
+    // one pass of kDwPix pixels per block while that still leaves >= ~1024 blocks
+    int64_t splits = (P + kDwPix - 1) / kDwPix;
+    const int64_t maxsplit = std::max<int64_t>(1, 2048 / g->Ci);
     if (splits > maxsplit) splits = maxsplit;
     if (splits < 1) splits = 1;
     a.pix_per_block = (P + splits - 1) / splits;

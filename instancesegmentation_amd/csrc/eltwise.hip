@@ -304,6 +304,29 @@ __global__ void bn_update_kernel(BnUpdateList items, int nitems) {
     if (threadIdx.x == 0 && u.num_batches_tracked) u.num_batches_tracked[0] += 1;
 }
 
+struct BnFinalList {
+    isg_bn it[ISG_LIST_CHUNK];
+};
+
+// fwd: coef[c] = (mean, gamma*rstd, beta, 0); bwd: coef[C + c] = (A, B, mean, Cc) — the
+// exact values fwd_coef / bwd_coef (common.h) compute from the statistics.
+__global__ void bn_finalize_kernel(BnFinalList items, int nitems, int bwd) {
+    const int it = blockIdx.x;
+    if (it >= nitems) return;
+    isg_bn bn = items.it[it];
+    float* out = bn.coef;
+    bn.coef = nullptr;  // evaluate from the statistics
+    for (int c = threadIdx.x; c < bn.C; c += blockDim.x) {
+        if (!bwd) {
+            const ChanCoef k = fwd_coef(bn, nullptr, c);
+            reinterpret_cast<f32x4*>(out)[c] = f32x4{k.c0, k.c1, k.c2, 0.f};
+        } else {
+            const ChanCoef k = bwd_coef(bn, c);
+            reinterpret_cast<f32x4*>(out)[bn.C + c] = f32x4{k.c0, k.c1, k.c2, k.c3};
+        }
+    }
+}
+
 __global__ void grad_final_kernel(GradFinalList items, int nitems) {
     const int it = blockIdx.x;
     if (it >= nitems) return;
@@ -456,6 +479,26 @@ __global__ void fill_f64_kernel(double* p, int64_t n, double v) {
         p[i] = v;
 }
 
+// Fold the ISG_WREP weight-gradient replicas: dst[i] = sum_r src[r*stride + i] (fixed
+// order), 4 elements per lane with 16-B loads where the layout allows.
+__global__ __launch_bounds__(kThreads) void sum_rep_kernel(float* __restrict__ dst,
+                                                            const float* __restrict__ src,
+                                                            int64_t n, int nrep, int64_t stride) {
+    const int64_t i4 = ((int64_t)blockIdx.x * kThreads + threadIdx.x) * 4;
+    if (i4 >= n) return;
+    if (i4 + 4 <= n && (stride & 3) == 0 && ((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 15) == 0) {
+        f32x4 acc = *reinterpret_cast<const f32x4*>(src + i4);
+        for (int r = 1; r < nrep; ++r) acc += *reinterpret_cast<const f32x4*>(src + r * stride + i4);
+        *reinterpret_cast<f32x4*>(dst + i4) = acc;
+        return;
+    }
+    for (int64_t i = i4; i < n && i < i4 + 4; ++i) {
+        float acc = src[i];
+        for (int r = 1; r < nrep; ++r) acc += src[r * stride + i];
+        dst[i] = acc;
+    }
+}
+
 unsigned grid_for(int64_t n, int cap = 2048) {
     int64_t b = (n + kThreads - 1) / kThreads;
     if (b > cap) b = cap;
@@ -522,6 +565,20 @@ int32_t isg_bn_update_running(const isg_bn_update* items, int32_t nitems, isg_st
     return 0;
 }
 
+int32_t isg_bn_finalize(const isg_bn* items, int32_t nitems, int32_t bwd, isg_stream_t st) {
+    for (int i = 0; i < nitems; ++i)
+        if (!items[i].coef || !items[i].stats || (((uintptr_t)items[i].coef) & 15))
+            return isg_set_error(ISG_ERR_INVALID, "bn_finalize: item %d needs stats and a 16-B aligned coef", i);
+    for (int b = 0; b < nitems; b += ISG_LIST_CHUNK) {
+        const int n = nitems - b < ISG_LIST_CHUNK ? nitems - b : ISG_LIST_CHUNK;
+        BnFinalList l;
+        memcpy(l.it, items + b, sizeof(isg_bn) * n);
+        hipLaunchKernelGGL(bn_finalize_kernel, dim3(n), dim3(128), 0, st, l, n, bwd ? 1 : 0);
+        if (int32_t e = isg_check_launch("bn_finalize_kernel")) return e;
+    }
+    return 0;
+}
+
 int32_t isg_grad_finalize(const isg_grad_final* items, int32_t nitems, isg_stream_t st) {
     for (int b = 0; b < nitems; b += ISG_LIST_CHUNK) {
         const int n = nitems - b < ISG_LIST_CHUNK ? nitems - b : ISG_LIST_CHUNK;
@@ -572,6 +629,17 @@ int32_t isg_adam_dev(float* param, const float* grad, float* exp_avg, float* exp
     hipLaunchKernelGGL(adam_dev_kernel, dim3(grid_for(n)), dim3(kThreads), 0, st, param, grad,
                        exp_avg, exp_avg_sq, live, n, step, lr, beta1, beta2, eps, weight_decay);
     return isg_check_launch("adam_dev_kernel");
+}
+
+int32_t isg_sum_replicas(float* dst, const float* src, int64_t n, int32_t nrep, int64_t stride,
+                         isg_stream_t st) {
+    if (n <= 0) return 0;
+    if (!dst || !src || nrep < 1 || (nrep > 1 && stride < n))
+        return isg_set_error(ISG_ERR_INVALID, "sum_replicas: bad arguments");
+    const int64_t blocks = ((n + 3) / 4 + kThreads - 1) / kThreads;
+    hipLaunchKernelGGL(sum_rep_kernel, dim3((unsigned)blocks), dim3(kThreads), 0, st, dst, src, n,
+                       nrep, stride);
+    return isg_check_launch("sum_rep_kernel");
 }
 
 int32_t isg_fill_f64(double* p, int64_t n, double v, isg_stream_t st) {

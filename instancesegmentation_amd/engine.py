@@ -21,6 +21,7 @@ Backward is derived op by op in reverse order:
     double-precision statistics in one pass at the end.
 """
 import ctypes
+import os
 import struct
 
 import torch
@@ -34,6 +35,7 @@ S_IN = (6, 7)
 S_OUT = (8, 9)
 S_DOUT = (10, 11)
 S_DIN = (12, 13)
+S_WREP = 14  # L.WREP replicas of the flat parameter gradient (wgrad atomics, isg.h)
 S_TENSOR0 = 16
 
 ALIGN = 64  # elements (256 B) between arena buffers
@@ -241,6 +243,13 @@ class Graph:
         self.used_params.add(k)
         return Ptr(S_PGRAD, self.pgrad_off[k] * 4)
 
+    def wrep_ptr(self, mod, attr):
+        """Replica 0 of a parameter's gradient in the S_WREP arena (L.WREP replicas of the
+        flat gradient, stride pgrad_size floats); folded into S_PGRAD by OP_SUM_REP."""
+        k = self.pname(mod, attr)
+        self.used_params.add(k)
+        return Ptr(S_WREP, self.pgrad_off[k] * 4)
+
     # -- allocation ----------------------------------------------------------------------
     def act_buf(self, C, H, W, name):
         b = Buf(S_ACT, self.N, C, H, W, name, off=self.act_size)
@@ -266,6 +275,9 @@ class Graph:
             "nbt": self.tptr(bn, "num_batches_tracked")})
         ref.gname = (bn, "weight")
         ref.bname = (bn, "bias")
+        # finalised coefficients (isg_bn.coef): 8*C floats = 4*C doubles, 64-B aligned
+        ref.coef_off = self.stats_size
+        self.stats_size += (4 * bn.num_features + 7) // 8 * 8
         self.bns.append(ref)
         self.bn_by_mod[id(bn)] = ref
         return ref
@@ -369,13 +381,28 @@ class Graph:
 
 # ---------------------------------------------------------------------------------
 # spec helpers
-def bn_spec(bnr, train):
+_BN_FINAL = os.environ.get("ISG_NO_BN_FINAL", "0") != "1"  # debugging switch
+
+
+def bn_spec(bnr, train, coef=True):
     if bnr is None:
         return {"train": 1}
     n = bnr.names
-    return {"gamma": n["gamma"], "beta": n["beta"], "running_mean": n["rm"],
-            "running_var": n["rv"], "stats": Ptr(S_STATS, bnr.stats_off * 8), "C": bnr.C,
-            "train": 1 if train else 0, "count": float(bnr.count), "eps": float(bnr.mod.eps)}
+    s = {"gamma": n["gamma"], "beta": n["beta"], "running_mean": n["rm"],
+         "running_var": n["rv"], "stats": Ptr(S_STATS, bnr.stats_off * 8), "C": bnr.C,
+         "train": 1 if train else 0, "count": float(bnr.count), "eps": float(bnr.mod.eps)}
+    if train and coef and _BN_FINAL:
+        # consumers read the coefficients OP_BN_FINAL wrote (forward half after the
+        # producing conv, backward half after the op that completes gsum/gxsum)
+        s["coef"] = Ptr(S_STATS, bnr.coef_off * 8)
+    return s
+
+
+def bn_final_record(bnrs, bwd):
+    items = [bn_spec(b, True) for b in bnrs]
+    return Record(L.OP_BN_FINAL, L.ListRec, {"n": len(items), "pad_": 1 if bwd else 0}, L.Bn,
+                  items, label=("bn_final_bwd " if bwd else "bn_final ") +
+                  ",".join(str(b.C) for b in bnrs))
 
 
 def fwd_seg(val, train):
@@ -402,6 +429,7 @@ class GradState:
         self.G = {}       # id(raw buf) -> g Buf (dL/d BN-output of a virtual value)
         self.inited = {}  # id(buf) -> set of (c0, C)
         self.external = {}  # id(buf) -> Buf (e.g. dlogits slot)
+        self.pending_final = []  # BNs whose gsum/gxsum the last op completed
 
     def alloc(self, like, name):
         b = Buf(S_GRAD, like.N, like.C, like.H, like.W, name, off=self.size)
@@ -440,6 +468,8 @@ class GradState:
                 s["slope"] = Ptr(val.slope.slot)
                 s["slope_grad"] = Ptr(S_STATS, val.slope.acc_off * 8)
                 val.slope.used_in_bwd = True
+            if val.bn is not None:
+                self.pending_final.append(val.bn)
             return s
         d = self.dbuf(val.buf)
         first = self.mark(val.buf, val.c0, val.C)
@@ -533,7 +563,8 @@ class ConvOp:
                                label="dx_" + self.out.name, flops=fl, nbytes=dyb + xb + wb))
         # ---- weight / bias gradient
         xsegs = [fwd_seg(v, g.train) for v in self.x.segs]
-        dw = g.gptr(self.mod, "weight")
+        dw = g.wrep_ptr(self.mod, "weight")
+        rep = {"rep_stride": g.pgrad_size, "nrep": L.WREP}
         has_bias = self.mod.bias is not None
         if self.kind == "convT":
             tg = dict(N=g.N, Ci=ge["Co"], H=ge["OH"], W=ge["OW"], Co=ge["Ci"], OH=ge["H"],
@@ -541,14 +572,14 @@ class ConvOp:
                       PH=ge["PH"], PW=ge["PW"], DH=1, DW=1, groups=1)
             ops.add(Record(L.OP_CONV_WGRAD, L.WgradRec,
                            {"g": tg, "dy": vtensor(xsegs, g.N, ge["H"], ge["W"]), "x": dyv,
-                            "dw": dw}, label="dw_" + self.out.name, flops=fl,
+                            "dw": dw, **rep}, label="dw_" + self.out.name, flops=fl,
                            nbytes=dyb + xb + wb))
             if has_bias and self.bnr is None:
                 gs.bias_sums.append((self.mod, self.out, dy))
         else:
-            rec = {"g": ge, "dy": dyv, "x": vtensor(xsegs, g.N, ge["H"], ge["W"]), "dw": dw}
+            rec = {"g": ge, "dy": dyv, "x": vtensor(xsegs, g.N, ge["H"], ge["W"]), "dw": dw, **rep}
             if has_bias and self.bnr is None:
-                rec["dbias"] = g.gptr(self.mod, "bias")
+                rec["dbias"] = g.wrep_ptr(self.mod, "bias")
             ops.add(Record(L.OP_CONV_WGRAD, L.WgradRec, rec, label="dw_" + self.out.name,
                            flops=fl, nbytes=dyb + xb + wb))
         if has_bias and self.bnr is not None:
@@ -624,6 +655,7 @@ class TailOp:
                     assert v.c0 == 0 and v.C == v.buf.C
                     assert id(v.buf) not in gs.G
                     gs.G[id(v.buf)] = gb
+                    gs.pending_final.append(v.bn)
         dterm, dns, dacc = [None] * 3, [0] * 3, [0] * 3
         for i, (v, up) in enumerate(self.terms):
             if v.bn is None and v.grad:
@@ -665,6 +697,9 @@ class Plan:
             fw.add(Record(L.OP_MEMSET, L.MemsetRec, {"p": Ptr(S_STATS), "bytes": g.stats_size * 8}))
         for op in g.ops:
             op.fwd(fw)
+            bnr = getattr(op, "bnr", None)
+            if train and bnr is not None and _BN_FINAL:
+                fw.add(bn_final_record([bnr], False))
         if train and g.bns:
             items = []
             for b in g.bns:
@@ -701,14 +736,24 @@ class Plan:
                 b = v.segs[0].buf
                 gs.external[id(b)] = Buf(S_DIN[i], b.N, b.C, b.H, b.W, f"din{i}")
         bw = OpList()
-        bw.add(Record(L.OP_MEMSET, L.MemsetRec, {"p": Ptr(S_PGRAD), "bytes": g.pgrad_size * 4}))
+        # weight gradients accumulate (atomics) into L.WREP replicas, folded into S_PGRAD
+        # by OP_SUM_REP before the BN/PReLU finalisation overwrites its own entries
+        bw.add(Record(L.OP_MEMSET, L.MemsetRec, {"p": Ptr(S_WREP),
+                                                 "bytes": L.WREP * g.pgrad_size * 4}))
         body = OpList()
+        gs.pending_final = []
         for op in reversed(g.ops):
             op.bwd(body, gs)
+            if g.train and gs.pending_final and _BN_FINAL:
+                body.add(bn_final_record(gs.pending_final, True))
+                gs.pending_final = []
         for r in body.recs:
             bw.add(r)
         self.din_written = [v.grad and bool(gs.inited.get(id(v.segs[0].buf)))
                             for v in ins]
+        bw.add(Record(L.OP_SUM_REP, L.SumRepRec, {"dst": Ptr(S_PGRAD), "src": Ptr(S_WREP),
+                                                  "n": g.pgrad_size, "stride": g.pgrad_size,
+                                                  "nrep": L.WREP}, label="sum_wgrad_replicas"))
         # finalisation of BN / PReLU / conv-bias-before-BN gradients
         conv_before = {id(bnr): mod for mod, bnr in gs.bias_from_bn}
         items = []

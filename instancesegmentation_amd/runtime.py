@@ -12,7 +12,8 @@ import torch
 import torch.nn as nn
 
 from . import _lib as L
-from .engine import S_ACT, S_DIN, S_DOUT, S_GRAD, S_IN, S_OUT, S_PGRAD, S_STATS, S_TENSOR0, Plan
+from .engine import (S_ACT, S_DIN, S_DOUT, S_GRAD, S_IN, S_OUT, S_PGRAD, S_STATS, S_TENSOR0,
+                     S_WREP, Plan)
 
 
 # ISG_DEBUG_POISON=1: fill every arena with NaN before use so a read of memory that no
@@ -106,6 +107,7 @@ class Runner:
         dev = act.device
         grad = _arena(max(p.grad_size, 1), torch.float32, dev)
         pgrad = _arena(max(p.graph.pgrad_size, 1), torch.float32, dev)
+        wrep = _arena(L.WREP * max(p.graph.pgrad_size, 1), torch.float32, dev)
         dins = []
         for i, x in enumerate(xs):
             if in_grad[i]:
@@ -117,6 +119,7 @@ class Runner:
         tab[S_STATS] = stats.data_ptr()
         tab[S_GRAD] = grad.data_ptr()
         tab[S_PGRAD] = pgrad.data_ptr()
+        tab[S_WREP] = wrep.data_ptr()
         for i, x in enumerate(xs):
             tab[S_IN[i]] = x.data_ptr()
             if dins[i] is not None:

@@ -21,7 +21,8 @@ import torch
 import torch.distributed as dist
 
 from . import _lib as L
-from .engine import (S_ACT, S_DOUT, S_GRAD, S_IN, S_OUT, S_PGRAD, S_STATS, S_TENSOR0, Plan)
+from .engine import (S_ACT, S_DOUT, S_GRAD, S_IN, S_OUT, S_PGRAD, S_STATS, S_TENSOR0, S_WREP,
+                     Plan)
 
 
 def flatten_module(model, device):
@@ -79,6 +80,7 @@ class Trainer:
         # the plan's packed param-grad layout is exactly the flat buffer's order
         self.grad_flat = torch.zeros_like(self.flat)
         self.pgrad = self.grad_flat
+        self.wrep = torch.empty(L.WREP * g.pgrad_size, dtype=torch.float32, device=dev)
         assert g.pgrad_size == self.flat.numel()
         self.logits = torch.empty(self.plan.out_shapes[0], dtype=torch.float32, device=dev)
         self.dlogits = torch.empty_like(self.logits)
@@ -109,6 +111,7 @@ class Trainer:
         tab[S_STATS] = self.stats.data_ptr()
         tab[S_GRAD] = self.gradarena.data_ptr()
         tab[S_PGRAD] = self.pgrad.data_ptr()
+        tab[S_WREP] = self.wrep.data_ptr()
         for i, x in enumerate(self.inputs):
             tab[S_IN[i]] = x.data_ptr()
         tab[S_OUT[0]] = self.logits.data_ptr()

@@ -188,6 +188,37 @@ def test_conv_wgrad_dense(cfg):
     close(DB, dy.sum((0, 2, 3)), what="dbias")
 
 
+@pytest.mark.parametrize("cfg", [DENSE[0], DENSE[1], DENSE[4], (16, 16, 24, 40, 3, 1, 1, 0)])
+def test_conv_wgrad_replicated(cfg):
+    """isg_conv_wgrad_rep adds into L.WREP replicas (the train plan's layout); folding them
+    with isg_sum_replicas gives the plain weight gradient. Last case: depthwise (d=0 flag)."""
+    Ci, Co, H, W, k, s, p, d = cfg
+    depthwise = d == 0
+    d = max(d, 1)
+    N = 2
+    if depthwise:
+        Co = Ci
+    ge, OH, OW = _geom(N, Ci, Co, H, W, k, s, p, d, groups=Ci if depthwise else 1)
+    x = rnd(N, Ci, H, W, seed=41)
+    dy = rnd(N, Co, OH, OW, seed=43)
+    wshape = (Co, 1 if depthwise else Ci, k, k)
+    ref = torch.nn.grad.conv2d_weight(x, wshape, dy, stride=s, padding=p, dilation=d,
+                                      groups=Ci if depthwise else 1)
+    X, DY = cuda32(x), cuda32(dy)
+    nw = int(np.prod(wshape))
+    stride_ = nw + Co + 37  # replica stride: weight, bias, padding (as in the flat layout)
+    REP = torch.zeros(L.WREP * stride_, device=DEV)
+    call("isg_conv_wgrad_rep", geom(**ge),
+         vt([{"p": ptr(DY), "n_stride": Co * OH * OW, "C": Co, "xform": L.XF_PLAIN}], N, OH, OW),
+         vt([{"p": ptr(X), "n_stride": Ci * H * W, "C": Ci, "xform": L.XF_PLAIN}], N, H, W),
+         ptr(REP), ptr(REP[nw:]), stride_, L.WREP, stream())
+    OUT = torch.full((stride_,), float("nan"), device=DEV)
+    call("isg_sum_replicas", ptr(OUT), ptr(REP), stride_, L.WREP, stride_, stream())
+    close(OUT[:nw].view(wshape), ref, what="replicated wgrad")
+    close(OUT[nw:nw + Co], dy.sum((0, 2, 3)), what="replicated dbias")
+    assert torch.all(OUT[nw + Co:] == 0)
+
+
 DW_CFG = [  # (C, H, W, kh, kw, ph, pw, d)
     (16, 32, 32, 3, 3, 1, 1, 1),
     (48, 16, 24, 3, 3, 2, 2, 2),

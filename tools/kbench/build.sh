@@ -1,0 +1,18 @@
+#!/bin/bash
+# Build libisg_stamp.so (all kernels with -DISG_STAMPS) and the kbench harness, in-tree.
+set -e
+cd "$(dirname "$0")"
+SRC=../../instancesegmentation_amd/csrc
+OUT=$PWD/_build
+mkdir -p $OUT
+FL="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -DISG_STAMPS -Wno-unused-function"
+objs=""
+for f in conv_mfma pw_gemm halo_conv wgrad dw_convt eltwise maskops; do
+  /opt/rocm/bin/hipcc $FL -c $SRC/$f.hip -o $OUT/$f.o &
+  objs="$objs $OUT/$f.o"
+done
+/opt/rocm/bin/hipcc $FL -x hip -c $SRC/api.cpp -o $OUT/api.o &
+wait
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/libisg_stamp.so $objs $OUT/api.o
+/opt/rocm/bin/hipcc -O2 -std=c++17 kbench.cpp -o $OUT/kbench -L$OUT -lisg_stamp -Wl,-rpath,'$ORIGIN'
+echo built $OUT/kbench
