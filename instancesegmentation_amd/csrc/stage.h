@@ -17,41 +17,105 @@ struct ChSrc {
     int xf, act;
 };
 
-ISG_DEV ChSrc ch_src(const isg_vtensor& vt, int c, int hw) {
-    const int c1 = vt.s[0].C, c2 = c1 + vt.s[1].C;
-    const bool s1 = vt.nseg > 1 && c >= c1, s2 = vt.nseg > 2 && c >= c2;
-    // explicit selects: a runtime index into the kernel-argument struct would copy it
-    const float* p = s2 ? vt.s[2].p : (s1 ? vt.s[1].p : vt.s[0].p);
-    const float* y = s2 ? vt.s[2].y : (s1 ? vt.s[1].y : vt.s[0].y);
-    const int64_t ns = s2 ? vt.s[2].n_stride : (s1 ? vt.s[1].n_stride : vt.s[0].n_stride);
-    const int64_t yns = s2 ? vt.s[2].y_n_stride : (s1 ? vt.s[1].y_n_stride : vt.s[0].y_n_stride);
-    const int xf = s2 ? vt.s[2].xform : (s1 ? vt.s[1].xform : vt.s[0].xform);
-    const int act = s2 ? vt.s[2].act : (s1 ? vt.s[1].act : vt.s[0].act);
-    const int cl = c - (s2 ? c2 : (s1 ? c1 : 0));
+// The addressing fields of a vtensor's segments, read once with constant indices into
+// plain registers. Selecting between fields of the kernel-argument struct directly lets
+// the compiler turn "select of loads" into "load of a selected address", which forces a
+// copy of the whole argument struct to scratch.
+struct VtLite {
+    const float *p0, *p1, *p2, *y0, *y1, *y2;
+    int ns0, ns1, ns2, yns0, yns1, yns2, xf0, xf1, xf2, act0, act1, act2;
+    int c1, c2;
+};
+
+ISG_DEV VtLite vt_lite(const isg_vtensor& vt) {
+    VtLite l;
+    l.p0 = vt.s[0].p; l.p1 = vt.s[1].p; l.p2 = vt.s[2].p;
+    l.y0 = vt.s[0].y; l.y1 = vt.s[1].y; l.y2 = vt.s[2].y;
+    l.ns0 = (int)vt.s[0].n_stride; l.ns1 = (int)vt.s[1].n_stride; l.ns2 = (int)vt.s[2].n_stride;
+    l.yns0 = (int)vt.s[0].y_n_stride; l.yns1 = (int)vt.s[1].y_n_stride;
+    l.yns2 = (int)vt.s[2].y_n_stride;
+    l.xf0 = vt.s[0].xform; l.xf1 = vt.s[1].xform; l.xf2 = vt.s[2].xform;
+    l.act0 = vt.s[0].act; l.act1 = vt.s[1].act; l.act2 = vt.s[2].act;
+    l.c1 = vt.nseg > 1 ? vt.s[0].C : 1 << 30;
+    l.c2 = vt.nseg > 2 ? vt.s[0].C + vt.s[1].C : 1 << 30;
+    return l;
+}
+
+ISG_DEV ChSrc ch_src(const VtLite& l, int c, int hw) {
     ChSrc r;
-    r.p = p + (int64_t)cl * hw;
-    r.y = (xf == ISG_XF_BN_BWD && y) ? y + (int64_t)cl * hw : r.p;
-    r.ns = (int)ns;
-    r.yns = (int)yns;
-    r.xf = xf;
-    r.act = act;
+    const float* y;
+    int cl;
+    if (c >= l.c2) {
+        r.p = l.p2; y = l.y2; r.ns = l.ns2; r.yns = l.yns2; r.xf = l.xf2; r.act = l.act2;
+        cl = c - l.c2;
+    } else if (c >= l.c1) {
+        r.p = l.p1; y = l.y1; r.ns = l.ns1; r.yns = l.yns1; r.xf = l.xf1; r.act = l.act1;
+        cl = c - l.c1;
+    } else {
+        r.p = l.p0; y = l.y0; r.ns = l.ns0; r.yns = l.yns0; r.xf = l.xf0; r.act = l.act0;
+        cl = c;
+    }
+    r.p += (int64_t)cl * hw;
+    r.y = (r.xf == ISG_XF_BN_BWD && y) ? y + (int64_t)cl * hw : r.p;
     return r;
 }
 
-// Coefficients of channel c of a vtensor (common.h ChanCoef conventions).
-ISG_DEV ChanCoef vt_coef(const isg_vtensor& vt, int c) {
-    const int c1 = vt.s[0].C, c2 = c1 + vt.s[1].C;
-    const int s = (vt.nseg > 2 && c >= c2) ? 2 : ((vt.nseg > 1 && c >= c1) ? 1 : 0);
-    const isg_vseg& sg = s == 2 ? vt.s[2] : (s == 1 ? vt.s[1] : vt.s[0]);
-    const int cl = c - (s == 2 ? c2 : (s == 1 ? c1 : 0));
+// fp64 evaluation from the statistics (eval mode, or direct ABI calls without
+// isg_bn.coef): out of line so its code exists once; bn passed by value (registers),
+// a reference to the kernel argument would copy the whole argument struct to scratch.
+__device__ __noinline__ ChanCoef coef_slow(isg_bn bn, const float* slope, int cl, int bwd) {
+    return bwd ? bwd_coef(bn, cl) : fwd_coef(bn, slope, cl);
+}
+
+// Coefficients of channel cl of one segment.
+ISG_DEV ChanCoef seg_coefs(const isg_vseg& sg, int cl) {
     ChanCoef k = {0.f, 1.f, 0.f, 0.f};
     if (sg.xform == ISG_XF_BN_FWD) {
-        if (sg.bn.stats || !sg.bn.train) k = fwd_coef(sg.bn, sg.slope, cl);
-        else k.c3 = sg.slope ? sg.slope[cl] : 0.f;  // activation only
+        if (sg.bn.coef) {
+            const f32x4 f = reinterpret_cast<const f32x4*>(sg.bn.coef)[cl];
+            k = ChanCoef{f[0], f[1], f[2], sg.slope ? sg.slope[cl] : 0.f};
+        } else if (sg.bn.stats || !sg.bn.train) {
+            k = coef_slow(sg.bn, sg.slope, cl, 0);
+        } else {
+            k.c3 = sg.slope ? sg.slope[cl] : 0.f;  // activation only
+        }
     } else if (sg.xform == ISG_XF_BN_BWD) {
-        k = bwd_coef(sg.bn, cl);
+        if (sg.bn.coef) {
+            const f32x4 f = reinterpret_cast<const f32x4*>(sg.bn.coef)[sg.bn.C + cl];
+            k = ChanCoef{f[0], f[1], f[2], f[3]};
+        } else {
+            k = coef_slow(sg.bn, nullptr, cl, 1);
+        }
     }
     return k;
+}
+
+// Coefficients of channel c of a vtensor (common.h ChanCoef conventions). Segments are
+// addressed with constant indices only: a runtime index into the kernel-argument struct
+// makes hipcc copy the whole struct to scratch.
+ISG_DEV ChanCoef vt_coef(const isg_vtensor& vt, int c) {
+    const int c1 = vt.s[0].C, c2 = c1 + vt.s[1].C;
+    if (vt.nseg > 2 && c >= c2) return seg_coefs(vt.s[2], c - c2);
+    if (vt.nseg > 1 && c >= c1) return seg_coefs(vt.s[1], c - c1);
+    return seg_coefs(vt.s[0], c);
+}
+
+// Per-channel staging record kept in LDS (built once per block by one thread per
+// channel): a wave-uniform channel index reads it with one broadcast LDS access.
+struct ChT {
+    const float* p;  // channel base, image 0
+    const float* y;  // BN_BWD saved forward output (else == p)
+    int ns, yns;
+    int xf, act;
+    ChanCoef k;
+};
+
+ISG_DEV ChT ch_table_entry(const isg_vtensor& vt, int c, int hw) {
+    const ChSrc s = ch_src(vt_lite(vt), c, hw);
+    ChT t;
+    t.p = s.p; t.y = s.y; t.ns = s.ns; t.yns = s.yns; t.xf = s.xf; t.act = s.act;
+    t.k = vt_coef(vt, c);
+    return t;
 }
 
 // v = transform of raw x (and saved y for BN_BWD); xf/act uniform -> scalar branches

@@ -5,22 +5,26 @@
 //   dW[row][col] += sum_p dy[row][p] * x[ci][p*S - P + (kh,kw)*D],  col = ci*KH*KW + kh*KW + kw
 //
 // A GEMM with the output pixels as the reduction (K) dimension. A workgroup owns a block
-// of up to 64 rows x 128 columns of dW and a contiguous range of 64-pixel tiles (4x16,
-// 2x32 or 1x64 output pixels). Per tile it stages into LDS
-//   * the dy rows (BatchNorm-backward rebuilt on load), and
+// of up to 64 rows x 128 columns of dW and a contiguous range of 64-pixel tiles
+// (TR x TC output pixels, TC in {8,16,32,64}). Per tile it stages into LDS
+//   * the dy rows (BatchNorm-backward rebuilt on load): wave w loads rows w, w+4, ...,
+//     lane = pixel;
 //   * the INPUT HALO of the tile for the block's input channels (producer BatchNorm +
-//     activation applied on load),
-// and every (kh,kw) tap reads the halo at a shifted offset (no im2col gather).
-// The global loads of tile t+1 are issued into registers before the MFMAs of tile t
-// (register double buffer): with 64-pixel tiles a block spends ~1-4k MFMA cycles per
-// tile, which covers the HBM latency of the next tile's loads.
+//     activation applied on load): slot s = (channel, halo row) is wave-uniform, lane =
+//     halo column (HC <= 64),
+// so every channel quantity is scalar (stage.h) and each element costs one address add,
+// one load and one fused transform. Every (kh,kw) tap reads the halo at a shifted offset
+// (no im2col gather). The loads of tile t+1 are issued into registers before the MFMAs
+// of tile t (register double buffer).
 // MFMA v_mfma_f32_16x16x4_f32: A[i=row][k=pixel] from LDS dy, B[k=pixel][j=col] from the
 // halo. Each wave keeps up to 4 16x16 accumulator tiles; blocks with fewer than 4 tiles
 // split the 64 pixels of a tile across waves. A single-row dW (the 4->1 mask-head conv,
 // segment.py:437) runs on the VALU instead: an MFMA there would be 15/16 padding.
-// Partial sums leave the block with one f32 atomic per dW element.
-#include "common.h"
+// Partial sums leave the block with one f32 atomic per dW element, into one of the
+// ISG_WREP replicas (include/isg.h).
 #include <cstdlib>
+
+#include "stage.h"
 
 namespace {
 
@@ -28,19 +32,9 @@ constexpr int kThreads = 256;
 constexpr int kTP = 64;             // pixels per tile
 constexpr int kAStride = kTP + 2;   // conflict-free A-fragment reads
 constexpr int kRowsBlk = 64;        // dW rows per block (BMT <= 4)
-constexpr int kColsBlk = 128;       // dW columns per block (BNT <= 8)
-constexpr int kPA = kRowsBlk * kTP / kThreads;  // A elements per thread per tile (16)
-constexpr int kPX = 16;             // halo elements per thread per tile (max)
-constexpr int kHaloMax = kPX * kThreads;
-constexpr int kMaxXCh = 128;        // halo channels per block
-
-struct VChan {
-    const float* p;
-    const float* y;
-    int ns, yns;  // elements between images (< 2^31 for every tensor here)
-    int xf, act;
-    ChanCoef k;
-};
+constexpr int kColsBlk = 512;       // dW columns per block (BMT*BNT <= 32 tiles)
+constexpr int kMaxXCh = 64;         // halo channels per block
+constexpr int kXs = 9216;           // halo floats per block (36 KB) incl. channel padding
 
 struct WgArgs {
     isg_vtensor dy;  // rows: N x R x OH x OW
@@ -56,7 +50,6 @@ struct WgArgs {
     int tiles_x, tiles_y;
     int64_t ntiles, tiles_per_block;
     int valu;                   // R == 1 path
-    unsigned m_hs, m_hc;        // ceil(2^32 / (HR*HC)), ceil(2^32 / HC)
     int dbg;                    // ablation bits (stamp build only, tools/kbench)
 };
 #ifdef ISG_STAMPS
@@ -65,65 +58,91 @@ struct WgArgs {
 #define DBG(a, b) 0
 #endif
 
-// Fill the per-channel source table of channels [c_lo, c_lo+nc) of a vtensor.
-ISG_DEV void load_vchan(const isg_vtensor& vt, int c_lo, int nc, int64_t hw, VChan* tab,
-                        int tid) {
-    for (int i = tid; i < nc; i += kThreads) {
-        const int c = c_lo + i;
-        int s = 0, cb = 0;
-        if (vt.nseg > 1 && c >= vt.s[0].C) { s = 1; cb = vt.s[0].C; }
-        if (vt.nseg > 2 && c >= vt.s[0].C + vt.s[1].C) { s = 2; cb = vt.s[0].C + vt.s[1].C; }
-        const isg_vseg& sg = vt.s[s];
-        const int cl = c - cb;
-        VChan v;
-        v.p = sg.p + (int64_t)cl * hw;
-        v.y = (sg.xform == ISG_XF_BN_BWD && sg.y) ? sg.y + (int64_t)cl * hw : v.p;  // always loadable
-        v.ns = (int)sg.n_stride;
-        v.yns = (int)sg.y_n_stride;
-        v.xf = sg.xform;
-        v.act = sg.act;
-        ChanCoef k = {0.f, 1.f, 0.f, 0.f};
-        if (sg.xform == ISG_XF_BN_FWD) {
-            if (sg.bn.stats || !sg.bn.train) {
-                k = fwd_coef(sg.bn, sg.slope, cl);
-            } else {
-                k.c3 = sg.slope ? sg.slope[cl] : 0.f;
-            }
-        } else if (sg.xform == ISG_XF_BN_BWD) {
-            k = bwd_coef(sg.bn, cl);
+struct TileCtx {
+    int per_img, TR, TC, apy, apx, lane, wave, Rb, nslots;
+    const ChT* tA;  // LDS: dy rows of the block
+    const ChT* tX;  // LDS: x channels of the block
+};
+
+ISG_DEV void tile_origin(const WgArgs& a, const TileCtx& t, int64_t tl, int& n, int& oy0,
+                         int& ox0) {
+    n = (int)(tl / t.per_img);
+    const int r = (int)(tl - (int64_t)n * t.per_img);
+    const int ty = r / a.tiles_x;
+    oy0 = ty * t.TR;
+    ox0 = (r - ty * a.tiles_x) * t.TC;
+}
+
+// Direct staging, groups of U slots with all their loads in flight together. The loop
+// bodies stay small on purpose: fully unrolled register-prefetch variants of this kernel
+// grew past 60-130 KB of code and ran 2-3x slower (instruction fetch, one wave per SIMD).
+template <int U>
+ISG_DEV void wg_stage(const WgArgs& a, const TileCtx& t, int64_t tl, int nrow_w, float* As,
+                      float* Xs) {
+    int n, oy0, ox0;
+    tile_origin(a, t, tl, n, oy0, ox0);
+    const int oy = oy0 + t.apy, ox = ox0 + t.apx;
+    const bool pv = oy < a.OH && ox < a.OW;
+    const int pix = pv ? oy * a.OW + ox : 0;
+    for (int j0 = 0; j0 < nrow_w; j0 += U) {
+        float v[U], w[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int row = min(t.wave + 4 * (j0 + u), t.Rb - 1);
+            const ChT c = t.tA[row];
+            v[u] = gld(c.p, n * c.ns + pix);
+            w[u] = gld(c.y, n * c.yns + pix);  // == p unless BatchNorm-backward
         }
-        v.k = k;
-        tab[i] = v;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int row = t.wave + 4 * (j0 + u);
+            if (row < t.Rb) {
+                const ChT c = t.tA[row];
+                As[row * kAStride + t.lane] = pv ? ch_xform(c.xf, c.act, c.k, v[u], w[u]) : 0.f;
+            }
+        }
+    }
+    const int iy0 = oy0 * a.SH - a.PH, ix = ox0 * a.SW - a.PW + t.lane;
+    const bool colok = t.lane < a.HC && ix >= 0 && ix < a.W;
+    for (int s0 = t.wave; s0 < t.nslots; s0 += 4 * U) {
+        float v[U], w[U];
+        bool ok[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int slot = min(s0 + 4 * u, t.nslots - 1);
+            const int cl = slot / a.HR, iy = iy0 + slot - cl * a.HR;
+            const ChT c = t.tX[cl];
+            ok[u] = colok && iy >= 0 && iy < a.H;
+            const int o = ok[u] ? iy * a.W + ix : 0;
+            v[u] = gld(c.p, n * c.ns + o);
+            w[u] = gld(c.y, n * c.yns + o);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int slot = s0 + 4 * u;
+            if (slot < t.nslots) {
+                const int cl = slot / a.HR, hr = slot - cl * a.HR;
+                const ChT c = t.tX[cl];
+                if (t.lane < a.HC)
+                    Xs[cl * a.hsp + hr * a.HC + t.lane] = ok[u] ? ch_xform(c.xf, c.act, c.k, v[u], w[u]) : 0.f;
+            }
+        }
     }
 }
 
-
-// exact n / d for n, d < 2^16 with m = ceil(2^32 / d) (host-computed)
-ISG_DEV int fdiv(int n, unsigned m) { return (int)__umulhi((unsigned)n, m); }
-
-// Virtual-tensor transform with per-lane format (selects, no branches).
-ISG_DEV float vchan_apply_sel(const VChan& c, float x, float y) {
-    const float z = (x - c.k.c0) * c.k.c1 + c.k.c2;
-    const float za = c.act == ISG_ACT_RELU ? fmaxf(z, 0.f)
-                     : (c.act == ISG_ACT_PRELU ? (z > 0.f ? z : z * c.k.c3) : z);
-    const float b = c.k.c0 * x + c.k.c1 * (y - c.k.c2) + c.k.c3;
-    return c.xf == ISG_XF_PLAIN ? x : (c.xf == ISG_XF_BN_FWD ? za : b);
-}
-
-// BMT: 16-row tiles of dW per block (A loads per thread = 4*BMT); AB / XB: the dy / x
+// BMT: 16-row tiles of dW per block (A row slots per wave = 4*BMT); AB / XB: the dy / x
 // operand has BatchNorm-backward channels (second load of the saved forward output).
-template <int BMT, bool AB, bool XB>
+template <int TPW>
 __global__ __launch_bounds__(kThreads) void wgrad_kernel(WgArgs a) {
-    constexpr int TPW = 4;      // accumulator tiles per wave (BMT*BNT <= 16)
-    constexpr int NA = 4 * BMT; // A elements per thread per tile
+    // TPW: accumulator tiles per wave = ceil(BMT*BNT / 4)
     __shared__ float As[kRowsBlk * kAStride];
-    __shared__ float Xs[kHaloMax + 64];
-    __shared__ VChan tabA[kRowsBlk];
-    __shared__ VChan tabX[kMaxXCh];
+    __shared__ float Xs[kXs];
+    __shared__ ChT tA[kRowsBlk];
+    __shared__ ChT tX[kMaxXCh];
 
     STAMP(0);
     const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wave = wave_id();
     const int kk = lane >> 4, pl = lane & 15;
     const int KK = a.KH * a.KW;
     const int NCOL = a.Ci * KK;
@@ -134,68 +153,52 @@ __global__ __launch_bounds__(kThreads) void wgrad_kernel(WgArgs a) {
     const int c_hi = min(NCOL, c_lo + a.BNT * 16);
     const int ci_lo = c_lo / KK;
     const int nci = (c_hi - 1) / KK + 1 - ci_lo;
-    const int hs = a.HR * a.HC;
-    const int TC = 1 << a.lgTC;
-    const int64_t ohw = (int64_t)a.OH * a.OW, xhw = (int64_t)a.H * a.W;
+    const int nslots = nci * a.HR;
+    const int TC = 1 << a.lgTC, TR = kTP >> a.lgTC;
+    const int ohw = a.OH * a.OW, xhw = a.H * a.W;
     // this workgroup's replica of dW / dbias (include/isg.h ISG_WREP)
     const int64_t rep_off = (int64_t)((blockIdx.x + 7u * blockIdx.y) % (unsigned)a.nrep) * a.rep_stride;
     float* const dwr = a.dw + rep_off;
 
-    if (!DBG(a, 1)) {
-        load_vchan(a.dy, r_lo, Rb, ohw, tabA, tid);
-        load_vchan(a.x, ci_lo, nci, xhw, tabX, tid);
-    } else {
-        for (int i = tid; i < kRowsBlk + kMaxXCh; i += kThreads) {
-            VChan v = {a.dy.s[0].p, a.dy.s[0].p, 0, 0, 0, 0, {0.f, 1.f, 0.f, 0.f}};
-            if (i < kRowsBlk) tabA[i] = v; else { v.p = v.y = a.x.s[0].p; tabX[i - kRowsBlk] = v; }
-        }
-    }
-
-    // ---- per-thread element lists (tile-invariant) --------------------------------
-    // A: pixel p = lane, rows wave + 4j (j < NA); rows >= Rb load row Rb-1, store 0
-    const int ap = lane;
-    const int apy = ap >> a.lgTC, apx = ap & (TC - 1);
-    const int na = (Rb + 3 - wave) / 4;  // wave-uniform
-    // X: halo element e = tid + 256 j, packed (cl << 20 | hr << 10 | hc); -1 past the end
-    const int nxe = nci * hs;
-    const int nxj = (nxe + kThreads - 1) / kThreads;  // block-uniform
-    int xe[kPX];
-#pragma unroll
-    for (int j = 0; j < kPX; ++j) {
-        const int e = tid + kThreads * j;
-        const int cl = fdiv(e, a.m_hs), rem = e - cl * hs;
-        const int hr = fdiv(rem, a.m_hc), hc = rem - hr * a.HC;
-        xe[j] = e < nxe ? ((cl << 20) | (hr << 10) | hc) : -1;
-    }
+    for (int i = tid; i < Rb; i += kThreads) tA[i] = ch_table_entry(a.dy, r_lo + i, ohw);
+    for (int i = tid; i < nci; i += kThreads) tX[i] = ch_table_entry(a.x, ci_lo + i, xhw);
+    // rows Rb .. 16*BMT of the A tile stay zero (never restaged)
+    for (int i = Rb * kAStride + tid; i < a.BMT * 16 * kAStride; i += kThreads) As[i] = 0.f;
 
     // ---- MFMA operand offsets --------------------------------------------------------
-    const int nt = BMT * a.BNT;
+    const int nt = a.BMT * a.BNT;
     const bool ksplit = nt < 4;
     const int ks = ksplit ? 4 / nt : 1;
     const int kpart = ksplit ? wave / nt : 0;
     const bool kactive = !ksplit || kpart < ks;
     const int kq_lo = kpart * (kTP / ks), kq_hi = kq_lo + kTP / ks;
+    // tv[i]: wave-uniform presence of accumulator tile i; columns past c_hi read any
+    // staged value (their D columns are never stored), so no per-lane guards in the loop
+    bool tv[TPW];
     int arow[TPW], xoff[TPW];
 #pragma unroll
     for (int i = 0; i < TPW; ++i) {
         const int t = ksplit ? (i == 0 && kactive ? wave % nt : 1 << 20) : wave + 4 * i;
         const int rt = t / a.BNT, ct = t - rt * a.BNT;
-        arow[i] = -1;
-        xoff[i] = -1;
-        if (t < nt) {
-            arow[i] = (rt * 16 + pl) * kAStride;
-            const int col = c_lo + ct * 16 + pl;
-            if (col < c_hi) {
-                const int ci = col / KK, tap = col - ci * KK;
-                const int kh = tap / a.KW, kw = tap - kh * a.KW;
-                xoff[i] = (ci - ci_lo) * a.hsp + kh * a.DH * a.HC + kw * a.DW;
-            }
-        }
+        tv[i] = t < nt;
+        arow[i] = tv[i] ? (rt * 16 + pl) * kAStride : 0;
+        const int col = min(c_lo + ct * 16 + pl, c_hi - 1);
+        const int ci = col / KK, tap = col - ci * KK;
+        const int kh = tap / a.KW, kw = tap - kh * a.KW;
+        xoff[i] = tv[i] ? (ci - ci_lo) * a.hsp + kh * a.DH * a.HC + kw * a.DW : 0;
     }
+    // halo offset of pixel 4*s + kk of the tile, per k-step s
+    int poffs[kTP / 4];
+#pragma unroll
+    for (int s = 0; s < kTP / 4; ++s) {
+        const int p = 4 * s + kk;
+        poffs[s] = (p >> a.lgTC) * a.SH * a.HC + (p & (TC - 1)) * a.SW;
+    }
+    const int s_lo = kq_lo / 4, s_hi = kq_hi / 4;
     f32x4 acc[TPW];
 #pragma unroll
     for (int i = 0; i < TPW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float vacc = 0.f;  // VALU path (R == 1): column tid&63, pixel quarter tid>>6
+    float vacc = 0.f;  // VALU path (R == 1): column lane, pixel quarter wave
     int vxoff = -1;
     if (a.valu) {
         const int col = c_lo + lane;
@@ -213,82 +216,15 @@ __global__ __launch_bounds__(kThreads) void wgrad_kernel(WgArgs a) {
     const int64_t t0 = (int64_t)blockIdx.x * a.tiles_per_block;
     const int64_t t1 = min(t0 + a.tiles_per_block, a.ntiles);
     const int per_img = a.tiles_x * a.tiles_y;
-    const int TR = kTP >> a.lgTC;
+    const int apy = lane >> a.lgTC, apx = lane & (TC - 1);
 
-    // register double buffer: raw values of the next tile; loads are unconditional
-    // (clamped addresses) so the compiler issues them back to back
-    float ra[NA], ry[NA], rx[kPX], rxy[kPX];
-    auto tile_origin = [&](int64_t tl, int& n, int& oy0, int& ox0) {
-        n = (int)(tl / per_img);
-        const int r = (int)(tl - (int64_t)n * per_img);
-        const int ty = r / a.tiles_x;
-        oy0 = ty * TR;
-        ox0 = (r - ty * a.tiles_x) * TC;
-    };
-    auto load_tile = [&](int64_t tl) {
-        int n, oy0, ox0;
-        tile_origin(tl, n, oy0, ox0);
-        const int oy = oy0 + apy, ox = ox0 + apx;
-        const int pix = (oy < a.OH && ox < a.OW) ? oy * a.OW + ox : 0;
-#pragma unroll
-        for (int j = 0; j < NA; ++j) {
-            if (j < na) {  // wave-uniform
-                const VChan& c = tabA[wave + 4 * j];
-                if (DBG(a, 2)) { ra[j] = 1.f; ry[j] = 1.f; continue; }
-                ra[j] = gld(c.p, n * c.ns + pix);
-                if (AB) ry[j] = gld(c.y, n * c.yns + pix);
-            }
-        }
-        const int iy0 = oy0 * a.SH - a.PH, ix0 = ox0 * a.SW - a.PW;
-#pragma unroll
-        for (int j = 0; j < kPX; ++j) {
-            if (j < nxj) {  // block-uniform
-                const int v = xe[j];
-                const int iy = iy0 + ((v >> 10) & 1023), ix = ix0 + (v & 1023);
-                const bool ok = v >= 0 && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
-                const VChan& c = tabX[v >= 0 ? v >> 20 : 0];
-                const int o = ok ? iy * a.W + ix : 0;
-                if (DBG(a, 2)) { rx[j] = 1.f; rxy[j] = 1.f; continue; }
-                rx[j] = gld(c.p, n * c.ns + o);
-                if (XB) rxy[j] = gld(c.y, n * c.yns + o);
-            }
-        }
-    };
-    auto store_tile = [&](int64_t tl) {
-        int n, oy0, ox0;
-        tile_origin(tl, n, oy0, ox0);
-        const bool pv = oy0 + apy < a.OH && ox0 + apx < a.OW;
-#pragma unroll
-        for (int j = 0; j < NA; ++j) {
-            float v = 0.f;
-            if (j < na) {  // wave-uniform
-                const VChan& c = tabA[wave + 4 * j];
-                const float t = vchan_apply_sel(c, ra[j], AB ? ry[j] : 0.f);
-                v = pv ? t : 0.f;
-            }
-            As[(wave + 4 * j) * kAStride + ap] = v;
-        }
-        const int iy0 = oy0 * a.SH - a.PH, ix0 = ox0 * a.SW - a.PW;
-#pragma unroll
-        for (int j = 0; j < kPX; ++j) {
-            if (j < nxj) {  // block-uniform
-                const int v = xe[j];
-                const int cl = v >> 20, hr = (v >> 10) & 1023, hc = v & 1023;
-                const int iy = iy0 + hr, ix = ix0 + hc;
-                const bool ok = v >= 0 && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
-                const float t = vchan_apply_sel(tabX[v >= 0 ? cl : 0], rx[j], XB ? rxy[j] : 0.f);
-                if (v >= 0) Xs[cl * a.hsp + hr * a.HC + hc] = ok ? t : 0.f;
-            }
-        }
-    };
-
-    if (t0 < t1) load_tile(t0);
+    const TileCtx tc{per_img, TR, TC, apy, apx, lane, wave, Rb, nslots, tA, tX};
+    const int nrow_w = (Rb - wave + 3) / 4;  // this wave's dy rows
     for (int64_t tl = t0; tl < t1; ++tl) {
         __syncthreads();  // previous tile's LDS reads are done
-        store_tile(tl);
+        wg_stage<8>(a, tc, tl, nrow_w, As, Xs);
         __syncthreads();
         if (tl == t0) STAMP(2);
-        if (tl + 1 < t1) load_tile(tl + 1);  // in flight during this tile's MFMAs
         if (do_bias && tid < Rb) {
             const float* rowp = As + tid * kAStride;
             float s = 0.f;
@@ -298,7 +234,7 @@ __global__ __launch_bounds__(kThreads) void wgrad_kernel(WgArgs a) {
         }
         if (a.valu) {
             if (vxoff >= 0) {
-                const int q0 = (tid >> 6) * 16;
+                const int q0 = wave * 16;
 #pragma unroll
                 for (int p = q0; p < q0 + 16; ++p) {
                     const int poff = (p >> a.lgTC) * a.SH * a.HC + (p & (TC - 1)) * a.SW;
@@ -308,17 +244,23 @@ __global__ __launch_bounds__(kThreads) void wgrad_kernel(WgArgs a) {
             continue;
         }
         if (!kactive || DBG(a, 4)) continue;
-#pragma unroll 4
-        for (int kq = kq_lo; kq < kq_hi; kq += 4) {
-            const int p = kq + kk;
-            const int poff = (p >> a.lgTC) * a.SH * a.HC + (p & (TC - 1)) * a.SW;
+        if (!ksplit) {
+            // every wave owns TPW tiles (absent ones compute on row 0 and are never
+            // stored): branch-free, so the LDS reads batch ahead of the MFMAs
 #pragma unroll
-            for (int i = 0; i < TPW; ++i) {
-                if (arow[i] >= 0) {  // wave-uniform
-                    const float av = As[arow[i] + p];
-                    const float bv = xoff[i] >= 0 ? Xs[xoff[i] + poff] : 0.f;
+            for (int s = 0; s < kTP / 4; ++s)
+#pragma unroll
+                for (int i = 0; i < TPW; ++i) {
+                    const float av = As[arow[i] + 4 * s + kk];
+                    const float bv = Xs[xoff[i] + poffs[s]];
                     acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[i], 0, 0, 0);
                 }
+        } else {
+            for (int s = s_lo; s < s_hi; ++s) {
+                const float av = As[arow[0] + 4 * s + kk];
+                const int p = 4 * s + kk;
+                const float bv = Xs[xoff[0] + (p >> a.lgTC) * a.SH * a.HC + (p & (TC - 1)) * a.SW];
+                acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[0], 0, 0, 0);
             }
         }
     }
@@ -391,20 +333,24 @@ int32_t isg_dense_conv_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, cons
     const int KK = g->KH * g->KW;
     const int ncol = g->Ci * KK;
     const int CT = (ncol + 15) / 16;
-    // tile shape: 1x64 rows for stride-1 1x1 convs on wide maps, else 4x16
+    // tile width: 64 pixels of a row for stride-1 1x1 convs on wide maps, else 16 (a
+    // 4x16 tile), narrowed until the halo row fits the 64 lanes
     const bool pw = KK == 1 && g->SH == 1 && g->SW == 1;
-    a.lgTC = (pw && g->OW >= 64) ? 6 : (g->OW >= 32 && pw ? 5 : 4);
-    const int TC = 1 << a.lgTC, TR = kTP / TC;
+    int tc = pw ? (g->OW >= 64 ? 64 : (g->OW >= 32 ? 32 : 16)) : 16;
+    auto hc_of = [&](int t) { return (t - 1) * g->SW + (g->KW - 1) * g->DW + 1; };
+    while (tc > 8 && hc_of(tc) > 64) tc /= 2;
+    if (hc_of(tc) > 64)
+        return isg_set_error(ISG_ERR_UNSUPPORTED, "conv wgrad: halo row %d > 64", hc_of(tc));
+    a.lgTC = tc == 64 ? 6 : (tc == 32 ? 5 : (tc == 16 ? 4 : 3));
+    const int TC = tc, TR = kTP / TC;
     a.HR = (TR - 1) * g->SH + (g->KH - 1) * g->DH + 1;
-    a.HC = (TC - 1) * g->SW + (g->KW - 1) * g->DW + 1;
-    if (a.HR >= 1024 || a.HC >= 1024)
-        return isg_set_error(ISG_ERR_UNSUPPORTED, "conv wgrad: halo %dx%d", a.HR, a.HC);
+    a.HC = hc_of(tc);
     const int hs = a.HR * a.HC;
     a.hsp = hs + ((2 - hs % 32) + 32) % 32;  // channel stride = 2 mod 32 banks
     a.valu = g->Co == 1 ? 1 : 0;
     const int nrt = (std::min(g->Co, kRowsBlk) + 15) / 16;
     a.BMT = nrt;
-    // widest column block whose halo fits the per-thread prefetch budget
+    // widest column block whose halo fits the slot budget
     auto max_nci = [&](int bnt) {
         int m = 0;
         for (int c_lo = 0; c_lo < ncol; c_lo += bnt * 16) {
@@ -413,13 +359,16 @@ int32_t isg_dense_conv_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, cons
         }
         return m;
     };
-    int bnt = a.valu ? 4 : std::min(CT, std::max(1, 16 / nrt));
+    auto fits = [&](int bnt) {
+        const int m = max_nci(bnt);
+        return m <= kMaxXCh && m * a.hsp <= kXs;
+    };
+    int bnt = a.valu ? 4 : std::min(CT, std::max(1, 32 / nrt));
     bnt = std::min(bnt, kColsBlk / 16);
-    while (bnt > 1 && (max_nci(bnt) * a.hsp > kHaloMax || max_nci(bnt) > kMaxXCh)) --bnt;
-    const int mnci = max_nci(bnt);
-    if (mnci * a.hsp > kHaloMax || mnci > kMaxXCh || mnci * hs > kHaloMax)
-        return isg_set_error(ISG_ERR_UNSUPPORTED, "conv wgrad: halo %d x %d too large", mnci, hs);
-    if (a.valu && bnt * 16 > 64) bnt = 4;
+    while (bnt > 1 && !fits(bnt)) --bnt;
+    if (!fits(bnt))
+        return isg_set_error(ISG_ERR_UNSUPPORTED, "conv wgrad: halo %d rows x %d too large",
+                             a.HR, a.HC);
     a.BNT = bnt;
     a.ncb = (ncol + bnt * 16 - 1) / (bnt * 16);
     const int nrb = (g->Co + kRowsBlk - 1) / kRowsBlk;
@@ -434,27 +383,17 @@ int32_t isg_dense_conv_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, cons
 #ifdef ISG_STAMPS
     { const char* e = getenv("ISG_DBG"); a.dbg = e ? atoi(e) : 0; }
 #endif
-    const int hs2 = a.HR * a.HC;
-    a.m_hs = (unsigned)(((1ull << 32) + hs2 - 1) / hs2);
-    a.m_hc = (unsigned)(((1ull << 32) + a.HC - 1) / a.HC);
-    bool xb = false;
-    for (int i = 0; i < x->nseg; ++i) xb = xb || x->s[i].xform == ISG_XF_BN_BWD;
-    bool ab = false;
-    for (int i = 0; i < dy->nseg; ++i) ab = ab || dy->s[i].xform == ISG_XF_BN_BWD;
     dim3 grid((unsigned)gx, (unsigned)gy);
-#define WG_LAUNCH(M, A, B) hipLaunchKernelGGL((wgrad_kernel<M, A, B>), grid, dim3(kThreads), 0, st, a)
-#define WG_LAUNCH_M(A, B)                        \
-    switch (a.BMT) {                             \
-        case 1: WG_LAUNCH(1, A, B); break;       \
-        case 2: WG_LAUNCH(2, A, B); break;       \
-        case 3: WG_LAUNCH(3, A, B); break;       \
-        default: WG_LAUNCH(4, A, B); break;      \
+    const int tpw = (a.BMT * a.BNT + 3) / 4;
+#define WG_LAUNCH(T) hipLaunchKernelGGL((wgrad_kernel<T>), grid, dim3(kThreads), 0, st, a)
+    switch (tpw) {
+        case 1: WG_LAUNCH(1); break;
+        case 2: WG_LAUNCH(2); break;
+        case 3: WG_LAUNCH(3); break;
+        case 4: WG_LAUNCH(4); break;
+        case 5: case 6: WG_LAUNCH(6); break;
+        default: WG_LAUNCH(8); break;
     }
-    if (ab && xb) WG_LAUNCH_M(true, true)
-    else if (ab) WG_LAUNCH_M(true, false)
-    else if (xb) WG_LAUNCH_M(false, true)
-    else WG_LAUNCH_M(false, false)
-#undef WG_LAUNCH_M
 #undef WG_LAUNCH
     return isg_check_launch("wgrad_kernel");
 }
