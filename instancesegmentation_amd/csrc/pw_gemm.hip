@@ -6,38 +6,43 @@
 //   D[m][p] = sum_k A[m][k] * Bv[k][p]     A[m][k] = w[m*rs + k*cs]
 //     forward: m = co, k = ci (rs = Ci, cs = 1);  dgrad: m = ci, k = co (rs = 1, cs = Ci)
 //
-// A workgroup owns a BM x BP tile (BM rows = WM waves x 16*MT, BP pixels = WP waves x
-// 16*GP). The activation tile is staged once into LDS in 64-channel chunks with the
-// producer's BN/activation (or BN-backward rebuild) applied on load, coalesced along
-// pixels; waves read B fragments from LDS and A fragments (weights, L1/L2-resident)
-// from global. Sink routing per output row (segment / mode / BN coefficients) is
-// resolved once per workgroup into LDS so the epilogue is branch-light.
-#include "common.h"
+// A workgroup owns BM (64 or 128) rows x 64 pixels. K is processed in chunks of 32:
+//   * activations: wave w stages channels w, w+4, ... of the chunk (wave-uniform channel,
+//     lane = pixel, one coalesced 256-B row per load), the producer's BatchNorm/activation
+//     (or BatchNorm-backward rebuild) applied on the way into LDS (stage.h records);
+//   * weights: the BM x 32 slice, coalesced along whichever of m / k is contiguous.
+// The MFMA loop is branch-free and reads both operands from LDS (padded strides: A rows
+// = 2 mod 32 banks, B rows = 16 mod 32). The epilogue routes each output row through its
+// sink (store + bias + BN statistics, accumulate, or activation backward with the
+// BN-backward sums), resolved once per workgroup into LDS.
+#include "stage.h"
 
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kKC = 32;        // channels per LDS chunk
-constexpr int kMaxCh = 256;    // M, K limit (larger shapes take the generic path)
+constexpr int kKC = 32;              // channels per K chunk
+constexpr int kBP = 64;              // pixels per block
 constexpr int kMaxBM = 128;
-constexpr int kMaxBP = 128;
+constexpr int kMaxK = 256;
+constexpr int kWst = kKC + 2;        // Ws row stride (2 mod 32)
+constexpr int kXst = kBP + 16;       // Xs row stride (16 mod 32)
 
 struct PwArgs {
     isg_vtensor src;
     isg_sinks out;
     const float* w;
     int rs, cs;
-    int N, HW, M, K;
-    int WM, WP;
+    int N, HW, M, K, BM;
     int64_t P;
 };
 
 struct RowInfo {
     float* p;
     const float* y;
-    int64_t ns, yns;
-    int mode, act, sink;
+    int ns, yns;
+    int mode, act;
     float bias;
+    int pad_;
     SinkCoef f;
 };
 
@@ -53,41 +58,41 @@ ISG_DEV float row16_sum(float v) {
     return v;
 }
 
-template <int MT, int GP>
+// TPW: 16x16 accumulator tiles per wave = (BM/16 row tiles x 4 pixel tiles) / 4 waves
+template <int TPW>
 __global__ __launch_bounds__(kThreads) void pw_kernel(PwArgs a) {
-    constexpr int XST = kMaxBP + 4;
-    __shared__ float Xs[kKC][XST];
-    __shared__ ChanCoef coef[kMaxCh];
+    __shared__ float Xs[kKC * kXst];
+    __shared__ float Ws[kMaxBM * kWst];
+    __shared__ ChT tab[kMaxK];
     __shared__ RowInfo ri[kMaxBM];
-    __shared__ SinkCoef scoef[kMaxCh];
+    __shared__ SinkCoef scoef[kMaxK];
     __shared__ float red[3][kMaxBM];
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = wave_id();
     const int kk = lane >> 4, pl = lane & 15;
-    const int BM = a.WM * 16 * MT, BP = a.WP * 16 * GP;
+    const int BM = a.BM;
     const int m0 = blockIdx.y * BM;
-    const int64_t p0 = (int64_t)blockIdx.x * BP;
-    const int wm = wave % a.WM, wp = wave / a.WM;
-    const bool active = wp < a.WP;
+    const int Mb = min(BM, a.M - m0);
+    const int64_t p0 = (int64_t)blockIdx.x * kBP;
 
-    load_vt_coefs(a.src, coef, tid, kThreads);
+    for (int c = tid; c < a.K; c += kThreads) tab[c] = ch_table_entry(a.src, c, a.HW);
     load_sink_coefs(a.out, scoef, tid, kThreads);
     __syncthreads();
     for (int r = tid; r < BM; r += kThreads) {
         const int m = m0 + r;
         RowInfo q = {};
         q.mode = -1;
-        if (m < a.M) {
+        if (r < Mb) {
             const int s = sink_of(a.out, m);
-            const isg_sink& k = a.out.s[s];
+            const isg_sink& k = s == 2 ? a.out.s[2] : (s == 1 ? a.out.s[1] : a.out.s[0]);
             const int cl = m - k.c0;
             q.p = k.p ? k.p + (int64_t)cl * a.HW : nullptr;
             q.y = k.y ? k.y + (int64_t)cl * a.HW : nullptr;
-            q.ns = k.n_stride;
-            q.yns = k.y_n_stride;
+            q.ns = (int)k.n_stride;
+            q.yns = (int)k.y_n_stride;
             q.mode = k.mode;
             q.act = k.act;
-            q.sink = s;
             q.bias = k.bias ? k.bias[cl] : 0.f;
             q.f = scoef[m];
         }
@@ -95,120 +100,134 @@ __global__ __launch_bounds__(kThreads) void pw_kernel(PwArgs a) {
         red[0][r] = red[1][r] = red[2][r] = 0.f;
     }
 
-    f32x4 acc[GP][MT];
+    // this lane's pixel of the block (staging) — the block never crosses an image when
+    // HW % 64 == 0, otherwise per-lane image split
+    const int64_t pg_l = p0 + lane;
+    const bool pv_l = pg_l < a.P;
+    const int n_l = pv_l ? (int)(pg_l / a.HW) : 0;
+    const int pix_l = pv_l ? (int)(pg_l - (int64_t)n_l * a.HW) : 0;
+
+    // accumulator tiles: t = wave + 4i -> row tile t>>2, pixel tile t&3
+    int arow[TPW], bcol[TPW];
 #pragma unroll
-    for (int g = 0; g < GP; ++g)
+    for (int i = 0; i < TPW; ++i) {
+        const int t = wave + 4 * i;
+        arow[i] = ((t >> 2) * 16 + pl) * kWst;
+        bcol[i] = (t & 3) * 16 + pl;
+    }
+    f32x4 acc[TPW];
 #pragma unroll
-        for (int t = 0; t < MT; ++t) acc[g][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < TPW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     const float* __restrict__ w = a.w;
+    const bool wk_contig = a.cs == 1;  // weight row m contiguous along k (forward)
     for (int kc = 0; kc < a.K; kc += kKC) {
         const int kn = min(kKC, a.K - kc);
-        __syncthreads();
-        for (int idx = tid; idx < kn * BP; idx += kThreads) {
-            const int k = idx / BP, pp = idx - k * BP;
-            const int64_t pg = p0 + pp;
-            float v = 0.f;
-            if (pg < a.P) {
-                const int n = (int)(pg / a.HW);
-                v = vt_load(a.src, coef, n, kc + k, a.HW, pg - (int64_t)n * a.HW);
+        __syncthreads();  // previous chunk consumed
+        // activations: 8 channels per wave, all loads in flight together
+        {
+            float v[kKC / 4], yv[kKC / 4];
+#pragma unroll
+            for (int u = 0; u < kKC / 4; ++u) {
+                const int k = min(wave + 4 * u, kn - 1);
+                const ChT c = tab[kc + k];
+                v[u] = gld(c.p, n_l * c.ns + pix_l);
+                yv[u] = gld(c.y, n_l * c.yns + pix_l);
             }
-            Xs[k][pp] = v;
+#pragma unroll
+            for (int u = 0; u < kKC / 4; ++u) {
+                const int k = wave + 4 * u;
+                const ChT c = tab[kc + min(k, kn - 1)];
+                const float t = ch_xform(c.xf, c.act, c.k, v[u], yv[u]);
+                Xs[k * kXst + lane] = (k < kn && pv_l) ? t : 0.f;
+            }
+        }
+        // weights: BM x 32 slice (rows past Mb and k past kn are zero)
+        for (int idx = tid; idx < BM * kKC; idx += kThreads) {
+            int m, k;
+            if (wk_contig) { m = idx / kKC; k = idx - m * kKC; }
+            else { k = idx / BM; m = idx - k * BM; }
+            float v = 0.f;
+            if (m < Mb && k < kn) v = gld(w, (int64_t)(m0 + m) * a.rs + (int64_t)(kc + k) * a.cs);
+            Ws[m * kWst + k] = v;
         }
         __syncthreads();
-        if (active) {
-#pragma unroll 4
-            for (int k0 = 0; k0 < kn; k0 += 4) {
-                const int k = k0 + kk;
-                const bool kv = k < kn;
-                float av[MT];
 #pragma unroll
-                for (int t = 0; t < MT; ++t) {
-                    const int m = m0 + wm * 16 * MT + t * 16 + pl;
-                    av[t] = (kv && m < a.M) ? w[(int64_t)m * a.rs + (int64_t)(kc + k) * a.cs] : 0.f;
-                }
+        for (int ks = 0; ks < kKC / 4; ++ks) {
 #pragma unroll
-                for (int g = 0; g < GP; ++g) {
-                    const float bv = kv ? Xs[k][wp * 16 * GP + g * 16 + pl] : 0.f;
-#pragma unroll
-                    for (int t = 0; t < MT; ++t)
-                        acc[g][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t], bv, acc[g][t], 0, 0, 0);
-                }
+            for (int i = 0; i < TPW; ++i) {
+                const float av = Ws[arow[i] + ks * 4 + kk];
+                const float bv = Xs[(ks * 4 + kk) * kXst + bcol[i]];
+                acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[i], 0, 0, 0);
             }
         }
     }
 
-    // ---- epilogue ----------------------------------------------------------------------
-    if (active) {
-        float s0[MT][4], s1[MT][4], s2[MT][4];
+    // ---- epilogue: lane holds D[row = rt*16 + kk*4 + r][pixel = ct*16 + pl] ------------
+    const bool need_red = sinks_need_red(a.out);
 #pragma unroll
-        for (int t = 0; t < MT; ++t)
+    for (int i = 0; i < TPW; ++i) {
+        const int t = wave + 4 * i;
+        const int rt = t >> 2, ct = t & 3;
+        if (rt * 16 >= Mb) continue;  // wave-uniform
+        const int64_t pg = p0 + ct * 16 + pl;
+        const bool pv = pg < a.P;
+        const int n = pv ? (int)(pg / a.HW) : 0;
+        const int pix = pv ? (int)(pg - (int64_t)n * a.HW) : 0;
+        float s0[4], s1[4], s2[4];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) s0[t][r] = s1[t][r] = s2[t][r] = 0.f;
-#pragma unroll
-        for (int g = 0; g < GP; ++g) {
-            const int64_t pg = p0 + wp * 16 * GP + g * 16 + pl;
-            const bool pv = pg < a.P;
-            const int n = pv ? (int)(pg / a.HW) : 0;
-            const int64_t pix = pg - (int64_t)n * a.HW;
-#pragma unroll
-            for (int t = 0; t < MT; ++t)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int rl = wm * 16 * MT + t * 16 + kk * 4 + r;
-                    const RowInfo& q = ri[rl];
-                    if (!pv || q.mode < 0 || q.mode == ISG_SINK_NONE) continue;
-                    float v = acc[g][t][r];
-                    float* dst = q.p + (int64_t)n * q.ns + pix;
-                    if (q.mode == ISG_SINK_STORE) {
-                        v += q.bias;
-                        *dst = v;
-                        s0[t][r] += v;
-                        s1[t][r] += v * v;
-                    } else if (q.mode == ISG_SINK_ACCUM) {
-                        *dst += v;
-                        s0[t][r] += v;
-                        s1[t][r] += v * v;
-                    } else {
-                        const float y = q.y[(int64_t)n * q.yns + pix];
-                        const float z = (y - q.f.mean) * q.f.scale + q.f.beta;
-                        float gv = v;
-                        if (q.act == ISG_ACT_RELU) {
-                            gv = z > 0.f ? v : 0.f;
-                        } else if (q.act == ISG_ACT_PRELU) {
-                            gv = z > 0.f ? v : v * q.f.slope;
-                            s2[t][r] += z > 0.f ? 0.f : z * v;
-                        }
-                        *dst = gv;
-                        s0[t][r] += gv;
-                        s1[t][r] += gv * (y - q.f.mean);
-                    }
+        for (int r = 0; r < 4; ++r) {
+            s0[r] = s1[r] = s2[r] = 0.f;
+            const int rl = rt * 16 + kk * 4 + r;
+            const RowInfo& q = ri[rl];
+            if (!pv || q.mode < 0 || q.mode == ISG_SINK_NONE) continue;
+            float v = acc[i][r];
+            const int off = n * q.ns + pix;
+            if (q.mode == ISG_SINK_STORE) {
+                v += q.bias;
+                gst(q.p, off, v);
+                s0[r] = v;
+                s1[r] = v * v;
+            } else if (q.mode == ISG_SINK_ACCUM) {
+                gst(q.p, off, gld(q.p, off) + v);
+                s0[r] = v;
+                s1[r] = v * v;
+            } else {
+                const float y = gld(q.y, n * q.yns + pix);
+                const float z = (y - q.f.mean) * q.f.scale + q.f.beta;
+                float gv = v;
+                if (q.act == ISG_ACT_RELU) {
+                    gv = z > 0.f ? v : 0.f;
+                } else if (q.act == ISG_ACT_PRELU) {
+                    gv = z > 0.f ? v : v * q.f.slope;
+                    s2[r] = z > 0.f ? 0.f : z * v;
                 }
+                gst(q.p, off, gv);
+                s0[r] = gv;
+                s1[r] = gv * (y - q.f.mean);
+            }
         }
-        if (sinks_need_red(a.out)) {
+        if (need_red) {
 #pragma unroll
-            for (int t = 0; t < MT; ++t)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const float t0 = row16_sum(s0[t][r]);
-                    const float t1 = row16_sum(s1[t][r]);
-                    const float t2 = row16_sum(s2[t][r]);
-                    const int rl = wm * 16 * MT + t * 16 + kk * 4 + r;
-                    if (pl == 0 && m0 + rl < a.M) {
-                        atomicAdd(&red[0][rl], t0);
-                        atomicAdd(&red[1][rl], t1);
-                        atomicAdd(&red[2][rl], t2);
-                    }
+            for (int r = 0; r < 4; ++r) {
+                const float t0 = row16_sum(s0[r]);
+                const float t1 = row16_sum(s1[r]);
+                const float t2 = row16_sum(s2[r]);
+                const int rl = rt * 16 + kk * 4 + r;
+                if (pl == 0 && rl < Mb) {
+                    atomicAdd(&red[0][rl], t0);
+                    atomicAdd(&red[1][rl], t1);
+                    atomicAdd(&red[2][rl], t2);
                 }
+            }
         }
     }
-    if (sinks_need_red(a.out)) {
+    if (need_red) {
         __syncthreads();
-        for (int rl = tid; rl < BM; rl += kThreads) {
+        for (int rl = tid; rl < Mb; rl += kThreads) {
             const int m = m0 + rl;
-            if (m >= a.M) continue;
             const int s = sink_of(a.out, m);
-            const isg_sink& k = a.out.s[s];
+            const isg_sink& k = s == 2 ? a.out.s[2] : (s == 1 ? a.out.s[1] : a.out.s[0]);
             const int cl = m - k.c0;
             if (k.mode == ISG_SINK_STORE || k.mode == ISG_SINK_ACCUM) {
                 if (k.stats) {
@@ -245,22 +264,25 @@ int32_t isg_pw_gemm(const isg_conv_geom* g, const isg_vtensor* src, const float*
     a.rs = dgrad ? 1 : g->Ci;
     a.cs = dgrad ? g->Ci : 1;
     a.P = (int64_t)g->N * a.HW;
-    if (a.K > kMaxCh || a.M > kMaxCh)
-        return isg_set_error(ISG_ERR_UNSUPPORTED, "pw gemm: %d x %d channels", a.M, a.K);
-    // shape the workgroup: rows first (MT = 2 when there are >= 32 rows), then pixels
-    const int mt = a.M > 16 ? 2 : 1;
-    const int mtiles = (a.M + 16 * mt - 1) / (16 * mt);
-    a.WM = mtiles >= 4 ? 4 : (mtiles >= 2 ? 2 : 1);
-    a.WP = 4 / a.WM;
-    // pixels per wave: 32 when the grid stays large, else 16
-    const int64_t blocks32 = ((a.P + a.WP * 32 - 1) / (a.WP * 32)) *
-                             ((a.M + a.WM * 16 * mt - 1) / (a.WM * 16 * mt));
-    const int gp = blocks32 >= 512 ? 2 : 1;
-    const int BM = a.WM * 16 * mt, BP = a.WP * 16 * gp;
-    dim3 grid((unsigned)((a.P + BP - 1) / BP), (unsigned)((a.M + BM - 1) / BM));
-    if (mt == 1 && gp == 1) hipLaunchKernelGGL((pw_kernel<1, 1>), grid, dim3(kThreads), 0, st, a);
-    else if (mt == 1) hipLaunchKernelGGL((pw_kernel<1, 2>), grid, dim3(kThreads), 0, st, a);
-    else if (gp == 1) hipLaunchKernelGGL((pw_kernel<2, 1>), grid, dim3(kThreads), 0, st, a);
-    else hipLaunchKernelGGL((pw_kernel<2, 2>), grid, dim3(kThreads), 0, st, a);
+    if (a.K > kMaxK)
+        return isg_set_error(ISG_ERR_UNSUPPORTED, "pw gemm: K = %d channels > %d", a.K, kMaxK);
+    if (a.M > 2 * kMaxBM)
+        return isg_set_error(ISG_ERR_UNSUPPORTED, "pw gemm: M = %d rows", a.M);
+    const int64_t pblocks = (a.P + kBP - 1) / kBP;
+    // rows per block: up to 128, halved while that keeps more workgroups in flight
+    int bm = std::min(kMaxBM, (a.M + 15) / 16 * 16);
+    while (bm > 16 && pblocks * ((a.M + bm - 1) / bm) < 512) bm = (bm / 2 + 15) / 16 * 16;
+    a.BM = bm;
+    const int tpw = bm / 16;  // (bm/16 row tiles * 4 pixel tiles) / 4 waves
+    dim3 grid((unsigned)pblocks, (unsigned)((a.M + bm - 1) / bm));
+    // template tile count >= tpw; surplus tiles compute on unused rows, never stored
+    switch (tpw) {
+        case 1: hipLaunchKernelGGL(pw_kernel<1>, grid, dim3(kThreads), 0, st, a); break;
+        case 2: hipLaunchKernelGGL(pw_kernel<2>, grid, dim3(kThreads), 0, st, a); break;
+        case 3: hipLaunchKernelGGL(pw_kernel<3>, grid, dim3(kThreads), 0, st, a); break;
+        case 4: hipLaunchKernelGGL(pw_kernel<4>, grid, dim3(kThreads), 0, st, a); break;
+        case 5: case 6: hipLaunchKernelGGL(pw_kernel<6>, grid, dim3(kThreads), 0, st, a); break;
+        default: hipLaunchKernelGGL(pw_kernel<8>, grid, dim3(kThreads), 0, st, a); break;
+    }
     return isg_check_launch("pw_kernel");
 }
