@@ -12,7 +12,7 @@
 //
 // MFMA maps (16x16x4 f32): A[i=co][k] = W (lane: co = l&15, k = l>>4),
 // B[k][j=pixel] = halo (lane: k = l>>4, pixel = l&15), D lane holds co = (l>>4)*4+r.
-#include "common.h"
+#include "stage.h"
 
 namespace {
 
@@ -20,6 +20,7 @@ constexpr int kThreads = 256;
 constexpr int kTW = 32;        // output tile width
 constexpr int kKMax = 512;     // K entries per chunk (channels_in_chunk * KH * KW)
 constexpr int kHaloMax = 6144; // floats of halo per chunk
+constexpr int kMaxCi = 64;     // channel records per block
 
 struct HaloArgs {
     isg_vtensor x;
@@ -49,10 +50,10 @@ __global__ __launch_bounds__(kThreads) void halo_conv_kernel(HaloArgs a) {
     __shared__ float Xs[kHaloMax];
     __shared__ float Ws[MT * 16 * kKMax / 4 + 16];  // chunk weights [co][k] (k <= cic*KK)
     __shared__ int koff[kKMax];
-    __shared__ ChanCoef coef[ISG_MAX_CH];
-    __shared__ float red[2][MT * 16];
+    __shared__ ChT tab[kMaxCi];
+    __shared__ float red[4][2][MT * 16];  // per-wave partials: fixed-order sum
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
     const int kk = lane >> 4, pl = lane & 15;
     const int KK = a.KH * a.KW;
     const int n = blockIdx.x / (a.tiles_x * a.tiles_y);
@@ -60,10 +61,12 @@ __global__ __launch_bounds__(kThreads) void halo_conv_kernel(HaloArgs a) {
     const int oy0 = (tr / a.tiles_x) * THO, ox0 = (tr % a.tiles_x) * kTW;
     const int iy0 = oy0 * a.SH - a.PH, ix0 = ox0 * a.SW - a.PW;
     const int hsz = a.HR * a.HC;
-    const int wst = a.cic * KK + 1;  // Ws row stride (odd: fewer bank conflicts)
+    const int wst = ((a.cic * KK + 3) & ~3) + 1;  // Ws row stride (odd), holds the k padding
 
-    load_vt_coefs(a.x, coef, tid, kThreads);
-    for (int i = tid; i < MT * 16; i += kThreads) red[0][i] = red[1][i] = 0.f;
+    for (int c = tid; c < a.Ci; c += kThreads) tab[c] = ch_table_entry(a.x, c, a.H * a.W);
+    for (int i = tid; i < MT * 16; i += kThreads)
+#pragma unroll
+        for (int wv = 0; wv < 4; ++wv) red[wv][0][i] = red[wv][1][i] = 0.f;
 
     // per-lane pixel offsets inside the halo for each of the wave's groups
     int poff[G];
@@ -79,26 +82,49 @@ __global__ __launch_bounds__(kThreads) void halo_conv_kernel(HaloArgs a) {
 #pragma unroll
         for (int m = 0; m < MT; ++m) acc[gi][m] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    const int64_t xhw = (int64_t)a.H * a.W;
+    const int npass = (a.HC + 63) >> 6;  // lane passes per halo row
     for (int c0 = 0; c0 < a.Ci; c0 += a.cic) {
         const int nc = min(a.cic, a.Ci - c0);
         const int K = nc * KK;
-        __syncthreads();  // previous chunk fully consumed
-        for (int idx = tid; idx < nc * hsz; idx += kThreads) {
-            const int cl = idx / hsz, rem = idx - cl * hsz;
-            const int hr = rem / a.HC, hc = rem - hr * a.HC;
-            const int iy = iy0 + hr, ix = ix0 + hc;
-            float v = 0.f;
-            if (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
-                v = vt_load(a.x, coef, n, c0 + cl, xhw, (int64_t)iy * a.W + ix);
-            Xs[idx] = v;
+        const int Kp = (K + 3) & ~3;
+        __syncthreads();  // previous chunk fully consumed (tab ready on the first pass)
+        // halo: item = (channel, halo row, lane pass), wave-uniform; lane = column.
+        // Groups of 8 items per wave with all loads in flight together.
+        const int nitems = nc * a.HR * npass;
+        for (int i0 = wave; i0 < nitems; i0 += 32) {
+            float v[8], yv[8];
+            bool ok[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int it = min(i0 + 4 * u, nitems - 1);
+                const int cr = it / npass, pass = it - cr * npass;
+                const int cl = cr / a.HR, hr = cr - cl * a.HR;
+                const ChT c = tab[c0 + cl];
+                const int iy = iy0 + hr, hc = pass * 64 + lane, ix = ix0 + hc;
+                ok[u] = hc < a.HC && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+                const int o = ok[u] ? iy * a.W + ix : 0;
+                v[u] = gld(c.p, n * c.ns + o);
+                yv[u] = gld(c.y, n * c.yns + o);
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int it = i0 + 4 * u;
+                if (it < nitems) {
+                    const int cr = it / npass, pass = it - cr * npass;
+                    const int cl = cr / a.HR, hr = cr - cl * a.HR;
+                    const ChT c = tab[c0 + cl];
+                    const int hc = pass * 64 + lane;
+                    if (hc < a.HC)
+                        Xs[cl * hsz + hr * a.HC + hc] = ok[u] ? ch_xform(c.xf, c.act, c.k, v[u], yv[u]) : 0.f;
+                }
+            }
         }
-        for (int idx = tid; idx < MT * 16 * K; idx += kThreads) {
-            const int co = idx / K, k = idx - co * K;
-            Ws[co * wst + k] = co < a.Co ? a.w[((int64_t)co * a.Ci + c0) * KK + k] : 0.f;
+        for (int idx = tid; idx < MT * 16 * Kp; idx += kThreads) {
+            const int co = idx / Kp, k = idx - co * Kp;
+            Ws[co * wst + k] = (co < a.Co && k < K) ? gld(a.w, ((int64_t)co * a.Ci + c0) * KK + k) : 0.f;
         }
-        for (int k = tid; k < ((K + 3) & ~3); k += kThreads) {
-            int o = -1;
+        for (int k = tid; k < Kp; k += kThreads) {
+            int o = 0;  // padding k: weight 0, any valid halo offset
             if (k < K) {
                 const int cl = k / KK, t = k - cl * KK;
                 const int kh = t / a.KW, kw = t - kh * a.KW;
@@ -107,15 +133,16 @@ __global__ __launch_bounds__(kThreads) void halo_conv_kernel(HaloArgs a) {
             koff[k] = o;
         }
         __syncthreads();
-        for (int k0 = 0; k0 < K; k0 += 4) {
+#pragma unroll 2
+        for (int k0 = 0; k0 < Kp; k0 += 4) {
             const int k = k0 + kk;
             const int o = koff[k];
             float av[MT];
 #pragma unroll
-            for (int m = 0; m < MT; ++m) av[m] = (o >= 0) ? Ws[(m * 16 + pl) * wst + k] : 0.f;
+            for (int m = 0; m < MT; ++m) av[m] = Ws[(m * 16 + pl) * wst + k];
 #pragma unroll
             for (int gi = 0; gi < G; ++gi) {
-                const float bv = (o >= 0) ? Xs[o + poff[gi]] : 0.f;
+                const float bv = Xs[o + poff[gi]];
 #pragma unroll
                 for (int m = 0; m < MT; ++m)
                     acc[gi][m] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m], bv, acc[gi][m], 0, 0, 0);
@@ -162,15 +189,17 @@ __global__ __launch_bounds__(kThreads) void halo_conv_kernel(HaloArgs a) {
                 const float t1 = row16_sum(s1[m][r]);
                 const int co = m * 16 + kk * 4 + r;
                 if (pl == 0 && co < a.Co) {
-                    atomicAdd(&red[0][co], t0);
-                    atomicAdd(&red[1][co], t1);
+                    red[wave][0][co] = t0;
+                    red[wave][1][co] = t1;
                 }
             }
         __syncthreads();
         double* sp = rep_ptr(o.stats, 4 * o.C);
         for (int co = tid; co < a.Co; co += kThreads) {
-            atomicAdd(&sp[co], (double)red[0][co]);
-            atomicAdd(&sp[o.C + co], (double)red[1][co]);
+            const float t0 = ((red[0][0][co] + red[1][0][co]) + red[2][0][co]) + red[3][0][co];
+            const float t1 = ((red[0][1][co] + red[1][1][co]) + red[2][1][co]) + red[3][1][co];
+            atomicAdd(&sp[co], (double)t0);
+            atomicAdd(&sp[o.C + co], (double)t1);
         }
     }
 }
@@ -180,7 +209,8 @@ __global__ __launch_bounds__(kThreads) void halo_conv_kernel(HaloArgs a) {
 // Returns 1 if handled, 0 if the shape is not for this kernel, <0 on error.
 int32_t isg_halo_conv_fwd(const isg_conv_geom* g, const isg_vtensor* x, const float* w,
                           const isg_sinks* out, hipStream_t st) {
-    if (g->groups != 1 || g->Co > 32 || out->nsink != 1 || out->s[0].mode != ISG_SINK_STORE ||
+    if (g->groups != 1 || g->Co > 32 || g->Ci > kMaxCi || out->nsink != 1 ||
+        out->s[0].mode != ISG_SINK_STORE ||
         (g->KH == 1 && g->KW == 1 && g->SH == 1 && g->SW == 1))
         return 0;
     const int KK = g->KH * g->KW;
@@ -198,8 +228,11 @@ int32_t isg_halo_conv_fwd(const isg_conv_geom* g, const isg_vtensor* x, const fl
     a.DH = g->DH; a.DW = g->DW; a.HR = HR; a.HC = HC;
     const int mt = g->Co <= 16 ? 1 : 2;
     int cic = kHaloMax / (HR * HC);
-    cic = std::min(cic, kKMax / KK);
-    cic = std::min(cic, (mt * 16 * kKMax / 4) / (mt * 16 * KK + 1));  // weight chunk fits Ws
+    auto wfit = [&](int c) {  // padded K fits koff and the weight chunk fits Ws
+        const int kp = (c * KK + 3) & ~3;
+        return kp <= kKMax && mt * 16 * (kp + 1) <= mt * 16 * kKMax / 4 + 16;
+    };
+    while (cic > 1 && !wfit(cic)) --cic;
     cic = std::max(1, std::min(cic, g->Ci));
     a.cic = cic;
     a.tiles_x = (g->OW + kTW - 1) / kTW;

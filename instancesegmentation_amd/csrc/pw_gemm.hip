@@ -25,6 +25,7 @@ constexpr int kBP = 64;              // pixels per block
 constexpr int kMaxBM = 128;
 constexpr int kMaxK = 256;
 constexpr int kWst = kKC + 2;        // Ws row stride (2 mod 32)
+static_assert(kMaxBM * kWst >= 4 * 3 * kMaxBM, "BN partials alias the weight tile");
 constexpr int kXst = kBP + 16;       // Xs row stride (16 mod 32)
 
 struct PwArgs {
@@ -65,8 +66,6 @@ __global__ __launch_bounds__(kThreads) void pw_kernel(PwArgs a) {
     __shared__ float Ws[kMaxBM * kWst];
     __shared__ ChT tab[kMaxK];
     __shared__ RowInfo ri[kMaxBM];
-    __shared__ SinkCoef scoef[kMaxK];
-    __shared__ float red[3][kMaxBM];
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = wave_id();
@@ -77,8 +76,6 @@ __global__ __launch_bounds__(kThreads) void pw_kernel(PwArgs a) {
     const int64_t p0 = (int64_t)blockIdx.x * kBP;
 
     for (int c = tid; c < a.K; c += kThreads) tab[c] = ch_table_entry(a.src, c, a.HW);
-    load_sink_coefs(a.out, scoef, tid, kThreads);
-    __syncthreads();
     for (int r = tid; r < BM; r += kThreads) {
         const int m = m0 + r;
         RowInfo q = {};
@@ -94,10 +91,17 @@ __global__ __launch_bounds__(kThreads) void pw_kernel(PwArgs a) {
             q.mode = k.mode;
             q.act = k.act;
             q.bias = k.bias ? k.bias[cl] : 0.f;
-            q.f = scoef[m];
+            q.f = SinkCoef{0.f, 1.f, 0.f, 0.f};
+            if (k.mode == ISG_SINK_ACTBWD) {
+                if (k.bn.stats || !k.bn.train) {
+                    const ChanCoef f = k.bn.coef ? fwd_coef(k.bn, nullptr, cl)
+                                                 : coef_slow(k.bn, nullptr, cl, 0);
+                    q.f.mean = f.c0; q.f.scale = f.c1; q.f.beta = f.c2;
+                }
+                q.f.slope = k.slope ? k.slope[cl] : 0.f;
+            }
         }
         ri[r] = q;
-        red[0][r] = red[1][r] = red[2][r] = 0.f;
     }
 
     // this lane's pixel of the block (staging) — the block never crosses an image when
@@ -165,6 +169,14 @@ __global__ __launch_bounds__(kThreads) void pw_kernel(PwArgs a) {
 
     // ---- epilogue: lane holds D[row = rt*16 + kk*4 + r][pixel = ct*16 + pl] ------------
     const bool need_red = sinks_need_red(a.out);
+    // per-wave BN partials [4 waves][3][BM] (fixed-order sum: deterministic statistics),
+    // in the weight tile's LDS, free once every wave is past the K loop
+    float (*red)[3][kMaxBM] = reinterpret_cast<float (*)[3][kMaxBM]>(Ws);
+    if (need_red) {
+        __syncthreads();
+        for (int i = tid; i < 4 * 3 * kMaxBM; i += kThreads) (&red[0][0][0])[i] = 0.f;
+        __syncthreads();
+    }
 #pragma unroll
     for (int i = 0; i < TPW; ++i) {
         const int t = wave + 4 * i;
@@ -215,9 +227,9 @@ __global__ __launch_bounds__(kThreads) void pw_kernel(PwArgs a) {
                 const float t2 = row16_sum(s2[r]);
                 const int rl = rt * 16 + kk * 4 + r;
                 if (pl == 0 && rl < Mb) {
-                    atomicAdd(&red[0][rl], t0);
-                    atomicAdd(&red[1][rl], t1);
-                    atomicAdd(&red[2][rl], t2);
+                    red[wave][0][rl] = t0;  // one tile per (wave, row)
+                    red[wave][1][rl] = t1;
+                    red[wave][2][rl] = t2;
                 }
             }
         }
@@ -225,6 +237,9 @@ __global__ __launch_bounds__(kThreads) void pw_kernel(PwArgs a) {
     if (need_red) {
         __syncthreads();
         for (int rl = tid; rl < Mb; rl += kThreads) {
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+                red[0][j][rl] = ((red[0][j][rl] + red[1][j][rl]) + red[2][j][rl]) + red[3][j][rl];
             const int m = m0 + rl;
             const int s = sink_of(a.out, m);
             const isg_sink& k = s == 2 ? a.out.s[2] : (s == 1 ? a.out.s[1] : a.out.s[0]);
@@ -232,17 +247,17 @@ __global__ __launch_bounds__(kThreads) void pw_kernel(PwArgs a) {
             if (k.mode == ISG_SINK_STORE || k.mode == ISG_SINK_ACCUM) {
                 if (k.stats) {
                     double* sp = rep_ptr(k.stats, 4 * k.C);
-                    atomicAdd(&sp[cl], (double)red[0][rl]);
-                    atomicAdd(&sp[k.C + cl], (double)red[1][rl]);
+                    atomicAdd(&sp[cl], (double)red[0][0][rl]);
+                    atomicAdd(&sp[k.C + cl], (double)red[0][1][rl]);
                 }
             } else if (k.mode == ISG_SINK_ACTBWD) {
                 if (k.bn.stats) {
                     double* sp = rep_ptr(k.bn.stats, 4 * k.C);
-                    atomicAdd(&sp[2 * k.C + cl], (double)red[0][rl]);
-                    atomicAdd(&sp[3 * k.C + cl], (double)red[1][rl]);
+                    atomicAdd(&sp[2 * k.C + cl], (double)red[0][0][rl]);
+                    atomicAdd(&sp[3 * k.C + cl], (double)red[0][1][rl]);
                 }
                 if (k.slope_grad && k.act == ISG_ACT_PRELU)
-                    atomicAdd(&rep_ptr(k.slope_grad, k.C)[cl], (double)red[2][rl]);
+                    atomicAdd(&rep_ptr(k.slope_grad, k.C)[cl], (double)red[0][2][rl]);
             }
         }
     }
