@@ -135,8 +135,10 @@ ISG_DEV void wg_stage(const WgArgs& a, const TileCtx& t, int64_t tl, int nrow_w,
 template <int TPW>
 __global__ __launch_bounds__(kThreads) void wgrad_kernel(WgArgs a) {
     // TPW: accumulator tiles per wave = ceil(BMT*BNT / 4)
-    __shared__ float As[kRowsBlk * kAStride];
-    __shared__ float Xs[kXs];
+    // dynamic LDS sized per launch (occupancy): A tile [BMT*16][kAStride], then the halo
+    extern __shared__ float smem[];
+    float* const As = smem;
+    float* const Xs = smem + a.BMT * 16 * kAStride;
     __shared__ ChT tA[kRowsBlk];
     __shared__ ChT tX[kMaxXCh];
 
@@ -363,7 +365,7 @@ int32_t isg_dense_conv_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, cons
         const int m = max_nci(bnt);
         return m <= kMaxXCh && m * a.hsp <= kXs;
     };
-    int bnt = a.valu ? 4 : std::min(CT, std::max(1, 32 / nrt));
+    int bnt = a.valu ? 4 : std::min(CT, std::max(1, 16 / nrt));  // <= 4 tiles per wave (VGPRs)
     bnt = std::min(bnt, kColsBlk / 16);
     while (bnt > 1 && !fits(bnt)) --bnt;
     if (!fits(bnt))
@@ -385,7 +387,10 @@ int32_t isg_dense_conv_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, cons
 #endif
     dim3 grid((unsigned)gx, (unsigned)gy);
     const int tpw = (a.BMT * a.BNT + 3) / 4;
-#define WG_LAUNCH(T) hipLaunchKernelGGL((wgrad_kernel<T>), grid, dim3(kThreads), 0, st, a)
+    // halo floats (>= 768: the k-split / VALU partial sums reuse that space)
+    const size_t xs = std::max<size_t>((size_t)max_nci(bnt) * a.hsp, 768);
+    const size_t lds = ((size_t)a.BMT * 16 * kAStride + xs) * sizeof(float);
+#define WG_LAUNCH(T) hipLaunchKernelGGL((wgrad_kernel<T>), grid, dim3(kThreads), lds, st, a)
     switch (tpw) {
         case 1: WG_LAUNCH(1); break;
         case 2: WG_LAUNCH(2); break;
