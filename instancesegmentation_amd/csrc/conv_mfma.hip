@@ -246,6 +246,8 @@ int32_t isg_halo_conv_fwd(const isg_conv_geom* g, const isg_vtensor* x, const fl
                           const isg_sinks* out, hipStream_t st);
 int32_t isg_pw_gemm(const isg_conv_geom* g, const isg_vtensor* src, const float* w,
                     const isg_sinks* out, bool dgrad, hipStream_t st);
+int32_t isg_tap_conv(const isg_conv_geom* g, const isg_vtensor* src, const float* w,
+                     const isg_sinks* out, bool dgrad, hipStream_t st);
 
 static bool is_pointwise(const isg_conv_geom* g) {
     return g->KH == 1 && g->KW == 1 && g->SH == 1 && g->SW == 1 && g->PH == 0 && g->PW == 0 &&
@@ -258,6 +260,10 @@ int32_t isg_dense_conv_fwd(const isg_conv_geom* g, const isg_vtensor* x, const f
     if (int32_t e = check_sinks(out, g->Co, "conv fwd")) return e;
     static const bool special_off = getenv("ISG_GENERIC_CONV") != nullptr;
     if (!special_off && is_pointwise(g)) return isg_pw_gemm(g, x, w, out, false, st);
+    if (!special_off) {  // dense spatial conv, <= 48 output channels (tap_conv.hip)
+        const int32_t t = isg_tap_conv(g, x, w, out, false, st);
+        if (t != 0) return t < 0 ? t : 0;
+    }
     // narrow outputs with spatial taps: LDS halo-tiled kernel (halo_conv.hip)
     static const bool halo_off = special_off || getenv("ISG_NO_HALO_CONV") != nullptr;
     if (!halo_off) {
@@ -285,6 +291,10 @@ int32_t isg_dense_conv_dgrad(const isg_conv_geom* g, const isg_vtensor* dy, cons
     if (int32_t e = check_sinks(dx, g->Ci, "conv dgrad")) return e;
     static const bool special_off = getenv("ISG_GENERIC_CONV") != nullptr;
     if (!special_off && is_pointwise(g)) return isg_pw_gemm(g, dy, w, dx, true, st);
+    if (!special_off) {
+        const int32_t t = isg_tap_conv(g, dy, w, dx, true, st);
+        if (t != 0) return t < 0 ? t : 0;
+    }
     if (g->KH > 16 || g->KW > 16) return isg_set_error(ISG_ERR_UNSUPPORTED, "conv dgrad: kernel > 16");
     const int maxk = g->Co * ((g->KH + g->SH - 1) / g->SH) * ((g->KW + g->SW - 1) / g->SW);
     if (maxk > kKtabMax) return isg_set_error(ISG_ERR_UNSUPPORTED, "conv dgrad: K=%d too large", maxk);

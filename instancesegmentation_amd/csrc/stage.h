@@ -126,3 +126,119 @@ ISG_DEV float ch_xform(int xf, int act, const ChanCoef& k, float x, float y) {
 }
 
 ISG_DEV int wave_id() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }
+
+// A wave-uniform pointer moved into SGPRs (each 32-bit half through readfirstlane), so
+// loads off it use the scalar-base + 32-bit vector-offset addressing form.
+template <class T>
+ISG_DEV T* uniform_ptr(T* p) {
+    const uint64_t v = (uint64_t)(uintptr_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return (T*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+}
+
+// An opaque copy of v: the compiler must recompute whatever depends on it (stops it from
+// hoisting per-item address arithmetic out of a loop into dozens of live registers).
+ISG_DEV int opaque(int v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
+
+// sum over the 16 lanes of a DPP row (lanes sharing l>>4), result in every lane
+ISG_DEV float dpp_row16_sum(float v) {
+    int x = __builtin_bit_cast(int, v);
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false));
+    x = __builtin_bit_cast(int, v);
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false));
+    x = __builtin_bit_cast(int, v);
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, x, 0x141, 0xF, 0xF, false));
+    x = __builtin_bit_cast(int, v);
+    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, x, 0x140, 0xF, 0xF, false));
+    return v;
+}
+
+// Per-output-row sink record kept in LDS (one per GEMM row = output channel), resolved
+// once per workgroup: the epilogue reads it with a broadcast LDS access.
+struct SinkRow {
+    float* p;        // channel base, image 0
+    const float* y;  // ACTBWD: saved forward output
+    int64_t ns, yns;
+    int mode, act;   // mode -1: row past M
+    float bias;
+    int pad_;
+    SinkCoef f;
+};
+
+ISG_DEV SinkRow sink_row(const isg_sinks& sk, int m, int64_t hw) {
+    SinkRow q = {};
+    const int s = sink_of(sk, m);
+    const isg_sink& k = s == 2 ? sk.s[2] : (s == 1 ? sk.s[1] : sk.s[0]);
+    const int cl = m - k.c0;
+    q.p = k.p ? k.p + (int64_t)cl * hw : nullptr;
+    q.y = k.y ? k.y + (int64_t)cl * hw : nullptr;
+    q.ns = k.n_stride;
+    q.yns = k.y_n_stride;
+    q.mode = k.mode;
+    q.act = k.act;
+    q.bias = k.bias ? k.bias[cl] : 0.f;
+    q.f = SinkCoef{0.f, 1.f, 0.f, 0.f};
+    if (k.mode == ISG_SINK_ACTBWD) {
+        if (k.bn.stats || !k.bn.train) {
+            const ChanCoef f = k.bn.coef ? fwd_coef(k.bn, nullptr, cl) : coef_slow(k.bn, nullptr, cl, 0);
+            q.f.mean = f.c0; q.f.scale = f.c1; q.f.beta = f.c2;
+        }
+        q.f.slope = k.slope ? k.slope[cl] : 0.f;
+    }
+    return q;
+}
+
+// Apply row q's sink to value v at flat offset (n, pix); returns the values to reduce
+// (STORE/ACCUM: v, v^2; ACTBWD: g, g*(y-mean), PReLU slope contribution).
+ISG_DEV void sink_row_apply(const SinkRow& q, int n, int64_t pix, float v, float& s0, float& s1,
+                            float& s2) {
+    const int64_t off = (int64_t)n * q.ns + pix;
+    if (q.mode == ISG_SINK_STORE) {
+        v += q.bias;
+        gst(q.p, off, v);
+        s0 = v;
+        s1 = v * v;
+    } else if (q.mode == ISG_SINK_ACCUM) {
+        gst(q.p, off, gld(q.p, off) + v);
+        s0 = v;
+        s1 = v * v;
+    } else if (q.mode == ISG_SINK_ACTBWD) {
+        const float y = gld(q.y, (int64_t)n * q.yns + pix);
+        const float z = (y - q.f.mean) * q.f.scale + q.f.beta;
+        float gv = v;
+        if (q.act == ISG_ACT_RELU) {
+            gv = z > 0.f ? v : 0.f;
+        } else if (q.act == ISG_ACT_PRELU) {
+            gv = z > 0.f ? v : v * q.f.slope;
+            s2 = z > 0.f ? 0.f : z * v;
+        }
+        gst(q.p, off, gv);
+        s0 = gv;
+        s1 = gv * (y - q.f.mean);
+    }
+}
+
+// Fold row m's block-reduced sums into the sink's replicated fp64 accumulators.
+ISG_DEV void sink_row_flush(const isg_sinks& sk, int m, float r0, float r1, float r2) {
+    const int s = sink_of(sk, m);
+    const isg_sink& k = s == 2 ? sk.s[2] : (s == 1 ? sk.s[1] : sk.s[0]);
+    const int cl = m - k.c0;
+    if (k.mode == ISG_SINK_STORE || k.mode == ISG_SINK_ACCUM) {
+        if (k.stats) {
+            double* sp = rep_ptr(k.stats, 4 * k.C);
+            atomicAdd(&sp[cl], (double)r0);
+            atomicAdd(&sp[k.C + cl], (double)r1);
+        }
+    } else if (k.mode == ISG_SINK_ACTBWD) {
+        if (k.bn.stats) {
+            double* sp = rep_ptr(k.bn.stats, 4 * k.C);
+            atomicAdd(&sp[2 * k.C + cl], (double)r0);
+            atomicAdd(&sp[3 * k.C + cl], (double)r1);
+        }
+        if (k.slope_grad && k.act == ISG_ACT_PRELU) atomicAdd(&rep_ptr(k.slope_grad, k.C)[cl], (double)r2);
+    }
+}

@@ -61,6 +61,11 @@ DENSE = [
     (96, 48, 16, 16, 1, 1, 0, 1),
     (48, 128, 16, 16, 1, 1, 0, 1),
     (16, 16, 20, 20, 3, 1, 2, 2),
+    # tap_conv coverage: Ci % 4 != 0, 3 row tiles, ragged edges, multi-tile grids
+    (3, 16, 64, 48, 5, 2, 2, 1),
+    (16, 36, 33, 45, 3, 1, 1, 1),
+    (20, 16, 130, 100, 5, 2, 2, 1),
+    (16, 4, 72, 88, 8, 4, 2, 1),
 ]
 
 

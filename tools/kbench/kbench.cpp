@@ -1,6 +1,6 @@
 // Kernel micro-benchmark harness: times one libisg op in isolation on synthetic data and
 // dumps per-workgroup s_memrealtime stamps (libisg_stamp.so, built with -DISG_STAMPS).
-//   kbench wgrad N Ci H W Co k s p d [reps]
+//   kbench wgrad|fwd|dgrad N Ci H W Co k s p d [reps]
 // Output: avg us per launch (hipEvent over reps), then stamp statistics of the last launch.
 #include <hip/hip_runtime.h>
 
@@ -35,13 +35,14 @@ static float* dalloc(size_t n, float v = 0.f, unsigned seed = 1) {
 
 int main(int argc, char** argv) {
     if (argc < 11) {
-        fprintf(stderr, "usage: kbench wgrad N Ci H W Co k s p d [reps]\n");
+        fprintf(stderr, "usage: kbench wgrad|fwd|dgrad N Ci H W Co k s p d [reps]\n");
         return 2;
     }
     const int N = atoi(argv[2]), Ci = atoi(argv[3]), H = atoi(argv[4]), W = atoi(argv[5]),
               Co = atoi(argv[6]), k = atoi(argv[7]), s = atoi(argv[8]), p = atoi(argv[9]),
               d = atoi(argv[10]);
     const int reps = argc > 11 ? atoi(argv[11]) : 50;
+    const char* op = argv[1];
     isg_conv_geom g{};
     g.N = N; g.Ci = Ci; g.H = H; g.W = W; g.Co = Co; g.KH = g.KW = k; g.SH = g.SW = s;
     g.PH = g.PW = p; g.DH = g.DW = d; g.groups = 1;
@@ -62,6 +63,13 @@ int main(int argc, char** argv) {
     const int64_t nw = (int64_t)Co * Ci * k * k;
     float* dw;
     CK(hipMalloc(&dw, ISG_WREP * nw * sizeof(float)));
+    float* wt = dalloc(nw, 0.f, 4);
+    float* out;
+    CK(hipMalloc(&out, std::max(nx, ny) * sizeof(float)));
+    double* ostats;
+    CK(hipMalloc(&ostats, C4 * sizeof(double)));
+    double* sgrad;
+    CK(hipMalloc(&sgrad, std::max(Ci, Co) * ISG_STAT_REP * sizeof(double)));
     // dy: BN backward rebuilt (the common case); x: BN fwd + PReLU
     isg_vtensor vdy{}, vx{};
     vdy.nseg = 1; vdy.N = N; vdy.H = g.OH; vdy.W = g.OW;
@@ -74,8 +82,24 @@ int main(int argc, char** argv) {
     vx.s[0].bn = isg_bn{gam, bet, nullptr, nullptr, stats, Ci, 1, (float)(N * H * W), 1e-5f};
     hipStream_t st;
     CK(hipStreamCreate(&st));
+    // forward: STORE sink with BN statistics; dgrad: ACTBWD sink (BN + PReLU backward)
+    isg_sinks sk{};
+    sk.nsink = 1;
+    isg_sink& s0 = sk.s[0];
+    if (!strcmp(op, "fwd")) {
+        s0.p = out; s0.n_stride = (int64_t)Co * g.OH * g.OW; s0.C = Co; s0.mode = ISG_SINK_STORE;
+        s0.bias = bet; s0.stats = ostats;
+    } else {
+        s0.p = out; s0.n_stride = (int64_t)Ci * H * W; s0.C = Ci; s0.mode = ISG_SINK_ACTBWD;
+        s0.act = ISG_ACT_PRELU; s0.y = x; s0.y_n_stride = s0.n_stride; s0.slope = slope;
+        s0.slope_grad = sgrad;
+        s0.bn = isg_bn{gam, bet, nullptr, nullptr, ostats, Ci, 1, (float)(N * H * W), 1e-5f};
+    }
     auto run = [&]() {
-        int rc = isg_conv_wgrad_rep(&g, &vdy, &vx, dw, nullptr, nw, ISG_WREP, (isg_stream_t)st);
+        int rc;
+        if (!strcmp(op, "fwd")) rc = isg_conv_fwd(&g, &vx, wt, &sk, (isg_stream_t)st);
+        else if (!strcmp(op, "dgrad")) rc = isg_conv_dgrad(&g, &vdy, wt, &sk, (isg_stream_t)st);
+        else rc = isg_conv_wgrad_rep(&g, &vdy, &vx, dw, nullptr, nw, ISG_WREP, (isg_stream_t)st);
         if (rc) {
             fprintf(stderr, "isg error %d: %s\n", rc, isg_last_error());
             exit(1);
@@ -92,6 +116,11 @@ int main(int argc, char** argv) {
     CK(hipEventSynchronize(e1));
     float ms;
     CK(hipEventElapsedTime(&ms, e0, e1));
+    if (strcmp(op, "wgrad")) {
+        printf("%s N%d Ci%d %dx%d -> Co%d %dx%d k%d s%d p%d d%d: %.2f us/launch (%d reps)\n", op, N,
+               Ci, H, W, Co, g.OH, g.OW, k, s, p, d, 1e3 * ms / reps, reps);
+        return 0;
+    }
     // stamped single launch
     unsigned long long* sp = (unsigned long long*)isg_dbg_stamps_wgrad();
     CK(hipMemset(sp, 0, 65536 * 8 * sizeof(unsigned long long)));
@@ -106,9 +135,9 @@ int main(int argc, char** argv) {
         t0 = std::min(t0, h[b * 8]);
         tend = std::max(tend, h[b * 8 + 4]);
     }
-    printf("wgrad N%d Ci%d %dx%d -> Co%d %dx%d k%d s%d p%d d%d: %.2f us/launch (%d reps); "
+    printf("%s N%d Ci%d %dx%d -> Co%d %dx%d k%d s%d p%d d%d: %.2f us/launch (%d reps); "
            "stamped launch %d blocks, span %.2f us\n",
-           N, Ci, H, W, Co, g.OH, g.OW, k, s, p, d, 1e3 * ms / reps, reps, nb,
+           op, N, Ci, H, W, Co, g.OH, g.OW, k, s, p, d, 1e3 * ms / reps, reps, nb,
            (tend - t0) / 100.0);
     // per-segment medians (10 ns ticks)
     for (int seg = 0; seg < 4; ++seg) {
