@@ -58,12 +58,12 @@ def op_timing(trainer, reps=20):
     for phase, ol in (("fwd", trainer.plan.fwd), ("bwd", trainer.plan.bwd)):
         for i, r in enumerate(ol.recs):
             sub = ol.slice(i, i + 1)
-            sub.run(trainer.table, L.stream_ptr())
+            sub.run(trainer.table, L.stream_ptr(), L.side_stream_ptr())
             torch.cuda.synchronize()
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph):
                 for _ in range(reps):
-                    sub.run(trainer.table, L.stream_ptr())
+                    sub.run(trainer.table, L.stream_ptr(), L.side_stream_ptr())
             graph.replay()
             stream = torch.cuda.current_stream()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -302,6 +302,15 @@ typedef struct {
 
 int32_t isg_exec(const void* ops, int32_t nops, void* const* table, isg_stream_t stream);
 
+/* Same, with a side stream: ops flagged "side" in their record header (the weight
+ * gradients, which nothing later in the list reads) are forked onto `side` after every
+ * op issued before them on `stream`; ops flagged "join" (and the end of the list) wait
+ * for all forked work. side == NULL runs everything on `stream`. Under HIP-graph
+ * capture the fork/join become graph edges, so the weight gradients overlap the
+ * input-gradient chain. */
+int32_t isg_exec_ms(const void* ops, int32_t nops, void* const* table, isg_stream_t stream,
+                    isg_stream_t side);
+
 /* sizeof() of the ABI structs and executor records (0 vtensor, 1 sinks, 2 conv record,
  * 3 wgrad record, 4 pool record, 5 tail, 6 tail_grad, 7 bn_update, 8 grad_final,
  * 9 bce record, 10 conv_geom, 11 bn, 12 vseg, 13 sink) so bindings can verify layouts. */

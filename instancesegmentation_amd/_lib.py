@@ -157,6 +157,7 @@ SIGNATURES = {
     "isg_mask_nms": (c_int32, [c_void_p, c_int32, c_int32, c_int32, c_float, c_void_p, c_void_p,
                                c_void_p, c_void_p, c_void_p]),
     "isg_exec": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p]),
+    "isg_exec_ms": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p]),
     "isg_last_error": (c_char_p, []),
     "isg_abi_version": (c_int32, []),
     "isg_stat_replicas": (c_int32, []),
@@ -201,3 +202,19 @@ def check(rc, what=""):
 
 def stream_ptr(device=None):
     return torch.cuda.current_stream(device).cuda_stream
+
+
+_SIDE = {}
+
+
+def side_stream_ptr(device=None):
+    """The executor's side stream of `device` (weight gradients fork onto it), or None
+    when disabled (ISG_NO_SIDE_STREAM=1)."""
+    if os.environ.get("ISG_NO_SIDE_STREAM", "0") == "1":
+        return None
+    d = torch.cuda.current_device() if device is None else torch.device(device).index
+    if d is None:
+        d = torch.cuda.current_device()
+    if d not in _SIDE:
+        _SIDE[d] = torch.cuda.Stream(device=d)
+    return _SIDE[d].cuda_stream

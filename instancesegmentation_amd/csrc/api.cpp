@@ -4,8 +4,11 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
+#include <utility>
+#include <vector>
 
 #include "../../include/isg.h"
 
@@ -169,19 +172,155 @@ struct MemsetRec {
 };
 
 struct OpHdr {
-    int32_t kind, desc_bytes, nfix, pad_;
+    int32_t kind, desc_bytes, nfix, flags;  // flags: ISG_OPF_SIDE | ISG_OPF_JOIN
 };
+enum { ISG_OPF_SIDE = 1, ISG_OPF_JOIN = 2 };
+
+// fork / join events of the executor's side stream, one pair per device (created on
+// first use, never destroyed; timing disabled)
+static int32_t side_events(hipEvent_t* fork, hipEvent_t* join) {
+    static hipEvent_t ev[64][2];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64)
+        return isg_set_error(ISG_ERR_HIP, "exec: no device for the side stream");
+    if (!ev[dev][0]) {
+        if (hipEventCreateWithFlags(&ev[dev][0], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&ev[dev][1], hipEventDisableTiming) != hipSuccess)
+            return isg_check_launch("exec: side-stream events");
+    }
+    *fork = ev[dev][0];
+    *join = ev[dev][1];
+    return ISG_OK;
+}
 struct Fix {
     int32_t loc, slot;
     int64_t offset;
 };
 
-int32_t isg_exec(const void* ops, int32_t nops, void* const* table, isg_stream_t st) {
+static int32_t run_op(int32_t kind, char* buf, isg_stream_t st) {
+    int32_t rc = 0;
+    switch (kind) {
+        case OP_CONV_FWD: {
+            auto* r = (ConvRec*)buf;
+            rc = isg_conv_fwd(&r->g, &r->a, r->w, &r->out, st);
+            break;
+        }
+        case OP_CONV_DGRAD: {
+            auto* r = (ConvRec*)buf;
+            rc = isg_conv_dgrad(&r->g, &r->a, r->w, &r->out, st);
+            break;
+        }
+        case OP_CONV_WGRAD: {
+            auto* r = (WgradRec*)buf;
+            rc = isg_conv_wgrad_rep(&r->g, &r->dy, &r->x, r->dw, r->dbias, r->rep_stride,
+                                    r->nrep < 1 ? 1 : r->nrep, st);
+            break;
+        }
+        case OP_CONVT_FWD: {
+            auto* r = (ConvRec*)buf;
+            rc = isg_convT_fwd(&r->g, &r->a, r->w, &r->out, st);
+            break;
+        }
+        case OP_MAXPOOL_FWD: {
+            auto* r = (PoolRec*)buf;
+            rc = isg_maxpool_fwd(&r->x, r->k, r->out, r->out_ns, st);
+            break;
+        }
+        case OP_MAXPOOL_BWD: {
+            auto* r = (PoolRec*)buf;
+            rc = isg_maxpool_bwd(&r->x, r->k, r->dout, r->dout_ns, &r->dx, st);
+            break;
+        }
+        case OP_TAIL_FWD:
+            rc = isg_tail_fwd((const isg_tail*)buf, st);
+            break;
+        case OP_TAIL_BWD:
+            rc = isg_tail_bwd((const isg_tail_grad*)buf, st);
+            break;
+        case OP_BN_UPDATE: {
+            auto* r = (ListRec*)buf;
+            rc = isg_bn_update_running((const isg_bn_update*)(buf + sizeof(ListRec)), r->n, st);
+            break;
+        }
+        case OP_BN_FINAL: {
+            auto* r = (ListRec*)buf;
+            rc = isg_bn_finalize((const isg_bn*)(buf + sizeof(ListRec)), r->n, r->pad_, st);
+            break;
+        }
+        case OP_GRAD_FINAL: {
+            auto* r = (ListRec*)buf;
+            rc = isg_grad_finalize((const isg_grad_final*)(buf + sizeof(ListRec)), r->n, st);
+            break;
+        }
+        case OP_BCE: {
+            auto* r = (BceRec*)buf;
+            rc = isg_bce_sigmoid(r->logits, r->target, r->n, r->loss, r->dlogits, r->grad_scale, st);
+            break;
+        }
+        case OP_SUM_REP: {
+            auto* r = (SumRepRec*)buf;
+            rc = isg_sum_replicas(r->dst, r->src, r->n, r->nrep, r->stride, st);
+            break;
+        }
+        case OP_MEMSET: {
+            auto* r = (MemsetRec*)buf;
+            if (hipMemsetAsync(r->p, 0, (size_t)r->bytes, st) != hipSuccess)
+                rc = isg_check_launch("memset");
+            break;
+        }
+        default:
+            return isg_set_error(ISG_ERR_INVALID, "exec: unknown op kind %d", kind);
+    }
+    return rc;
+}
+
+int32_t isg_exec_ms(const void* ops, int32_t nops, void* const* table, isg_stream_t main_st,
+                    isg_stream_t side) {
     const char* p = (const char*)ops;
     alignas(16) char buf[8192];
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    bool forked = false;  // side-stream work outstanding since the last join
+    static const int batch = [] {
+        const char* e = getenv("ISG_SIDE_BATCH");
+        const int b = e ? atoi(e) : 24;
+        return b < 1 ? 1 : b;
+    }();
+    std::vector<std::pair<int32_t, std::string>> pending;
+    auto flush = [&]() -> int32_t {
+        if (pending.empty()) return ISG_OK;
+        if (hipEventRecord(ev_fork, main_st) != hipSuccess || hipStreamWaitEvent(side, ev_fork, 0) != hipSuccess)
+            return isg_check_launch("exec: fork side stream");
+        forked = true;
+        alignas(16) char pb[8192];
+        for (auto& op : pending) {
+            std::memcpy(pb, op.second.data(), op.second.size());
+            if (int32_t e = run_op(op.first, pb, side)) return e;
+        }
+        pending.clear();
+        return ISG_OK;
+    };
+    auto join = [&]() -> int32_t {
+        if (int32_t e = flush()) return e;
+        if (!forked) return ISG_OK;
+        forked = false;
+        if (hipEventRecord(ev_join, side) != hipSuccess || hipStreamWaitEvent(main_st, ev_join, 0) != hipSuccess)
+            return isg_check_launch("exec: join side stream");
+        return ISG_OK;
+    };
     for (int i = 0; i < nops; ++i) {
         OpHdr h;
         std::memcpy(&h, p, sizeof(h));
+        isg_stream_t st = main_st;
+        if ((h.flags & ISG_OPF_JOIN) && side) {
+            if (int32_t e = join()) return e;
+        }
+        if ((h.flags & ISG_OPF_SIDE) && side) {
+            // the op depends on everything issued so far on the main stream
+            if (!ev_fork) {
+                if (int32_t e = side_events(&ev_fork, &ev_join)) return e;
+            }
+            st = side;
+        }
         p += sizeof(h);
         if (h.desc_bytes < 0 || h.desc_bytes > (int)sizeof(buf))
             return isg_set_error(ISG_ERR_INVALID, "exec: op %d bad desc size %d", i, h.desc_bytes);
@@ -196,84 +335,24 @@ int32_t isg_exec(const void* ops, int32_t nops, void* const* table, isg_stream_t
             std::memcpy(buf + fx.loc, &v, sizeof(v));
         }
         int32_t rc = 0;
-        switch (h.kind) {
-            case OP_CONV_FWD: {
-                auto* r = (ConvRec*)buf;
-                rc = isg_conv_fwd(&r->g, &r->a, r->w, &r->out, st);
-                break;
-            }
-            case OP_CONV_DGRAD: {
-                auto* r = (ConvRec*)buf;
-                rc = isg_conv_dgrad(&r->g, &r->a, r->w, &r->out, st);
-                break;
-            }
-            case OP_CONV_WGRAD: {
-                auto* r = (WgradRec*)buf;
-                rc = isg_conv_wgrad_rep(&r->g, &r->dy, &r->x, r->dw, r->dbias, r->rep_stride,
-                                        r->nrep < 1 ? 1 : r->nrep, st);
-                break;
-            }
-            case OP_CONVT_FWD: {
-                auto* r = (ConvRec*)buf;
-                rc = isg_convT_fwd(&r->g, &r->a, r->w, &r->out, st);
-                break;
-            }
-            case OP_MAXPOOL_FWD: {
-                auto* r = (PoolRec*)buf;
-                rc = isg_maxpool_fwd(&r->x, r->k, r->out, r->out_ns, st);
-                break;
-            }
-            case OP_MAXPOOL_BWD: {
-                auto* r = (PoolRec*)buf;
-                rc = isg_maxpool_bwd(&r->x, r->k, r->dout, r->dout_ns, &r->dx, st);
-                break;
-            }
-            case OP_TAIL_FWD:
-                rc = isg_tail_fwd((const isg_tail*)buf, st);
-                break;
-            case OP_TAIL_BWD:
-                rc = isg_tail_bwd((const isg_tail_grad*)buf, st);
-                break;
-            case OP_BN_UPDATE: {
-                auto* r = (ListRec*)buf;
-                rc = isg_bn_update_running((const isg_bn_update*)(buf + sizeof(ListRec)), r->n, st);
-                break;
-            }
-            case OP_BN_FINAL: {
-                auto* r = (ListRec*)buf;
-                rc = isg_bn_finalize((const isg_bn*)(buf + sizeof(ListRec)), r->n, r->pad_, st);
-                break;
-            }
-            case OP_GRAD_FINAL: {
-                auto* r = (ListRec*)buf;
-                rc = isg_grad_finalize((const isg_grad_final*)(buf + sizeof(ListRec)), r->n, st);
-                break;
-            }
-            case OP_BCE: {
-                auto* r = (BceRec*)buf;
-                rc = isg_bce_sigmoid(r->logits, r->target, r->n, r->loss, r->dlogits, r->grad_scale, st);
-                break;
-            }
-            case OP_SUM_REP: {
-                auto* r = (SumRepRec*)buf;
-                rc = isg_sum_replicas(r->dst, r->src, r->n, r->nrep, r->stride, st);
-                break;
-            }
-            case OP_MEMSET: {
-                auto* r = (MemsetRec*)buf;
-                if (hipMemsetAsync(r->p, 0, (size_t)r->bytes, st) != hipSuccess)
-                    rc = isg_check_launch("memset");
-                break;
-            }
-            default:
-                return isg_set_error(ISG_ERR_INVALID, "exec: op %d unknown kind %d", i, h.kind);
+        if (side && st == side) {
+            // deferred: launched in batches behind one fork (a later fork only adds
+            // dependencies, so batching is always safe)
+            pending.emplace_back(h.kind, std::string(buf, buf + h.desc_bytes));
+            if ((int)pending.size() >= batch) rc = flush();
+        } else {
+            rc = run_op(h.kind, buf, st);
         }
         if (rc) {
             std::string m = g_last_error;
             return isg_set_error(rc, "exec op %d (kind %d): %s", i, h.kind, m.c_str());
         }
     }
-    return ISG_OK;
+    return join();
+}
+
+int32_t isg_exec(const void* ops, int32_t nops, void* const* table, isg_stream_t st) {
+    return isg_exec_ms(ops, nops, table, st, nullptr);
 }
 
 // sizes of the executor records, so the Python planner can verify its ctypes mirrors

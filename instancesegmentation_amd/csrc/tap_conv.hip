@@ -84,7 +84,10 @@ struct TapArgs {
     int BY, BX, tiles_x, tiles_y, nph, ntiles;  // ntiles over all phases and images
     int nchunk;       // chunks of 4 channels (one per wave)
     int HR, HCu, PS, RS, CHS;  // halo rows, units per row (cols, or col pairs), LDS layout
-    int ws_floats;    // weights in LDS: [Cp][KK+1][MP] (row KK zero: padded taps)
+    int ws_floats;    // weights in LDS: [Cp][WCS] with WCS >= (KK+1)*MP (row KK zero)
+    int WCS;          // per-channel weight stride (== 16 mod 32: conflict-free quads)
+    uint32_t m_img, m_tpi, m_tx;  // ceil(2^32/d) for d = N*tpi, tpi, tiles_x (exact, x*d < 2^32;
+                                  // 0 for d == 1)
 };
 
 template <int MT, int G, bool YB, bool PAIR>
@@ -141,15 +144,12 @@ __global__ __launch_bounds__(kThreads) void tap_conv_kernel(TapArgs a) {
         if (r < a.M) q = sink_row(a.out, r, (int64_t)a.DstH * a.DstW);
         ri[r] = q;
     }
-    {
-        const int KK1 = a.KK + 1;
-        for (int f = tid; f < a.ws_floats; f += kThreads) {
-            const int m = f % MP, rest = f / MP;
-            const int k = rest % KK1, c = rest / KK1;
-            float x = 0.f;
-            if (m < a.M && c < a.C && k < a.KK) x = gld(a.w, (int64_t)m * a.wm + (int64_t)c * a.wc + k);
-            Ws[f] = x;
-        }
+    for (int f = tid; f < a.ws_floats; f += kThreads) {
+        const int c = f / a.WCS, rem = f - c * a.WCS;
+        const int k = rem / MP, m = rem - k * MP;
+        float x = 0.f;
+        if (m < a.M && c < a.C && k < a.KK) x = gld(a.w, (int64_t)m * a.wm + (int64_t)c * a.wc + k);
+        Ws[f] = x;
     }
     __syncthreads();
 
@@ -164,18 +164,21 @@ __global__ __launch_bounds__(kThreads) void tap_conv_kernel(TapArgs a) {
         xbase[g] = kq * a.CHS + my * tyl * a.RS + txl;
         gpix[g] = q < tpx ? (tyl << 16) | txl : -1;
     }
-    const int wlane = kq * (a.KK + 1) * MP + pl;  // lane part of the weight index
+    const int wlane = kq * a.WCS + pl;  // lane part of the weight index
     const uint32_t plane_bytes = (uint32_t)a.SrcH * a.SrcW * 4u;
 
     // ---- work items: (tile, chunk), tiles strided over the grid -------------------------
     const int tpi = a.tiles_x * a.tiles_y;
     auto tile_geo = [&](int tile, int& p, int& n, int& ty0, int& tx0, bool& live) {
-        p = tile / (a.N * tpi);
+        // magic 0 encodes a divisor of 1
+        auto qdiv = [](int x, uint32_t m) { return m ? (int)__umulhi((uint32_t)x, m) : x; };
+        p = qdiv(tile, a.m_img);
         const int r = tile - p * a.N * tpi;
-        n = r / tpi;
+        n = qdiv(r, a.m_tpi);
         const int tr = r - n * tpi;
-        ty0 = (tr / a.tiles_x) * a.BY;
-        tx0 = (tr % a.tiles_x) * a.BX;
+        const int tyi = qdiv(tr, a.m_tx);
+        ty0 = tyi * a.BY;
+        tx0 = (tr - tyi * a.tiles_x) * a.BX;
         const int ph = dg ? p / a.q.SW : 0, pw = dg ? p % a.q.SW : 0;
         const int TH = dg ? (a.OutH - ph + a.q.SH - 1) / a.q.SH : a.OutH;
         const int TW = dg ? (a.OutW - pw + a.q.SW - 1) / a.q.SW : a.OutW;
@@ -284,7 +287,7 @@ __global__ __launch_bounds__(kThreads) void tap_conv_kernel(TapArgs a) {
         bool live;
         tile_geo(tile, p, n, ty0, tx0, live);
         const int tb = p_beg[p], tn = p_n[p];
-        const float* const wch = Ws + ch * 4 * (a.KK + 1) * MP + wlane;
+        const float* const wch = Ws + ch * 4 * a.WCS + wlane;
         for (int t0 = 0; t0 < tn; t0 += 4) {
             const int4 to = *reinterpret_cast<const int4*>(&toff[tb + t0]);
             const int4 tw = *reinterpret_cast<const int4*>(&twof[tb + t0]);
@@ -311,26 +314,35 @@ __global__ __launch_bounds__(kThreads) void tap_conv_kernel(TapArgs a) {
             const int TH = dg ? (a.OutH - ph + a.q.SH - 1) / a.q.SH : a.OutH;
             const int TW = dg ? (a.OutW - pw + a.q.SW - 1) / a.q.SW : a.OutW;
             const int dmy = dg ? a.q.SH : 1, dmx = dg ? a.q.SW : 1;
+            int64_t gp[G];
+            bool gv[G];
 #pragma unroll
             for (int g = 0; g < G; ++g) {
                 const int ty = ty0 + (gpix[g] >> 16), tx = tx0 + (gpix[g] & 0xFFFF);
-                const bool pv = gpix[g] >= 0 && ty < TH && tx < TW;
-                const int64_t pix = (int64_t)(dmy * ty + ph) * a.DstW + (dmx * tx + pw);
-#pragma unroll
-                for (int m = 0; m < MT; ++m)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const int row = m * 16 + kq * 4 + r;
-                        if (row < a.M && pv) {
-                            float t0 = 0.f, t1 = 0.f, t2 = 0.f;
-                            sink_row_apply(ri[row], n, pix, acc[g][m][r], t0, t1, t2);
-                            s0[m][r] += t0;
-                            s1[m][r] += t1;
-                            s2[m][r] += t2;
-                        }
-                        acc[g][m][r] = 0.f;
-                    }
+                gv[g] = gpix[g] >= 0 && ty < TH && tx < TW;
+                gp[g] = (int64_t)(dmy * ty + ph) * a.DstW + (dmx * tx + pw);
             }
+#pragma unroll
+            for (int m = 0; m < MT; ++m)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = m * 16 + kq * 4 + r;
+                    if (row < a.M) {
+                        const SinkRow q = ri[row];
+#pragma unroll
+                        for (int g = 0; g < G; ++g) {
+                            if (gv[g]) {
+                                float t0 = 0.f, t1 = 0.f, t2 = 0.f;
+                                sink_row_apply(q, n, gp[g], acc[g][m][r], t0, t1, t2);
+                                s0[m][r] += t0;
+                                s1[m][r] += t1;
+                                s2[m][r] += t2;
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int g = 0; g < G; ++g) acc[g][m][r] = 0.f;
+                }
         }
         tile = ntile;
         ch = nch;
@@ -442,7 +454,9 @@ int32_t isg_tap_conv(const isg_conv_geom* g, const isg_vtensor* src, const float
     const int TWm = dgrad ? (g->W + g->SW - 1) / g->SW : g->OW;
     const int mt = (a.M + 15) / 16;
     const int Cp = (a.C + 3) & ~3;
-    a.ws_floats = Cp * (KK + 1) * 16 * mt;
+    a.WCS = (KK + 1) * 16 * mt;
+    a.WCS += ((16 - a.WCS % 32) + 32) % 32;
+    a.ws_floats = Cp * a.WCS;
     // tile width: the widest whose halo row fits 64 lanes (columns, or column pairs), split
     // evenly over the output width
     const int bxmax = mx == 1 ? 64 - ext_x : (128 - ext_x - 1) / 2 + 1;
@@ -478,6 +492,12 @@ int32_t isg_tap_conv(const isg_conv_geom* g, const isg_vtensor* src, const float
     a.tiles_x = tiles_x;
     a.tiles_y = (THm + BY - 1) / BY;
     a.ntiles = g->N * a.tiles_x * a.tiles_y * a.nph;
+    const int64_t tpi = (int64_t)a.tiles_x * a.tiles_y;
+    if ((int64_t)a.ntiles * g->N * tpi >= (1ll << 32)) return 0;  // magic-division range
+    auto magic = [](int64_t d) { return d == 1 ? 0u : (uint32_t)(((1ull << 32) + d - 1) / d); };
+    a.m_img = magic(g->N * tpi);
+    a.m_tpi = magic(tpi);
+    a.m_tx = magic(a.tiles_x);
     bool yb = false;
     for (int i = 0; i < src->nseg; ++i) yb |= src->s[i].xform == ISG_XF_BN_BWD;
     const size_t lds = (size_t)(a.ws_floats + 4 * a.CHS) * sizeof(float);

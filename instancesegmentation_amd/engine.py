@@ -81,8 +81,11 @@ def _fill(obj, spec, base, fix):
 
 
 class Record:
+    OPF_SIDE, OPF_JOIN = 1, 2  # executor header flags (api.cpp)
+
     def __init__(self, kind, cls, spec, items_cls=None, items=None, label="", flops=0, nbytes=0):
         self.kind = kind
+        self.flags = 0
         self.label = label
         self.flops = flops    # algorithmic FLOPs of this launch (2*MAC)
         self.nbytes = nbytes  # algorithmic HBM bytes (each operand read/written once)
@@ -104,7 +107,8 @@ class Record:
     def pack(self):
         n = len(self.body)
         pad = (-n) % 8
-        out = [struct.pack("<iiii", self.kind, n, len(self.fix), 0), self.body, b"\0" * pad]
+        out = [struct.pack("<iiii", self.kind, n, len(self.fix), self.flags), self.body,
+               b"\0" * pad]
         out += [struct.pack("<iiq", loc, slot, off) for loc, slot, off in self.fix]
         return b"".join(out)
 
@@ -121,9 +125,13 @@ class OpList:
         self._buf = ctypes.create_string_buffer(self.blob, len(self.blob))
         return self
 
-    def run(self, table, stream):
-        L.check(L.lib().isg_exec(ctypes.addressof(self._buf), len(self.recs), table, stream),
-                "exec")
+    def run(self, table, stream, side=None):
+        if side is None:
+            L.check(L.lib().isg_exec(ctypes.addressof(self._buf), len(self.recs), table, stream),
+                    "exec")
+        else:
+            L.check(L.lib().isg_exec_ms(ctypes.addressof(self._buf), len(self.recs), table,
+                                        stream, side), "exec")
 
     def slice(self, i, j):
         """A compiled sub-list recs[i:j] (to bracket one op with events)."""
@@ -748,12 +756,16 @@ class Plan:
                 body.add(bn_final_record(gs.pending_final, True))
                 gs.pending_final = []
         for r in body.recs:
+            if r.kind == L.OP_CONV_WGRAD:
+                r.flags |= Record.OPF_SIDE  # nothing later in the list reads a weight gradient
             bw.add(r)
         self.din_written = [v.grad and bool(gs.inited.get(id(v.segs[0].buf)))
                             for v in ins]
-        bw.add(Record(L.OP_SUM_REP, L.SumRepRec, {"dst": Ptr(S_PGRAD), "src": Ptr(S_WREP),
+        fold = Record(L.OP_SUM_REP, L.SumRepRec, {"dst": Ptr(S_PGRAD), "src": Ptr(S_WREP),
                                                   "n": g.pgrad_size, "stride": g.pgrad_size,
-                                                  "nrep": L.WREP}, label="sum_wgrad_replicas"))
+                                                  "nrep": L.WREP}, label="sum_wgrad_replicas")
+        fold.flags |= Record.OPF_JOIN  # every forked weight gradient is in the replicas
+        bw.add(fold)
         # finalisation of BN / PReLU / conv-bias-before-BN gradients
         conv_before = {id(bnr): mod for mod, bnr in gs.bias_from_bn}
         items = []

@@ -129,7 +129,7 @@ class Runner:
         for j, t in enumerate(tensors):
             tab[S_TENSOR0 + j] = t.data_ptr()
         with torch.cuda.device(dev):
-            p.bwd.run(tab, L.stream_ptr(dev))
+            p.bwd.run(tab, L.stream_ptr(dev), L.side_stream_ptr(dev))
         g = p.graph
         pgrads = []
         for k in g.param_names:

@@ -133,7 +133,7 @@ class Trainer:
         L.check(lib.isg_bce_sigmoid(self.logits.data_ptr(), self.target.data_ptr(), n,
                                     self.loss_acc.data_ptr(), self.dlogits.data_ptr(),
                                     1.0 / n, st), "bce")
-        self.plan.bwd.run(self.table, st)
+        self.plan.bwd.run(self.table, st, L.side_stream_ptr(self.device))
 
     def _adam(self):
         L.check(L.lib().isg_adam_dev(self.flat.data_ptr(), self.grad_flat.data_ptr(),
@@ -157,7 +157,7 @@ class Trainer:
         'coll' (eager RCCL all-reduce), 'tic'/'toc' (timing events around one op).
         split=(phase, idx) isolates op `idx` of the forward/backward list."""
         def run_list(ol):
-            return lambda: ol.run(self.table, L.stream_ptr(self.device))
+            return lambda: ol.run(self.table, L.stream_ptr(self.device), L.side_stream_ptr(self.device))
         units = []
         for phase, ol in (("fwd", self.plan.fwd), ("bwd", self.plan.bwd)):
             if split and split[0] == phase:
