@@ -13,6 +13,9 @@
 #include "../../include/isg.h"
 
 static thread_local std::string g_last_error;
+static thread_local bool g_fin_handled = false;
+
+void isg_fin_note_handled() { g_fin_handled = true; }
 
 
 int32_t isg_set_error(int32_t code, const char* fmt, ...) {
@@ -197,7 +200,31 @@ struct Fix {
     int64_t offset;
 };
 
+static int32_t run_op_raw(int32_t kind, char* buf, isg_stream_t st);
+
+// BN finalisation the producing kernel did not fuse (its launcher did not report
+// isg_fin_note_handled): one isg_bn_finalize launch per sink, as before the fusion.
+static int32_t fin_fallback(const isg_sinks* sk, isg_stream_t st) {
+    if (!sk || !sk->fin_counter || g_fin_handled) return ISG_OK;
+    for (int i = 0; i < sk->nsink && i < ISG_MAX_SEGS; ++i) {
+        if (!sk->s[i].fin_mode) continue;
+        isg_bn b = sk->s[i].fin_bn;
+        if (int32_t e = isg_bn_finalize(&b, 1, sk->s[i].fin_mode == 2 ? 1 : 0, st)) return e;
+    }
+    return ISG_OK;
+}
+
 static int32_t run_op(int32_t kind, char* buf, isg_stream_t st) {
+    g_fin_handled = false;
+    int32_t rc = run_op_raw(kind, buf, st);
+    if (rc) return rc;
+    const isg_sinks* sk = nullptr;
+    if (kind == OP_CONV_FWD || kind == OP_CONV_DGRAD || kind == OP_CONVT_FWD) sk = &((ConvRec*)buf)->out;
+    else if (kind == OP_MAXPOOL_BWD) sk = &((PoolRec*)buf)->dx;
+    return fin_fallback(sk, st);
+}
+
+static int32_t run_op_raw(int32_t kind, char* buf, isg_stream_t st) {
     int32_t rc = 0;
     switch (kind) {
         case OP_CONV_FWD: {

@@ -283,6 +283,76 @@ ISG_DEV bool sinks_need_red(const isg_sinks& sk) {
     return false;
 }
 
+// ---- fused BatchNorm finalisation ---------------------------------------------------
+// Every thread of every workgroup of a launch whose sinks carry fin_mode calls this LAST
+// (no early return before it). The statistics are written only by device-scope atomics,
+// which are performed at the memory side: once a workgroup's waves have retired them
+// (vmcnt(0)) no release fence is needed, the ticket alone publishes. Tickets are two
+// level — 32 sub-counters, the last arriver of each bumps the top counter — so at most
+// ~nb/32 workgroups contend on one address. The workgroup that completes the top counter
+// acquires and evaluates the coefficients (fp64, isg_bn_finalize's math), then re-zeroes
+// the counters. Counter block: ISG_FIN_CTR uint32 (top, then 32 subs), zeroed.
+#define ISG_FIN_SUBS 32
+ISG_DEV bool fin_last_block(uint32_t* ctr) {
+    __shared__ int s_last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0 && threadIdx.y == 0) {
+        const unsigned nb = gridDim.x * gridDim.y * gridDim.z;
+        const unsigned b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+        bool last;
+        if (nb <= 2 * ISG_FIN_SUBS) {
+            last = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nb - 1;
+        } else {
+            const unsigned sub = b % ISG_FIN_SUBS;
+            const unsigned ns = nb / ISG_FIN_SUBS + (sub < nb % ISG_FIN_SUBS ? 1u : 0u);
+            last = __hip_atomic_fetch_add(ctr + 1 + sub, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ns - 1 &&
+                   __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ISG_FIN_SUBS - 1;
+        }
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        s_last = last ? 1 : 0;
+    }
+    __syncthreads();
+    return s_last != 0;
+}
+
+// Block-cooperative: the coefficients of one sink's fin_bn (fp64, isg_bn_finalize's math).
+ISG_DEV void fin_sink(const isg_sink& k) {
+    if (!k.fin_mode) return;
+    const int tid = threadIdx.x + threadIdx.y * blockDim.x, nt = blockDim.x * blockDim.y;
+    isg_bn bn = k.fin_bn;
+    float* const out = bn.coef;
+    bn.coef = nullptr;  // evaluate from the statistics
+    for (int c = tid; c < bn.C; c += nt) {
+        if (k.fin_mode == 1) {
+            const ChanCoef f = fwd_coef(bn, nullptr, c);
+            reinterpret_cast<f32x4*>(out)[c] = f32x4{f.c0, f.c1, f.c2, 0.f};
+        } else {
+            const ChanCoef f = bwd_coef(bn, c);
+            reinterpret_cast<f32x4*>(out)[bn.C + c] = f32x4{f.c0, f.c1, f.c2, f.c3};
+        }
+    }
+}
+
+ISG_DEV void fin_reset(uint32_t* ctr) {
+    const int tid = threadIdx.x + threadIdx.y * blockDim.x;
+    if (tid <= ISG_FIN_SUBS) __hip_atomic_store(ctr + tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+ISG_DEV void sinks_finalize(const isg_sinks& sk) {
+    uint32_t* const ctr = sk.fin_counter;
+    if (!ctr || !fin_last_block(ctr)) return;
+    for (int s = 0; s < sk.nsink; ++s) fin_sink(s == 2 ? sk.s[2] : (s == 1 ? sk.s[1] : sk.s[0]));
+    fin_reset(ctr);
+}
+
+// Host: launchers of kernels that end in sinks_finalize() report it here, so the
+// executor knows whether a separate finalisation launch is still needed.
+void isg_fin_note_handled();
+
 // ---- diagnostic stamps (built only into the tools/kbench harness library) -------------
 // STAMP(i): thread 0 of each workgroup records s_memrealtime (100 MHz, chip-global) in
 // slot i of its 8-slot record. Compiled out of libisg.so.

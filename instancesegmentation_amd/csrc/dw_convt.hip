@@ -125,6 +125,7 @@ ISG_DEV bool sink1_needs_red(const isg_sink& k) {
 struct DwArgs {
     isg_vseg x;      // fwd: input; dgrad: dy
     isg_sink out;
+    uint32_t* fin_counter;  // fused BN finalisation ticket (isg_sinks.fin_counter)
     const float* w;  // [C][KH][KW]
     int N, C, H, W, OH, OW, KH, KW, PH, PW, DH, DW;
 };
@@ -161,6 +162,10 @@ __global__ __launch_bounds__(kThreads) void dw_kernel(DwArgs a) {
     if (sink1_needs_red(a.out)) {
         block_reduce<3>(red, sh);
         if (threadIdx.x == 0) sink1_flush(a.out, c, red);
+    }
+    if (a.fin_counter && fin_last_block(a.fin_counter)) {
+        fin_sink(a.out);
+        fin_reset(a.fin_counter);
     }
 }
 
@@ -357,10 +362,11 @@ int32_t isg_depthwise_fwd(const isg_conv_geom* g, const isg_vtensor* x, const fl
                           const isg_sinks* out, hipStream_t st) {
     if (x->nseg != 1 || out->nsink != 1 || g->SH != 1 || g->SW != 1 || g->Ci != g->Co)
         return isg_set_error(ISG_ERR_UNSUPPORTED, "depthwise fwd: need 1 seg/sink, stride 1");
-    DwArgs a{x->s[0], out->s[0], w, g->N, g->Ci, g->H, g->W, g->OH, g->OW,
+    DwArgs a{x->s[0], out->s[0], out->fin_counter, w, g->N, g->Ci, g->H, g->W, g->OH, g->OW,
              g->KH, g->KW, g->PH, g->PW, g->DH, g->DW};
     dim3 grid((unsigned)(((int64_t)g->OH * g->OW + kThreads - 1) / kThreads), g->Ci, g->N);
     hipLaunchKernelGGL(dw_kernel<false>, grid, dim3(kThreads), 0, st, a);
+    if (a.fin_counter) isg_fin_note_handled();
     return isg_check_launch("dw_kernel<fwd>");
 }
 
@@ -368,10 +374,11 @@ int32_t isg_depthwise_dgrad(const isg_conv_geom* g, const isg_vtensor* dy, const
                             const isg_sinks* dx, hipStream_t st) {
     if (dy->nseg != 1 || dx->nsink != 1 || g->SH != 1 || g->SW != 1 || g->Ci != g->Co)
         return isg_set_error(ISG_ERR_UNSUPPORTED, "depthwise dgrad: need 1 seg/sink, stride 1");
-    DwArgs a{dy->s[0], dx->s[0], w, g->N, g->Ci, g->H, g->W, g->OH, g->OW,
+    DwArgs a{dy->s[0], dx->s[0], dx->fin_counter, w, g->N, g->Ci, g->H, g->W, g->OH, g->OW,
              g->KH, g->KW, g->PH, g->PW, g->DH, g->DW};
     dim3 grid((unsigned)(((int64_t)g->H * g->W + kThreads - 1) / kThreads), g->Ci, g->N);
     hipLaunchKernelGGL(dw_kernel<true>, grid, dim3(kThreads), 0, st, a);
+    if (a.fin_counter) isg_fin_note_handled();
     return isg_check_launch("dw_kernel<dgrad>");
 }
 

@@ -261,6 +261,7 @@ __global__ __launch_bounds__(kThreads) void pw_kernel(PwArgs a) {
             }
         }
     }
+    sinks_finalize(a.out);
 }
 
 }  // namespace
@@ -299,5 +300,6 @@ int32_t isg_pw_gemm(const isg_conv_geom* g, const isg_vtensor* src, const float*
         case 5: case 6: hipLaunchKernelGGL(pw_kernel<6>, grid, dim3(kThreads), 0, st, a); break;
         default: hipLaunchKernelGGL(pw_kernel<8>, grid, dim3(kThreads), 0, st, a); break;
     }
+    if (out->fin_counter) isg_fin_note_handled();
     return isg_check_launch("pw_kernel");
 }

@@ -372,6 +372,7 @@ __global__ __launch_bounds__(kThreads) void tap_conv_kernel(TapArgs a) {
             sink_row_flush(a.out, row, r3[0], r3[1], r3[2]);
         }
     }
+    sinks_finalize(a.out);
 }
 
 template <int MT, int G, bool YB, bool PAIR>
@@ -391,6 +392,7 @@ int32_t tap_launch(const TapArgs& a, size_t lds, hipStream_t st) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, kThreads, lds) != hipSuccess || occ < 1) occ = 1;
     const int grid = std::max(1, std::min(a.ntiles, occ * cus));
     hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(kThreads), lds, st, a);
+    if (a.out.fin_counter) isg_fin_note_handled();
     return isg_check_launch("tap_conv_kernel");
 }
 

@@ -286,6 +286,11 @@ class Graph:
         # finalised coefficients (isg_bn.coef): 8*C floats = 4*C doubles, 64-B aligned
         ref.coef_off = self.stats_size
         self.stats_size += (4 * bn.num_features + 7) // 8 * 8
+        # tickets of the fused finalisation (isg_sinks.fin_counter: 33 uint32 each),
+        # forward and backward, inside the forward's stats memset
+        ref.ctr_fwd = self.stats_size
+        ref.ctr_bwd = self.stats_size + 24
+        self.stats_size += 48
         self.bns.append(ref)
         self.bn_by_mod[id(bn)] = ref
         return ref
@@ -390,6 +395,25 @@ class Graph:
 # ---------------------------------------------------------------------------------
 # spec helpers
 _BN_FINAL = os.environ.get("ISG_NO_BN_FINAL", "0") != "1"  # debugging switch
+# finalise BN coefficients in the producing kernel's last workgroup (isg_sink.fin_*)
+# instead of a separate OP_BN_FINAL launch. Opt-in: measured slower on MI355X (each
+# workgroup's returning ticket atomic plus the last workgroup's fp64 tail cost more than
+# the ~2.4 us finalisation launch they replace: 7.16 vs 6.5 ms/step).
+_BN_FUSE = _BN_FINAL and os.environ.get("ISG_BN_FUSE", "0") == "1"
+
+
+def sinks_spec(sinks):
+    """isg_sinks spec from sink specs; a sink's private '_fin_ctr' (the ticket of a fused
+    BN finalisation) becomes the launch's fin_counter."""
+    ctr = None
+    for sk in sinks:
+        c = sk.pop("_fin_ctr", None)
+        if c is not None and ctr is None:
+            ctr = c
+    out = {"s": sinks, "nsink": len(sinks)}
+    if ctr is not None:
+        out["fin_counter"] = ctr
+    return out
 
 
 def bn_spec(bnr, train, coef=True):
@@ -477,7 +501,12 @@ class GradState:
                 s["slope_grad"] = Ptr(S_STATS, val.slope.acc_off * 8)
                 val.slope.used_in_bwd = True
             if val.bn is not None:
-                self.pending_final.append(val.bn)
+                if train and _BN_FUSE:
+                    s["fin_bn"] = s["bn"]
+                    s["fin_mode"] = 2
+                    s["_fin_ctr"] = Ptr(S_STATS, val.bn.ctr_bwd * 8)
+                else:
+                    self.pending_final.append(val.bn)
             return s
         d = self.dbuf(val.buf)
         first = self.mark(val.buf, val.c0, val.C)
@@ -532,11 +561,17 @@ class ConvOp:
                 "mode": L.SINK_STORE}
         if self.mod.bias is not None:
             sink["bias"] = g.tptr(self.mod, "bias")
+        self.fused_final = False
         if self.bnr is not None and g.train:
             sink["stats"] = Ptr(S_STATS, self.bnr.stats_off * 8)
+            if _BN_FUSE:
+                sink["fin_bn"] = bn_spec(self.bnr, True)
+                sink["fin_mode"] = 1
+                sink["_fin_ctr"] = Ptr(S_STATS, self.bnr.ctr_fwd * 8)
+                self.fused_final = True
         ge = self.geom
         rec = {"g": ge, "a": vtensor(segs, g.N, ge["H"], ge["W"]), "w": g.tptr(self.mod, "weight"),
-               "out": {"s": [sink], "nsink": 1}}
+               "out": sinks_spec([sink])}
         kind = L.OP_CONVT_FWD if self.kind == "convT" else L.OP_CONV_FWD
         fl, xb, yb, wb = self._cost()
         ops.add(Record(kind, L.ConvRec, rec, label=self.out.name, flops=fl, nbytes=xb + yb + wb))
@@ -557,7 +592,7 @@ class ConvOp:
             for v in self.x.segs:
                 sinks.append(gs.sink_for(v, c, g.train))
                 c += v.C
-            sk = {"s": sinks, "nsink": len(sinks)}
+            sk = sinks_spec(sinks)
             w = g.tptr(self.mod, "weight")
             if self.kind == "convT":
                 # dx_T = conv(dy_T, W) with the forward conv's stride/pad/kernel
@@ -622,7 +657,7 @@ class PoolOp:
         ops.add(Record(L.OP_MAXPOOL_BWD, L.PoolRec,
                        {"x": vtensor(segs, g.N, self.x.H, self.x.W), "k": self.k,
                         "dout": d.ptr(self.c0), "dout_ns": d.n_stride,
-                        "dx": {"s": sinks, "nsink": len(sinks)}}, label="dx_" + self.out.name))
+                        "dx": sinks_spec(sinks)}, label="dx_" + self.out.name))
 
 
 class TailOp:
@@ -706,7 +741,7 @@ class Plan:
         for op in g.ops:
             op.fwd(fw)
             bnr = getattr(op, "bnr", None)
-            if train and bnr is not None and _BN_FINAL:
+            if train and bnr is not None and _BN_FINAL and not getattr(op, "fused_final", False):
                 fw.add(bn_final_record([bnr], False))
         if train and g.bns:
             items = []
