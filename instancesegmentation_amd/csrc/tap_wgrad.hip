@@ -1,0 +1,334 @@
+// Weight gradient of the narrow dense spatial convs on v_mfma_f32_16x16x4_f32: the stem
+// 5x5 s2 convs (segment.py:23-26; 60 % of the network's FLOPs and the largest single
+// kernel of the train step), the dense 3x3 of BottleneckDim (:242), the head 3x3 (:437)
+// and the 2x2 s2 down convs (:121) — every dense conv with at most 16 output channels,
+// source stride 1 or 2 and at most 32 taps.
+//
+//   dW[co][ci][kh][kw] = sum_{n,oy,ox} dy[co][n][oy][ox] * x[ci][n][S*oy - P + kh*D][...]
+//
+// GEMM: rows i = co (16), columns j = (ci of a 4-channel chunk, tap), reduction over the
+// output pixels in steps of 4 along an output row. blockIdx.y = the channel chunk;
+// persistent workgroups walk 4 x BX output tiles (wave w owns tile row w). Per tile the
+// workgroup stages the chunk's input halo (a stride-2 source as even / odd column planes,
+// the producer's BatchNorm + activation applied on load; wave w stages channel
+// 4*chunk + w) and the tile's dy rows (BatchNorm backward rebuilt on load; wave w stages
+// tile row w of all 16 rows); the NEXT tile's loads are issued into registers before
+// this tile's MFMAs. Each column's (channel, tap) halo offset is a per-lane constant and
+// the pixel step a wave-uniform one, so the MFMA loop is one ds_read per MFMA plus one dy
+// read per step shared by the NT column tiles. Accumulators live across all of a
+// workgroup's tiles; one f32 atomic per dW element per workgroup goes to one of the
+// ISG_WREP replicas.
+//
+// MFMA lane maps (16x16x4 f32): A[i=co][k=pixel] = dy (lane: co = l&15, pixel = l>>4),
+// B[k][j] = halo (lane: pixel = l>>4, column j = l&15), D lane: co = (l>>4)*4+r, j = l&15.
+#include "stage.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kBY = 4;      // tile rows = waves
+constexpr int kPF = 16;     // staged halo rows per wave (registers)
+constexpr int kMaxNT = 8;   // column tiles per chunk (4 channels x taps <= 128)
+constexpr int kMaxC = 64;
+
+struct TwArgs {
+    isg_vtensor dy;   // N x Co x OH x OW (Co <= 16)
+    isg_vtensor x;    // N x C x H x W
+    float* dw;        // [Co][C][KH][KW], replica r at dw + r*rep_stride
+    float* dbias;     // [Co] or NULL
+    int64_t rep_stride;
+    int nrep;
+    int N, C, Co, H, W, OH, OW, KH, KW, SH, SW, PH, PW, DH, DW, KK;
+    int BX, tiles_x, tiles_y, ntiles;
+    int HR, HCu, PS, RS, CHS, DQ;  // halo rows / units / LDS layout; dy LDS row stride
+    uint32_t m_tpi, m_tx;          // magic divisors (0 = divide by 1)
+};
+
+template <int NT, bool YB, bool PAIR>
+__global__ __launch_bounds__(kThreads) void tap_wgrad_kernel(TwArgs a) {
+    constexpr int MX = PAIR ? 2 : 1;
+    extern __shared__ float lds[];
+    float* const Xs = lds;              // [4][CHS]
+    float* const Ds = lds + 4 * a.CHS;  // [16][DQ]
+    __shared__ ChT tabx[kMaxC];
+    __shared__ ChT taby[16];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
+    const int kq = lane >> 4, pl = lane & 15;
+    const int ch = blockIdx.y;  // 4-channel chunk
+    for (int c = tid; c < a.C; c += kThreads) tabx[c] = ch_table_entry(a.x, c, (int64_t)a.H * a.W);
+    for (int c = tid; c < a.Co; c += kThreads) taby[c] = ch_table_entry(a.dy, c, (int64_t)a.OH * a.OW);
+    __syncthreads();
+
+    // per-lane column offsets into the halo: column j = ci_l*KK + tap (ci_l < 4), pixel kq
+    int boff[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const int j = t * 16 + pl;
+        int o = 0;
+        if (j < 4 * a.KK) {
+            const int cl = j / a.KK, tap = j - cl * a.KK;
+            const int kh = tap / a.KW, kw = tap - kh * a.KW;
+            const int cx = kw * a.DW;
+            o = cl * a.CHS + kh * a.DH * a.RS + (cx % MX) * a.PS + cx / MX;
+        }
+        boff[t] = o + kq;  // 4 consecutive output pixels = 4 consecutive plane units
+    }
+    const int aoff = pl * a.DQ + wave * a.BX + kq;  // dy row co = pl, tile row = wave
+
+    const int tpi = a.tiles_x * a.tiles_y;
+    auto qdiv = [](int x, uint32_t m) { return m ? (int)__umulhi((uint32_t)x, m) : x; };
+    auto tile_geo = [&](int tile, int& n, int& oy0, int& ox0) {
+        n = qdiv(tile, a.m_tpi);
+        const int tr = tile - n * tpi;
+        const int tyi = qdiv(tr, a.m_tx);
+        oy0 = tyi * kBY;
+        ox0 = (tr - tyi * a.tiles_x) * a.BX;
+    };
+    const uint32_t xplane = (uint32_t)a.H * a.W * 4u, yplane = (uint32_t)a.OH * a.OW * 4u;
+
+    typedef float v2f __attribute__((ext_vector_type(2)));
+    v2f v[kPF];
+    float dv[16], dyy[16];
+    uint32_t rowok = 0;
+    bool colok = false, dok = false;
+    auto load_tile = [&](int tile) {
+        int n, oy0, ox0;
+        tile_geo(tile, n, oy0, ox0);
+        // x halo rows of channel 4*ch + wave
+        {
+            const int c = ch * 4 + wave;
+            const ChT t = tabx[min(c, a.C - 1)];
+            const auto xr = __builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(t.p + (int64_t)n * t.ns),
+                                                              (short)0, (int)xplane, 0x00020000);
+            const int sy0 = oy0 * a.SH - a.PH, sx0 = ox0 * a.SW - a.PW;
+            const int ix = sx0 + MX * lane;
+            colok = c < a.C && lane < a.HCu && ix >= 0 && ix < a.W;
+            const uint32_t voff = colok ? (uint32_t)ix * 4u : 0x80000000u;
+            rowok = 0;
+#pragma unroll
+            for (int r = 0; r < kPF; ++r) {
+                if (r < a.HR) {
+                    const int iy = sy0 + r;
+                    if ((unsigned)iy < (unsigned)a.H) {
+                        rowok |= 1u << r;
+                        const uint32_t o = colok ? voff + (uint32_t)iy * (uint32_t)a.W * 4u : voff;
+                        if constexpr (PAIR)
+                            v[r] = __builtin_bit_cast(v2f, __builtin_amdgcn_raw_buffer_load_b64(xr, o, 0, 0));
+                        else
+                            v[r][0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, o, 0, 0));
+                    }
+                }
+            }
+        }
+        // dy: tile row oy0 + wave of every row co
+        {
+            const int oy = oy0 + wave, ox = ox0 + lane;
+            dok = lane < a.BX && ox < a.OW && oy < a.OH;
+            const uint32_t o = dok ? ((uint32_t)oy * (uint32_t)a.OW + (uint32_t)ox) * 4u : 0x80000000u;
+#pragma unroll
+            for (int co = 0; co < 16; ++co) {
+                if (co < a.Co) {
+                    const ChT ty = taby[co];
+                    const auto dr = __builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(ty.p + (int64_t)n * ty.ns),
+                                                                      (short)0, (int)yplane, 0x00020000);
+                    dv[co] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dr, o, 0, 0));
+                    if constexpr (YB) {
+                        const auto yr = __builtin_amdgcn_make_buffer_rsrc(
+                            (void*)uniform_ptr(ty.y + (int64_t)n * ty.yns), (short)0, (int)yplane, 0x00020000);
+                        dyy[co] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(yr, o, 0, 0));
+                    }
+                }
+            }
+        }
+    };
+    auto store_tile = [&]() {
+        {
+            const int c = ch * 4 + wave;
+            const ChT t = tabx[min(c, a.C - 1)];
+            float* const xs = Xs + wave * a.CHS + lane;
+            if (lane < a.PS) {
+#pragma unroll
+                for (int r = 0; r < kPF; ++r) {
+                    if (r < a.HR) {
+                        const bool ok = ((rowok >> r) & 1u) && colok;
+                        float x0 = 0.f, x1 = 0.f;
+                        if (ok) {
+                            x0 = ch_xform(t.xf, t.act, t.k, v[r][0], v[r][0]);
+                            if constexpr (PAIR) x1 = ch_xform(t.xf, t.act, t.k, v[r][1], v[r][1]);
+                        }
+                        xs[r * a.RS] = x0;
+                        if constexpr (PAIR) xs[r * a.RS + a.PS] = x1;
+                    }
+                }
+            }
+        }
+        if (lane < a.BX) {
+            float* const ds = Ds + wave * a.BX + lane;
+#pragma unroll
+            for (int co = 0; co < 16; ++co) {
+                float d = 0.f;
+                if (co < a.Co && dok) {
+                    const ChT ty = taby[co];
+                    d = ch_xform(ty.xf, ty.act, ty.k, dv[co], YB ? dyy[co] : dv[co]);
+                }
+                ds[co * a.DQ] = d;
+            }
+        }
+    };
+
+    f32x4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float bsum = 0.f;  // dbias partial: sum of this lane's dy values (row co = pl)
+
+    int tile = blockIdx.x;
+    if (tile < a.ntiles) load_tile(tile);
+    const int nstep = a.BX >> 2;
+    const int xrow = wave * a.SH * a.RS;  // halo row of this wave's tile row
+    while (tile < a.ntiles) {
+        __syncthreads();  // LDS free
+        store_tile();
+        __syncthreads();
+        const int ntile = tile + gridDim.x;
+        if (ntile < a.ntiles) load_tile(ntile);
+        for (int s = 0; s < nstep; ++s) {
+            const float av = Ds[aoff + 4 * s];
+            bsum += av;
+            const int xo = xrow + 4 * s;  // 4 output pixels = 4 plane units (stride 1 or 2)
+            float bv[NT];
+#pragma unroll
+            for (int t = 0; t < NT; ++t) bv[t] = Xs[boff[t] + xo];
+#pragma unroll
+            for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[t], acc[t], 0, 0, 0);
+        }
+        tile = ntile;
+    }
+
+    // ---- reduce the 4 waves' partials in LDS (fixed order), one atomic per dW element
+    __syncthreads();
+    float* const red = lds;  // [4][16 rows][NT*16 cols]
+    const int ncol = NT * 16;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[(wave * 16 + kq * 4 + r) * ncol + t * 16 + pl] = acc[t][r];
+    __syncthreads();
+    float* const dwr = a.dw + (int64_t)(blockIdx.x % a.nrep) * a.rep_stride;
+    for (int e = tid; e < 16 * ncol; e += kThreads) {
+        const int co = e / ncol, j = e - co * ncol;
+        const int cl = j / a.KK, tap = j - cl * a.KK;
+        const int ci = ch * 4 + cl;
+        if (co < a.Co && j < 4 * a.KK && ci < a.C) {
+            const float s = ((red[e] + red[16 * ncol + e]) + red[32 * ncol + e]) + red[48 * ncol + e];
+            atomicAdd(&dwr[((int64_t)co * a.C + ci) * a.KK + tap], s);
+        }
+    }
+    if (a.dbias && ch == 0) {
+        // lanes with the same co (pl) in the 4 kq groups and 4 waves
+        __syncthreads();
+        float* const rb = lds;
+        rb[wave * 64 + lane] = bsum;
+        __syncthreads();
+        if (tid < 16 && tid < a.Co) {
+            float s = 0.f;
+            for (int w = 0; w < 4; ++w)
+                for (int q = 0; q < 4; ++q) s += rb[w * 64 + q * 16 + tid];
+            atomicAdd(&(a.dbias + (int64_t)(blockIdx.x % a.nrep) * a.rep_stride)[tid], s);
+        }
+    }
+}
+
+template <int NT, bool YB, bool PAIR>
+int32_t tw_launch(const TwArgs& a, int nchunk, size_t lds, hipStream_t st) {
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+            cus = 256;
+    }
+    auto k = tap_wgrad_kernel<NT, YB, PAIR>;
+    if (lds > 48 * 1024 &&
+        hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+        return isg_check_launch("tap_wgrad_kernel: dynamic LDS");
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, kThreads, lds) != hipSuccess || occ < 1) occ = 1;
+    // workgroups per chunk: fill the chip once over all chunks
+    const int per = std::max(1, std::min(a.ntiles, (occ * cus + nchunk - 1) / nchunk));
+    hipLaunchKernelGGL(k, dim3((unsigned)per, (unsigned)nchunk), dim3(kThreads), lds, st, a);
+    return isg_check_launch("tap_wgrad_kernel");
+}
+
+template <int NT>
+int32_t tw_launch_v(const TwArgs& a, int nchunk, size_t lds, bool yb, bool pair, hipStream_t st) {
+    if (pair) return yb ? tw_launch<NT, true, true>(a, nchunk, lds, st) : tw_launch<NT, false, true>(a, nchunk, lds, st);
+    return yb ? tw_launch<NT, true, false>(a, nchunk, lds, st) : tw_launch<NT, false, false>(a, nchunk, lds, st);
+}
+
+}  // namespace
+
+// Returns 1 if launched, 0 if the shape is not for this kernel, <0 on error.
+int32_t isg_tap_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, float* dw,
+                      float* dbias, int64_t rep_stride, int32_t nrep, hipStream_t st) {
+    static const bool off = getenv("ISG_NO_TAP_WGRAD") != nullptr;
+    if (off || g->groups != 1 || g->Co > 16 || g->Ci > kMaxC) return 0;
+    if (g->SH != g->SW || (g->SH != 1 && g->SH != 2)) return 0;
+    const int KK = g->KH * g->KW;
+    int NT = (4 * KK + 15) / 16;
+    if (NT > kMaxNT) return 0;
+    NT = NT == 5 ? 6 : NT == 7 ? 8 : NT;  // the instantiated column-tile counts
+    if (g->SH == 2 && (g->PW % 2 || g->W % 2)) return 0;  // column pairs start even
+    for (int i = 0; i < x->nseg; ++i)
+        if (x->s[i].xform == ISG_XF_BN_BWD) return 0;  // the gathered side never needs y
+    if ((int64_t)g->H * g->W * 4 >= (1ll << 31) || (int64_t)g->OH * g->OW * 4 >= (1ll << 31)) return 0;
+    TwArgs a{};
+    a.dy = *dy; a.x = *x; a.dw = dw; a.dbias = dbias;
+    a.rep_stride = nrep > 1 ? rep_stride : 0;
+    a.nrep = nrep < 1 ? 1 : nrep;
+    a.N = g->N; a.C = g->Ci; a.Co = g->Co; a.H = g->H; a.W = g->W; a.OH = g->OH; a.OW = g->OW;
+    a.KH = g->KH; a.KW = g->KW; a.SH = g->SH; a.SW = g->SW; a.PH = g->PH; a.PW = g->PW;
+    a.DH = g->DH; a.DW = g->DW; a.KK = KK;
+    const int mx = g->SW;
+    const int ext_x = (g->KW - 1) * g->DW, ext_y = (g->KH - 1) * g->DH;
+    // tile width: a multiple of 4 whose halo row fits 64 lanes, split evenly
+    const int bxmax = (mx == 1 ? 64 - ext_x : (128 - ext_x - 1) / 2 + 1) & ~3;
+    if (bxmax < 4) return 0;
+    a.tiles_x = (g->OW + bxmax - 1) / bxmax;
+    a.BX = ((g->OW + a.tiles_x - 1) / a.tiles_x + 3) & ~3;
+    const int HC = mx * (a.BX - 1) + ext_x + 1;
+    a.HCu = (HC + mx - 1) / mx;
+    if (a.HCu > 64 || a.BX > 64) return 0;
+    a.PS = a.HCu;
+    a.RS = mx * a.PS;
+    a.HR = g->SH * (kBY - 1) + ext_y + 1;
+    if (a.HR > kPF) return 0;
+    a.CHS = a.HR * a.RS;
+    a.CHS += ((16 - a.CHS % 32) + 32) % 32;
+    a.DQ = kBY * a.BX;
+    a.DQ += ((16 - a.DQ % 32) + 32) % 32;
+    a.tiles_y = (g->OH + kBY - 1) / kBY;
+    const int64_t tpi = (int64_t)a.tiles_x * a.tiles_y;
+    a.ntiles = (int)(g->N * tpi);
+    if ((int64_t)a.ntiles * tpi >= (1ll << 32)) return 0;
+    auto magic = [](int64_t d) { return d == 1 ? 0u : (uint32_t)(((1ull << 32) + d - 1) / d); };
+    a.m_tpi = magic(tpi);
+    a.m_tx = magic(a.tiles_x);
+    const int nchunk = (g->Ci + 3) / 4;
+    size_t lds = (size_t)(4 * a.CHS + 16 * a.DQ) * sizeof(float);
+    lds = std::max(lds, (size_t)(4 * 16 * NT * 16) * sizeof(float));  // the wave reduction
+    if (lds > 64 * 1024) return 0;
+    bool yb = false;
+    for (int i = 0; i < dy->nseg; ++i) yb |= dy->s[i].xform == ISG_XF_BN_BWD;
+    const bool pair = mx == 2;
+    int32_t e;
+    switch (NT) {
+        case 1: e = tw_launch_v<1>(a, nchunk, lds, yb, pair, st); break;
+        case 2: e = tw_launch_v<2>(a, nchunk, lds, yb, pair, st); break;
+        case 3: e = tw_launch_v<3>(a, nchunk, lds, yb, pair, st); break;
+        case 4: e = tw_launch_v<4>(a, nchunk, lds, yb, pair, st); break;
+        case 6: e = tw_launch_v<6>(a, nchunk, lds, yb, pair, st); break;
+        default: e = tw_launch_v<8>(a, nchunk, lds, yb, pair, st); break;
+    }
+    return e ? e : 1;
+}

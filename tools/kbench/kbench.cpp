@@ -135,6 +135,11 @@ int main(int argc, char** argv) {
         t0 = std::min(t0, h[b * 8]);
         tend = std::max(tend, h[b * 8 + 4]);
     }
+    if (nb == 0) {
+        printf("%s N%d Ci%d %dx%d -> Co%d %dx%d k%d s%d p%d d%d: %.2f us/launch (%d reps)\n", op, N,
+               Ci, H, W, Co, g.OH, g.OW, k, s, p, d, 1e3 * ms / reps, reps);
+        return 0;
+    }
     printf("%s N%d Ci%d %dx%d -> Co%d %dx%d k%d s%d p%d d%d: %.2f us/launch (%d reps); "
            "stamped launch %d blocks, span %.2f us\n",
            op, N, Ci, H, W, Co, g.OH, g.OW, k, s, p, d, 1e3 * ms / reps, reps, nb,
