@@ -177,7 +177,7 @@ struct MemsetRec {
 struct OpHdr {
     int32_t kind, desc_bytes, nfix, flags;  // flags: ISG_OPF_SIDE | ISG_OPF_JOIN
 };
-enum { ISG_OPF_SIDE = 1, ISG_OPF_JOIN = 2 };
+enum { ISG_OPF_SIDE = 1, ISG_OPF_JOIN = 2, ISG_OPF_FORK_NOW = 4 };  // FORK_NOW: no batching
 
 // fork / join events of the executor's side stream, one pair per device (created on
 // first use, never destroyed; timing disabled)
@@ -366,7 +366,7 @@ int32_t isg_exec_ms(const void* ops, int32_t nops, void* const* table, isg_strea
             // deferred: launched in batches behind one fork (a later fork only adds
             // dependencies, so batching is always safe)
             pending.emplace_back(h.kind, std::string(buf, buf + h.desc_bytes));
-            if ((int)pending.size() >= batch) rc = flush();
+            if ((int)pending.size() >= batch || (h.flags & ISG_OPF_FORK_NOW)) rc = flush();
         } else {
             rc = run_op(h.kind, buf, st);
         }

@@ -250,6 +250,8 @@ int32_t isg_pw_gemm(const isg_conv_geom* g, const isg_vtensor* src, const float*
                     const isg_sinks* out, bool dgrad, hipStream_t st);
 int32_t isg_tap_conv(const isg_conv_geom* g, const isg_vtensor* src, const float* w,
                      const isg_sinks* out, bool dgrad, hipStream_t st);
+int32_t isg_thin_conv(const isg_conv_geom* g, const isg_vtensor* src, const float* w,
+                      const isg_sinks* out, bool dgrad, hipStream_t st);
 
 static bool is_pointwise(const isg_conv_geom* g) {
     return g->KH == 1 && g->KW == 1 && g->SH == 1 && g->SW == 1 && g->PH == 0 && g->PW == 0 &&
@@ -262,6 +264,10 @@ int32_t isg_dense_conv_fwd(const isg_conv_geom* g, const isg_vtensor* x, const f
     if (int32_t e = check_sinks(out, g->Co, "conv fwd")) return e;
     static const bool special_off = getenv("ISG_GENERIC_CONV") != nullptr;
     if (!special_off && is_pointwise(g)) return isg_pw_gemm(g, x, w, out, false, st);
+    if (!special_off) {  // thin stride-1 convs on the VALU (thin_conv.hip)
+        const int32_t t = isg_thin_conv(g, x, w, out, false, st);
+        if (t != 0) return t < 0 ? t : 0;
+    }
     if (!special_off) {  // dense spatial conv, <= 48 output channels (tap_conv.hip)
         const int32_t t = isg_tap_conv(g, x, w, out, false, st);
         if (t != 0) return t < 0 ? t : 0;
@@ -293,6 +299,10 @@ int32_t isg_dense_conv_dgrad(const isg_conv_geom* g, const isg_vtensor* dy, cons
     if (int32_t e = check_sinks(dx, g->Ci, "conv dgrad")) return e;
     static const bool special_off = getenv("ISG_GENERIC_CONV") != nullptr;
     if (!special_off && is_pointwise(g)) return isg_pw_gemm(g, dy, w, dx, true, st);
+    if (!special_off) {
+        const int32_t t = isg_thin_conv(g, dy, w, dx, true, st);
+        if (t != 0) return t < 0 ? t : 0;
+    }
     if (!special_off) {
         const int32_t t = isg_tap_conv(g, dy, w, dx, true, st);
         if (t != 0) return t < 0 ? t : 0;

@@ -42,6 +42,11 @@ struct TwArgs {
     int BX, tiles_x, tiles_y, ntiles;
     int HR, HCu, PS, RS, CHS, DQ;  // halo rows / units / LDS layout; dy LDS row stride
     uint32_t m_tpi, m_tx;          // magic divisors (0 = divide by 1)
+    // column tile t, lane pl: channel pl>>2 of the chunk, tap gtap[t][pl&3] (-1: padding,
+    // reads the slot-0 tap's address, result discarded). Taps are grouped so that the 32
+    // lanes of a ds_read_b32 group hit 32 distinct banks (host: tw_layout).
+    int8_t gtap[8][4];
+    int dbg;  // ablation bits (ISG_TW_DBG, experiments only): 1 no MFMA loop, 2 no loads
 };
 
 template <int NT, bool YB, bool PAIR>
@@ -60,19 +65,16 @@ __global__ __launch_bounds__(kThreads) void tap_wgrad_kernel(TwArgs a) {
     for (int c = tid; c < a.Co; c += kThreads) taby[c] = ch_table_entry(a.dy, c, (int64_t)a.OH * a.OW);
     __syncthreads();
 
-    // per-lane column offsets into the halo: column j = ci_l*KK + tap (ci_l < 4), pixel kq
+    // per-lane column offsets into the halo (channel pl>>2, tap of the group), pixel kq
     int boff[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-        const int j = t * 16 + pl;
-        int o = 0;
-        if (j < 4 * a.KK) {
-            const int cl = j / a.KK, tap = j - cl * a.KK;
-            const int kh = tap / a.KW, kw = tap - kh * a.KW;
-            const int cx = kw * a.DW;
-            o = cl * a.CHS + kh * a.DH * a.RS + (cx % MX) * a.PS + cx / MX;
-        }
-        boff[t] = o + kq;  // 4 consecutive output pixels = 4 consecutive plane units
+        int tap = a.gtap[t][pl & 3];
+        if (tap < 0) tap = a.gtap[t][0];
+        if (tap < 0) tap = 0;  // an all-padding tile (NT rounded up)
+        const int kh = tap / a.KW, kw = tap - kh * a.KW;
+        const int cx = kw * a.DW;
+        boff[t] = (pl >> 2) * a.CHS + kh * a.DH * a.RS + (cx % MX) * a.PS + cx / MX + kq;
     }
     const int aoff = pl * a.DQ + wave * a.BX + kq;  // dy row co = pl, tile row = wave
 
@@ -183,15 +185,15 @@ __global__ __launch_bounds__(kThreads) void tap_wgrad_kernel(TwArgs a) {
     float bsum = 0.f;  // dbias partial: sum of this lane's dy values (row co = pl)
 
     int tile = blockIdx.x;
-    if (tile < a.ntiles) load_tile(tile);
-    const int nstep = a.BX >> 2;
+    if (tile < a.ntiles && !(a.dbg & 2)) load_tile(tile);
+    const int nstep = (a.dbg & 1) ? 0 : a.BX >> 2;
     const int xrow = wave * a.SH * a.RS;  // halo row of this wave's tile row
     while (tile < a.ntiles) {
         __syncthreads();  // LDS free
         store_tile();
         __syncthreads();
         const int ntile = tile + gridDim.x;
-        if (ntile < a.ntiles) load_tile(ntile);
+        if (ntile < a.ntiles && !(a.dbg & 2)) load_tile(ntile);
         for (int s = 0; s < nstep; ++s) {
             const float av = Ds[aoff + 4 * s];
             bsum += av;
@@ -217,9 +219,10 @@ __global__ __launch_bounds__(kThreads) void tap_wgrad_kernel(TwArgs a) {
     float* const dwr = a.dw + (int64_t)(blockIdx.x % a.nrep) * a.rep_stride;
     for (int e = tid; e < 16 * ncol; e += kThreads) {
         const int co = e / ncol, j = e - co * ncol;
-        const int cl = j / a.KK, tap = j - cl * a.KK;
-        const int ci = ch * 4 + cl;
-        if (co < a.Co && j < 4 * a.KK && ci < a.C) {
+        const int t = j >> 4, l16 = j & 15;
+        const int tap = a.gtap[t][l16 & 3];
+        const int ci = ch * 4 + (l16 >> 2);
+        if (co < a.Co && tap >= 0 && ci < a.C) {
             const float s = ((red[e] + red[16 * ncol + e]) + red[32 * ncol + e]) + red[48 * ncol + e];
             atomicAdd(&dwr[((int64_t)co * a.C + ci) * a.KK + tap], s);
         }
@@ -266,6 +269,90 @@ int32_t tw_launch_v(const TwArgs& a, int nchunk, size_t lds, bool yb, bool pair,
     return yb ? tw_launch<NT, true, false>(a, nchunk, lds, st) : tw_launch<NT, false, false>(a, nchunk, lds, st);
 }
 
+// Worst bank multiplicity of one column tile's B reads: lanes pl (16 columns) x kq; the
+// ds_read_b32 groups are lanes 0-31 (kq 0,1) and 32-63 (kq 2,3), bank = dword % 32.
+int tw_tile_conflicts(const int* off16) {
+    int worst = 1;
+    for (int base = 0; base < 4; base += 2) {
+        int cnt[32] = {0};
+        int addr[32][32];
+        for (int kq = base; kq < base + 2; ++kq)
+            for (int l = 0; l < 16; ++l) {
+                const int ad = off16[l] + kq, b = ad % 32;
+                bool dup = false;
+                for (int i = 0; i < cnt[b]; ++i) dup |= addr[b][i] == ad;
+                if (!dup) addr[b][cnt[b]++] = ad;
+                worst = std::max(worst, cnt[b]);
+            }
+    }
+    return worst;
+}
+
+// Choose PS / RS / CHS paddings and group the KK taps into column tiles of 4 channels x 4
+// taps such that every tile's reads are bank-conflict-free (4 channels at CHS = 8 mod 32
+// apart, 4 taps of one parity with distinct offsets mod 8). Falls back to the layout
+// with the smallest worst case. Returns false if more than 8 tiles would be needed.
+bool tw_layout(TwArgs& a, int mx, int& NT) {
+    int best = 1 << 30;
+    TwArgs b = a;
+    for (int ps = a.HCu; ps < a.HCu + 8; ++ps) {
+        for (int rs = mx * ps; rs < mx * ps + 8; ++rs) {
+            int chs = a.HR * rs;
+            chs += ((8 - chs % 32) + 32) % 32;
+            auto toff = [&](int tap) {
+                const int kh = tap / a.KW, kw = tap - kh * a.KW, cx = kw * a.DW;
+                return kh * a.DH * rs + (cx % mx) * ps + cx / mx;
+            };
+            // greedy: per parity class, repeatedly take one tap from each residue mod 8
+            int8_t grp[8][4];
+            int ng = 0;
+            bool used[32] = {false};
+            bool ok = true;
+            for (int par = 0; par < 2 && ok; ++par) {
+                for (;;) {
+                    int g[4], n = 0;
+                    bool taken[8] = {false};
+                    for (int t = 0; t < a.KK && n < 4; ++t) {
+                        const int o = toff(t);
+                        if (used[t] || (o & 1) != par || taken[o % 8]) continue;
+                        taken[o % 8] = true;
+                        g[n++] = t;
+                    }
+                    if (!n) break;
+                    if (ng == 8) { ok = false; break; }
+                    for (int i = 0; i < 4; ++i) grp[ng][i] = (int8_t)(i < n ? g[i] : -1);
+                    for (int i = 0; i < n; ++i) used[g[i]] = true;
+                    ++ng;
+                }
+            }
+            if (!ok || (size_t)(4 * chs) * 4 > 40 * 1024) continue;
+            int worst = 1;
+            for (int t = 0; t < ng; ++t) {
+                int off[16];
+                for (int l = 0; l < 16; ++l) {
+                    const int tap = grp[t][l & 3] >= 0 ? grp[t][l & 3] : grp[t][0];
+                    off[l] = (l >> 2) * chs + toff(tap);
+                }
+                worst = std::max(worst, tw_tile_conflicts(off));
+            }
+            const int cost = worst * 16 + ng;
+            if (cost < best) {
+                best = cost;
+                b.PS = ps; b.RS = rs; b.CHS = chs;
+                for (int t = 0; t < 8; ++t)
+                    for (int i = 0; i < 4; ++i) b.gtap[t][i] = t < ng ? grp[t][i] : (int8_t)-1;
+                NT = ng;
+                if (worst == 1) break;
+            }
+        }
+        if (best < 32) break;  // conflict-free found
+    }
+    if (best == (1 << 30)) return false;
+    a = b;
+    NT = NT <= 4 ? NT : NT <= 6 ? 6 : 8;  // instantiated tile counts (extra tiles: padding)
+    return true;
+}
+
 }  // namespace
 
 // Returns 1 if launched, 0 if the shape is not for this kernel, <0 on error.
@@ -275,14 +362,14 @@ int32_t isg_tap_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_v
     if (off || g->groups != 1 || g->Co > 16 || g->Ci > kMaxC) return 0;
     if (g->SH != g->SW || (g->SH != 1 && g->SH != 2)) return 0;
     const int KK = g->KH * g->KW;
-    int NT = (4 * KK + 15) / 16;
-    if (NT > kMaxNT) return 0;
-    NT = NT == 5 ? 6 : NT == 7 ? 8 : NT;  // the instantiated column-tile counts
+    if (KK > 32) return 0;
     if (g->SH == 2 && (g->PW % 2 || g->W % 2)) return 0;  // column pairs start even
     for (int i = 0; i < x->nseg; ++i)
         if (x->s[i].xform == ISG_XF_BN_BWD) return 0;  // the gathered side never needs y
     if ((int64_t)g->H * g->W * 4 >= (1ll << 31) || (int64_t)g->OH * g->OW * 4 >= (1ll << 31)) return 0;
     TwArgs a{};
+    static const int dbg = getenv("ISG_TW_DBG") ? atoi(getenv("ISG_TW_DBG")) : 0;
+    a.dbg = dbg;
     a.dy = *dy; a.x = *x; a.dw = dw; a.dbias = dbias;
     a.rep_stride = nrep > 1 ? rep_stride : 0;
     a.nrep = nrep < 1 ? 1 : nrep;
@@ -299,14 +386,13 @@ int32_t isg_tap_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_v
     const int HC = mx * (a.BX - 1) + ext_x + 1;
     a.HCu = (HC + mx - 1) / mx;
     if (a.HCu > 64 || a.BX > 64) return 0;
-    a.PS = a.HCu;
-    a.RS = mx * a.PS;
     a.HR = g->SH * (kBY - 1) + ext_y + 1;
     if (a.HR > kPF) return 0;
-    a.CHS = a.HR * a.RS;
-    a.CHS += ((16 - a.CHS % 32) + 32) % 32;
+    // LDS layout + tap grouping with the fewest bank conflicts (first conflict-free one)
+    int NT = 0;
+    if (!tw_layout(a, mx, NT)) return 0;
     a.DQ = kBY * a.BX;
-    a.DQ += ((16 - a.DQ % 32) + 32) % 32;
+    a.DQ += ((2 - a.DQ % 32) + 32) % 32;  // dy rows: lane co*DQ + kq conflict-free
     a.tiles_y = (g->OH + kBY - 1) / kBY;
     const int64_t tpi = (int64_t)a.tiles_x * a.tiles_y;
     a.ntiles = (int)(g->N * tpi);
@@ -316,6 +402,7 @@ int32_t isg_tap_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_v
     a.m_tx = magic(a.tiles_x);
     const int nchunk = (g->Ci + 3) / 4;
     size_t lds = (size_t)(4 * a.CHS + 16 * a.DQ) * sizeof(float);
+    if (NT < 1) return 0;
     lds = std::max(lds, (size_t)(4 * 16 * NT * 16) * sizeof(float));  // the wave reduction
     if (lds > 64 * 1024) return 0;
     bool yb = false;

@@ -81,7 +81,7 @@ def _fill(obj, spec, base, fix):
 
 
 class Record:
-    OPF_SIDE, OPF_JOIN = 1, 2  # executor header flags (api.cpp)
+    OPF_SIDE, OPF_JOIN, OPF_FORK_NOW = 1, 2, 4  # executor header flags (api.cpp)
 
     def __init__(self, kind, cls, spec, items_cls=None, items=None, label="", flops=0, nbytes=0):
         self.kind = kind
@@ -402,6 +402,25 @@ _BN_FINAL = os.environ.get("ISG_NO_BN_FINAL", "0") != "1"  # debugging switch
 _BN_FUSE = _BN_FINAL and os.environ.get("ISG_BN_FUSE", "0") == "1"
 
 
+def _fork_pools(ol):
+    """Max-pool forwards depend only on their input and nothing writes what they read or
+    produce until their first consumer: fork each onto the executor's side stream and
+    join right before the first later op that reads any byte of its output."""
+    if os.environ.get("ISG_NO_SIDE_POOL", "0") == "1":
+        return
+    recs = ol.recs
+    for i, r in enumerate(recs):
+        if r.kind != L.OP_MAXPOOL_FWD or getattr(r, "out_range", None) is None:
+            continue
+        slot, lo, hi = r.out_range
+        for j in range(i + 1, len(recs)):
+            if any(fs == slot and lo <= off < hi for _, fs, off in recs[j].fix):
+                if j > i + 1:  # something to overlap with
+                    r.flags |= Record.OPF_SIDE | Record.OPF_FORK_NOW
+                    recs[j].flags |= Record.OPF_JOIN
+                break
+
+
 def sinks_spec(sinks):
     """isg_sinks spec from sink specs; a sink's private '_fin_ctr' (the ticket of a fused
     BN finalisation) becomes the launch's fin_counter."""
@@ -636,10 +655,15 @@ class PoolOp:
     def fwd(self, ops):
         g = self.g
         segs = [fwd_seg(v, g.train) for v in self.x.segs]
-        ops.add(Record(L.OP_MAXPOOL_FWD, L.PoolRec,
-                       {"x": vtensor(segs, g.N, self.x.H, self.x.W), "k": self.k,
-                        "out": self.out.ptr(self.c0), "out_ns": self.out.n_stride},
-                       label=self.out.name))
+        r = Record(L.OP_MAXPOOL_FWD, L.PoolRec,
+                   {"x": vtensor(segs, g.N, self.x.H, self.x.W), "k": self.k,
+                    "out": self.out.ptr(self.c0), "out_ns": self.out.n_stride},
+                   label=self.out.name)
+        # bytes this op writes (for _fork_pools): its channels of every image
+        o = self.out.ptr(self.c0)
+        hw = self.out.H * self.out.W
+        r.out_range = (o.slot, o.off, o.off + ((g.N - 1) * self.out.n_stride + self.x.C * hw) * 4)
+        ops.add(r)
 
     def bwd(self, ops, gs):
         g = self.g
@@ -753,6 +777,7 @@ class Plan:
             for i in range(0, len(items), L.LIST_CHUNK):
                 chunk = items[i:i + L.LIST_CHUNK]
                 fw.add(Record(L.OP_BN_UPDATE, L.ListRec, {"n": len(chunk)}, L.BnUpdate, chunk))
+        _fork_pools(fw)
         self.fwd = fw.compile()
         self.act_size = g.act_size
         self.stats_size = max(g.stats_size, 8)

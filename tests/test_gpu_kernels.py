@@ -66,6 +66,7 @@ DENSE = [
     (16, 36, 33, 45, 3, 1, 1, 1),
     (20, 16, 130, 100, 5, 2, 2, 1),
     (16, 4, 72, 88, 8, 4, 2, 1),
+    (4, 4, 40, 36, 3, 1, 1, 1),
 ]
 
 

@@ -7,7 +7,7 @@ OUT=$PWD/_build
 mkdir -p $OUT
 FL="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -DISG_STAMPS -Wno-unused-function"
 objs=""
-for f in conv_mfma pw_gemm tap_conv tap_wgrad halo_conv wgrad dw_convt eltwise maskops; do
+for f in conv_mfma pw_gemm tap_conv tap_wgrad thin_conv halo_conv wgrad dw_convt eltwise maskops; do
   /opt/rocm/bin/hipcc $FL -c $SRC/$f.hip -o $OUT/$f.o &
   objs="$objs $OUT/$f.o"
 done
