@@ -19,7 +19,7 @@ SINK_STORE, SINK_ACCUM, SINK_ACTBWD, SINK_NONE = 0, 1, 2, 3
 MAX_SEGS = 3
 LIST_CHUNK = 32
 STAT_REP = 16     # ISG_STAT_REP: accumulator replicas (isg.h)
-ABI_VERSION = 4
+ABI_VERSION = 5
 WREP = 16         # ISG_WREP: weight-gradient replicas (isg.h)
 
 

@@ -67,7 +67,7 @@ static int32_t check_geom(const isg_conv_geom* g) {
 extern "C" {
 
 const char* isg_last_error(void) { return g_last_error.c_str(); }
-int32_t isg_abi_version(void) { return 4; }
+int32_t isg_abi_version(void) { return 5; }
 int32_t isg_stat_replicas(void) { return ISG_STAT_REP; }
 
 int32_t isg_conv_fwd(const isg_conv_geom* g, const isg_vtensor* x, const float* w,

@@ -25,6 +25,33 @@ from .engine import (S_ACT, S_DOUT, S_GRAD, S_IN, S_OUT, S_PGRAD, S_STATS, S_TEN
                      Plan)
 
 
+class GradSync:
+    """The data-parallel exchange of one step, one process per GPU:
+    rank 0's BatchNorm running statistics are broadcast before the step (DDP
+    broadcast_buffers), and the flat gradient bucket is averaged over the ranks after
+    the backward (one collective: RCCL AVG on "nccl"; SUM then scale on gloo, which has no
+    AVG). BN batch statistics stay local to each replica, as in the reference run per
+    replica."""
+
+    def __init__(self, process_group=None):
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        self.avg = self.world > 1 and dist.get_backend(process_group) == "nccl"
+
+    def buffers(self, flatb):
+        if self.world > 1:
+            dist.broadcast(flatb, 0, group=self.pg)
+
+    def grads(self, grad_flat):
+        if self.world == 1:
+            return
+        if self.avg:
+            dist.all_reduce(grad_flat, op=dist.ReduceOp.AVG, group=self.pg)
+        else:
+            dist.all_reduce(grad_flat, op=dist.ReduceOp.SUM, group=self.pg)
+            grad_flat.div_(self.world)
+
+
 def flatten_module(model, device):
     """Re-bind every parameter and floating buffer of `model` as a view of one flat
     buffer (params) / (float buffers); returns (flat_params, flat_bufs, param_index)."""
@@ -72,7 +99,8 @@ class Trainer:
         g = self.plan.graph
         self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
         self.pg = process_group
-        self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        self.sync = GradSync(process_group)
+        self.world = self.sync.world
         dev = self.device
         self.act = torch.empty(max(self.plan.act_size, 1), dtype=torch.float32, device=dev)
         self.stats = torch.empty(self.plan.stats_size, dtype=torch.float64, device=dev)
@@ -207,7 +235,7 @@ class Trainer:
             elif callable(u):
                 u()
             elif u == "coll":
-                dist.all_reduce(self.grad_flat, op=dist.ReduceOp.AVG, group=self.pg)
+                self.sync.grads(self.grad_flat)
             elif u == "tic":
                 ev = torch.cuda.Event(enable_timing=True)
                 ev.record()
@@ -225,8 +253,7 @@ class Trainer:
         if target is not None:
             self.target.copy_(target, non_blocking=True)
         self.step_count += 1
-        if self.world > 1:  # DDP broadcast_buffers: rank 0's BN running stats
-            dist.broadcast(self.flatb, 0, group=self.pg)
+        self.sync.buffers(self.flatb)  # DDP broadcast_buffers: rank 0's BN running stats
         self._run(self.graphs if self.graphs else self._schedule(self.split))
         return self.loss_acc / self.logits.numel()
 

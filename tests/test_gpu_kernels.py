@@ -67,6 +67,14 @@ DENSE = [
     (20, 16, 130, 100, 5, 2, 2, 1),
     (16, 4, 72, 88, 8, 4, 2, 1),
     (4, 4, 40, 36, 3, 1, 1, 1),
+    # the Segment(20) 128^2 shapes (tile choices of tap_conv / tap_wgrad at network scale)
+    (16, 16, 64, 64, 5, 2, 2, 1),
+    (36, 16, 64, 64, 2, 2, 0, 1),
+    (48, 16, 32, 32, 2, 2, 0, 1),
+    (16, 16, 32, 32, 3, 1, 1, 1),
+    (20, 16, 128, 128, 5, 2, 2, 1),
+    (16, 16, 16, 16, 3, 1, 1, 1),
+    (48, 16, 16, 16, 2, 2, 0, 1),
 ]
 
 
