@@ -90,6 +90,24 @@ def roofline_of(rec, ms):
             "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": None}
 
 
+def pmc_traffic(label, args):
+    """HBM bytes per launch of the dominant op from the committed PMC pass
+    (profiles/traffic.json, written by tools/kbench/traffic.sh: 2*FETCH_SIZE + WRITE_SIZE,
+    the gfx950 correction of MI355X_MICROARCH.md), or None when no pass covers this op at
+    this configuration. PMC counters need rocprofv3 as the parent process, so they cannot
+    be read live inside this run."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "traffic.json")
+    try:
+        with open(path) as f:
+            runs = json.load(f)
+    except (OSError, ValueError):
+        return None
+    for r in runs:
+        if r.get("label") == label and r.get("config") == [args.batch, args.cin, args.size]:
+            return r.get("hbm_bytes_per_launch")
+    return None
+
+
 def cpu_baseline(args):
     """Oracle (torch eager fp32 CPU) train step on the same config: bounded sample."""
     import numpy as np
@@ -191,6 +209,7 @@ def main():
         roof = roofline_of(dom_rec, ms)
         roof["kernel"] = f"{dom[0]}:{dom_rec.label}"
         roof["avg_ms"] = round(ms, 4)
+        roof["traffic"] = pmc_traffic(dom_rec.label, args)
 
     value = world * args.batch * args.steps / elapsed
     out = {

@@ -23,6 +23,10 @@
 // B[k][j] = halo (lane: pixel = l>>4, column j = l&15), D lane: co = (l>>4)*4+r, j = l&15.
 #include "stage.h"
 
+#include <cstring>
+#include <mutex>
+#include <vector>
+
 namespace {
 
 constexpr int kThreads = 256;
@@ -353,6 +357,393 @@ bool tw_layout(TwArgs& a, int mx, int& NT) {
     return true;
 }
 
+// ---- all-channel variant for stride-2 convs (the stem, segment.py:23-26) -----------------
+// The chunked kernel above re-stages (and re-transforms) the tile's dy rows once per
+// 4-channel chunk: for the stem's 20 input channels that is 5 passes over dy and the saved
+// y, and its staging instructions, not the MFMAs, bounded it. Here one workgroup stages
+// the halo of EVERY input channel plus dy once per tile, and the 4 waves split the
+// C*KK GEMM columns (wave w owns column tiles [w*NTW, (w+1)*NTW)); each wave walks all 4
+// tile rows. Waves own disjoint columns, so the epilogue needs no cross-wave reduction.
+//
+// Staging: a "pair item" is two consecutive halo rows of one channel (lanes 0-31 the
+// first, 32-63 the second, one column pair per lane), so the channel — its pointer,
+// transform and coefficients — stays wave-uniform. Items are prefetched into registers
+// for the next tile while this tile's MFMAs run.
+constexpr int kTwaMaxPW = 30;  // pair items per wave (C * ceil(HR/2) <= 120)
+constexpr int kTwaTiles = 32;  // column tiles (C*KK <= 512)
+constexpr int kDyPT = 7;       // dy tile elements per thread (16 x 4 x BX, BX <= 28)
+
+
+struct TwaArgs {
+    isg_vtensor dy;
+    isg_vtensor x;
+    float* dw;
+    float* dbias;
+    int64_t rep_stride;
+    int nrep;
+    int N, C, Co, H, W, OH, OW, KH, KW, PH, PW, KK;
+    int BX, tiles_x, tiles_y, ntiles;
+    int HR, HRP, HCu, PS, RS, CHS, DQ, KPW;
+    uint32_t m_tpi, m_tx, m_4bx, m_bx, m_hrp;
+    int dbg;  // ablation bits (ISG_TW_DBG): 1 no MFMA loop, 2 no global loads, 4 no LDS stores
+    // tile t, lane pl: column id ci*KK + tap, or -1 - (a column id to read) for padding
+    int16_t col[kTwaTiles][16];
+};
+
+template <int NTW, bool YB>
+__global__ __launch_bounds__(kThreads, 2) void tap_wgrad_all_kernel(TwaArgs a) {
+    extern __shared__ float lds[];
+    float* const Xs = lds;                  // [C][CHS]: rows of RS = even plane | odd plane
+    float* const Ds = lds + a.C * a.CHS;    // [16][DQ]: dy rows, 4 tile rows of BX
+    __shared__ ChT tabx[kMaxC];
+    __shared__ ChT taby[16];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
+    const int kq = lane >> 4, pl = lane & 15, half = lane >> 5, hl = lane & 31;
+    for (int c = tid; c < a.C; c += kThreads) tabx[c] = ch_table_entry(a.x, c, (int64_t)a.H * a.W);
+    for (int c = tid; c < a.Co; c += kThreads) taby[c] = ch_table_entry(a.dy, c, (int64_t)a.OH * a.OW);
+    __syncthreads();
+
+    int boff[NTW];
+    bool cval[NTW];
+#pragma unroll
+    for (int t = 0; t < NTW; ++t) {
+        int c = a.col[wave * NTW + t][pl];
+        cval[t] = c >= 0;
+        if (c < 0) c = -1 - c;
+        const int ci = c / a.KK, tap = c - ci * a.KK;
+        const int kh = tap / a.KW, kw = tap - kh * a.KW;
+        boff[t] = ci * a.CHS + kh * a.RS + (kw & 1) * a.PS + (kw >> 1) + kq;
+    }
+    const int aoff = pl * a.DQ + kq;
+
+    const int tpi = a.tiles_x * a.tiles_y;
+    auto qdiv = [](int x, uint32_t m) { return m ? (int)__umulhi((uint32_t)x, m) : x; };
+    auto tile_geo = [&](int tile, int& n, int& oy0, int& ox0) {
+        n = qdiv(tile, a.m_tpi);
+        const int tr = tile - n * tpi;
+        const int tyi = qdiv(tr, a.m_tx);
+        oy0 = tyi * kBY;
+        ox0 = (tr - tyi * a.tiles_x) * a.BX;
+    };
+    const uint32_t xplane = (uint32_t)a.H * a.W * 4u, yplane = (uint32_t)a.OH * a.OW * 4u;
+
+    typedef float v2f __attribute__((ext_vector_type(2)));
+    v2f v[kTwaMaxPW];
+    float dv[kDyPT], dyy[kDyPT];
+    uint32_t okm = 0;   // bit j: item j's row and column are inside the image
+    uint32_t dokm = 0;  // bit i: dy element i is inside the map
+    auto load_tile = [&](int tile) {
+        int n, oy0, ox0;
+        tile_geo(tile, n, oy0, ox0);
+        const int sy0 = oy0 * 2 - a.PH, ix = ox0 * 2 - a.PW + 2 * hl;
+        const bool colok = hl < a.HCu && ix >= 0 && ix < a.W;
+        okm = 0;
+        // branch-free: every item slot issues its load (items past C*HRP and halo rows
+        // past HR get an out-of-range offset, which the buffer load returns as 0)
+#pragma unroll
+        for (int j = 0; j < kTwaMaxPW; ++j) {
+            const int k = 4 * j + wave;
+            const int ch = (int)__umulhi((uint32_t)k, a.m_hrp), rp = k - ch * a.HRP;
+            const ChT t = tabx[min(ch, a.C - 1)];
+            const auto xr = __builtin_amdgcn_make_buffer_rsrc((void*)uniform_ptr(t.p + (int64_t)n * t.ns),
+                                                              (short)0, (int)xplane, 0x00020000);
+            const int r = 2 * rp + half, iy = sy0 + r;
+            const bool ok = colok && ch < a.C && r < a.HR && (unsigned)iy < (unsigned)a.H;
+            okm |= (uint32_t)ok << j;
+            const uint32_t o = ok ? ((uint32_t)iy * (uint32_t)a.W + (uint32_t)ix) * 4u : 0x80000000u;
+            v[j] = __builtin_bit_cast(v2f, __builtin_amdgcn_raw_buffer_load_b64(xr, o, 0, 0));
+        }
+        // dy: kDyPT elements per thread (co, tile row, column), per-lane addresses
+        dokm = 0;
+#pragma unroll
+        for (int i = 0; i < kDyPT; ++i) {
+            const int e = tid + kThreads * i;
+            const int co = qdiv(e, a.m_4bx), rem = e - co * 4 * a.BX;
+            const int r = qdiv(rem, a.m_bx), px = rem - r * a.BX;
+            const int oy = oy0 + r, ox = ox0 + px;
+            const bool ok = co < a.Co && oy < a.OH && ox < a.OW;
+            dokm |= (uint32_t)ok << i;
+            const ChT& ty = taby[min(co, a.Co - 1)];
+            const int64_t o = ok ? (int64_t)oy * a.OW + ox : 0;  // invalid: channel base
+            dv[i] = gld(ty.p + (int64_t)n * ty.ns, o);
+            if constexpr (YB) dyy[i] = gld(ty.y + (int64_t)n * ty.yns, o);
+        }
+    };
+    auto store_tile = [&]() {
+#pragma unroll
+        for (int j = 0; j < kTwaMaxPW; ++j) {
+            const int k = 4 * j + wave;
+            const int ch = (int)__umulhi((uint32_t)k, a.m_hrp), rp = k - ch * a.HRP;
+            const int r = 2 * rp + half;
+            if (ch < a.C && hl < a.PS && r < a.HR) {
+                const ChT t = tabx[ch];
+                float x0 = 0.f, x1 = 0.f;
+                if ((okm >> j) & 1u) {
+                    x0 = ch_xform(t.xf, t.act, t.k, v[j][0], v[j][0]);
+                    x1 = ch_xform(t.xf, t.act, t.k, v[j][1], v[j][1]);
+                }
+                float* const xs = Xs + ch * a.CHS + r * a.RS + hl;
+                xs[0] = x0;
+                xs[a.PS] = x1;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < kDyPT; ++i) {
+            const int e = tid + kThreads * i;
+            const int co = qdiv(e, a.m_4bx), rem = e - co * 4 * a.BX;
+            if (co < 16) {
+                float d = 0.f;
+                if ((dokm >> i) & 1u) {
+                    const ChT& ty = taby[co];
+                    d = ch_xform(ty.xf, ty.act, ty.k, dv[i], YB ? dyy[i] : dv[i]);
+                }
+                Ds[co * a.DQ + rem] = d;
+            }
+        }
+    };
+
+    f32x4 acc[NTW];
+#pragma unroll
+    for (int t = 0; t < NTW; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float bsum = 0.f;  // dbias partial (wave 0): sum of this lane's dy values (row co = pl)
+
+    int tile = blockIdx.x;
+    if (tile < a.ntiles && !(a.dbg & 2)) load_tile(tile);
+    const int nstep = (a.dbg & 1) ? 0 : a.BX >> 2;
+    while (tile < a.ntiles) {
+        __syncthreads();  // LDS free
+        if (!(a.dbg & 4)) store_tile();
+        __syncthreads();
+        const int ntile = tile + gridDim.x;
+        if (ntile < a.ntiles && !(a.dbg & 2)) load_tile(ntile);
+        // kBY rows x nstep pixel quads, software-pipelined: the next quad's dy and halo
+        // operands are read from LDS while this quad's MFMAs run
+        const int nq = kBY * nstep;
+        int r = 0, sq = 0;
+        if (nq) {
+        float av = Ds[aoff];
+        float bv[NTW];
+#pragma unroll
+        for (int t = 0; t < NTW; ++t) bv[t] = Xs[boff[t]];
+#pragma unroll 1
+        for (int q = 0; q < nq; ++q) {
+            if (++sq == nstep) { sq = 0; ++r; }
+            const bool more = q + 1 < nq;
+            const int xo = more ? r * 2 * a.RS + 4 * sq : 0;
+            const int dq = more ? r * a.BX + 4 * sq : 0;
+            const float avn = Ds[aoff + dq];
+            float bn[NTW];
+#pragma unroll
+            for (int t = 0; t < NTW; ++t) bn[t] = Xs[boff[t] + xo];
+            if (wave == 0) bsum += av;
+#pragma unroll
+            for (int t = 0; t < NTW; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[t], acc[t], 0, 0, 0);
+            av = avn;
+#pragma unroll
+            for (int t = 0; t < NTW; ++t) bv[t] = bn[t];
+        }
+        }
+        tile = ntile;
+    }
+
+    // ---- epilogue: waves own disjoint columns; one atomic per dW element per workgroup
+    float* const dwr = a.dw + (int64_t)(blockIdx.x % a.nrep) * a.rep_stride;
+#pragma unroll
+    for (int t = 0; t < NTW; ++t) {
+        if (!cval[t]) continue;
+        const int c = a.col[wave * NTW + t][pl];
+        const int ci = c / a.KK, tap = c - ci * a.KK;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int co = kq * 4 + i;
+            if (co < a.Co) atomicAdd(&dwr[((int64_t)co * a.C + ci) * a.KK + tap], acc[t][i]);
+        }
+    }
+    if (a.dbias) {
+        __syncthreads();
+        float* const rb = lds;
+        if (wave == 0) rb[lane] = bsum;
+        __syncthreads();
+        if (tid < 16 && tid < a.Co) {
+            const float s = ((rb[tid] + rb[16 + tid]) + rb[32 + tid]) + rb[48 + tid];
+            atomicAdd(&(a.dbias + (int64_t)(blockIdx.x % a.nrep) * a.rep_stride)[tid], s);
+        }
+    }
+}
+
+template <int NTW>
+int32_t twa_launch(const TwaArgs& a, size_t lds, bool yb, hipStream_t st) {
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+            cus = 256;
+    }
+    auto k = yb ? tap_wgrad_all_kernel<NTW, true> : tap_wgrad_all_kernel<NTW, false>;
+    if (lds > 48 * 1024 &&
+        hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+        return isg_check_launch("tap_wgrad_all_kernel: dynamic LDS");
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, kThreads, lds) != hipSuccess || occ < 1) occ = 1;
+    const int per = std::max(1, std::min(a.ntiles, occ * cus));
+    hipLaunchKernelGGL(k, dim3((unsigned)per), dim3(kThreads), lds, st, a);
+    return isg_check_launch("tap_wgrad_all_kernel");
+}
+
+// Bank multiplicity of one column tile's B reads (lanes 0-31: kq 0/1 x 16 columns).
+int twa_conflicts(const int* off, int n) {
+    int cnt[32] = {0};
+    int addr[32][32];
+    int worst = 1;
+    for (int kq = 0; kq < 2; ++kq)
+        for (int l = 0; l < n; ++l) {
+            const int ad = off[l] + kq, b = ad % 32;
+            bool dup = false;
+            for (int i = 0; i < cnt[b]; ++i) dup |= addr[b][i] == ad;
+            if (!dup) addr[b][cnt[b]++] = ad;
+            worst = std::max(worst, cnt[b]);
+        }
+    return worst;
+}
+
+// Pads (PS, RS, CHS) and groups the C*KK columns into tiles of 16 with at most `lim`-way
+// bank conflicts (2-way costs 4 LDS cycles against a 32-cycle MFMA), fewest tiles first.
+bool twa_layout(TwaArgs& a, int& ntiles) {
+    const int ncol = a.C * a.KK;
+    int best = 1 << 30;
+    TwaArgs b = a;
+    const int minimal = (ncol + 15) / 16;
+    for (int lim = 1; lim <= 2 && best > minimal; ++lim) {
+        for (int ps = a.HCu; ps < a.HCu + 4; ++ps) {
+            for (int rs = 2 * ps; rs < 2 * ps + 4; ++rs) {
+                for (int pad = 0; pad < 32; pad += 4) {
+                    const int chs = a.HR * rs + pad;
+                    if ((size_t)(a.C * chs + 16 * a.DQ) * 4 > 64 * 1024) continue;
+                    auto off = [&](int c) {
+                        const int ci = c / a.KK, tap = c - ci * a.KK, kh = tap / a.KW, kw = tap - kh * a.KW;
+                        return ci * chs + kh * rs + (kw & 1) * ps + (kw >> 1);
+                    };
+                    std::vector<char> used(ncol, 0);
+                    int16_t col[kTwaTiles][16];
+                    int nt = 0, left = ncol;
+                    bool ok = true;
+                    while (left > 0) {
+                        if (nt == kTwaTiles) { ok = false; break; }
+                        int o[16], ids[16], n = 0;
+                        for (int c = 0; c < ncol && n < 16; ++c) {
+                            if (used[c]) continue;
+                            o[n] = off(c);
+                            if (twa_conflicts(o, n + 1) > lim) continue;
+                            ids[n++] = c;
+                            used[c] = 1;
+                            --left;
+                        }
+                        for (int l = 0; l < 16; ++l) col[nt][l] = (int16_t)(l < n ? ids[l] : -1 - ids[0]);
+                        ++nt;
+                    }
+                    if (!ok) continue;
+                    if (nt < best) {
+                        best = nt;
+                        b.PS = ps; b.RS = rs; b.CHS = chs;
+                        for (int t = 0; t < kTwaTiles; ++t)
+                            for (int l = 0; l < 16; ++l) b.col[t][l] = t < nt ? col[t][l] : (int16_t)-1;
+                    }
+                    if (best == minimal) break;
+                }
+                if (best == minimal) break;
+            }
+            if (best == minimal) break;
+        }
+    }
+    if (best == (1 << 30)) return false;
+    a = b;
+    ntiles = best;
+    return true;
+}
+
+// Returns 1 if launched, 0 if the shape is not for this kernel, <0 on error.
+int32_t twa_try(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, float* dw,
+                float* dbias, int64_t rep_stride, int32_t nrep, hipStream_t st) {
+    static const bool off = getenv("ISG_NO_TWA") != nullptr;
+    if (off || g->SH != 2 || g->SW != 2 || g->DH != 1 || g->DW != 1) return 0;
+    if (g->PW % 2 || g->W % 2) return 0;
+    const int KK = g->KH * g->KW;
+    // measured (kbench): the stem layer1 (20 x 25 columns) 433 -> 308 us; the 16-channel
+    // layer2 (400 columns, a 4x smaller map) is faster on the chunked kernel (71 vs ~100 us)
+    if (g->Ci * KK > 16 * kTwaTiles || g->Ci * KK < 448) return 0;
+    TwaArgs a{};
+    a.N = g->N; a.C = g->Ci; a.Co = g->Co; a.H = g->H; a.W = g->W; a.OH = g->OH; a.OW = g->OW;
+    a.KH = g->KH; a.KW = g->KW; a.PH = g->PH; a.PW = g->PW; a.KK = KK;
+    // tile width: a multiple of 4 whose halo (column pairs) fits one 32-lane half-wave
+    const int bxmax = (32 * 2 - (g->KW - 1) - 1) / 2 + 1;
+    const int bxm = std::min(bxmax, 64) & ~3;
+    if (bxm < 4) return 0;
+    a.tiles_x = (g->OW + bxm - 1) / bxm;
+    a.BX = ((g->OW + a.tiles_x - 1) / a.tiles_x + 3) & ~3;
+    if (a.BX > bxm) a.BX = bxm;
+    a.tiles_x = (g->OW + a.BX - 1) / a.BX;
+    a.HCu = (2 * (a.BX - 1) + g->KW + 1) / 2;
+    if (a.HCu > 32 || 16 * kBY * a.BX > kThreads * kDyPT) return 0;
+    a.HR = 2 * (kBY - 1) + g->KH;
+    a.HRP = (a.HR + 1) / 2;
+    if (a.HRP < 4) return 0;  // the item walk wraps at most once per step of 4
+    a.KPW = (a.C * a.HRP + 3) / 4;
+    if (a.KPW > kTwaMaxPW) return 0;
+    a.DQ = kBY * a.BX;
+    a.DQ += ((2 - a.DQ % 32) + 32) % 32;  // av reads (co*DQ + kq) conflict-free
+    // the layout search is host work of a few ms: cache it per geometry
+    struct Cached { int key[7]; int ntiles; int PS, RS, CHS; int16_t col[kTwaTiles][16]; };
+    static std::mutex mu;
+    static std::vector<Cached> cache;
+    const int key[7] = {a.C, a.KK, a.KW, a.HR, a.HCu, a.DQ, 0};
+    int ntiles = 0;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        const Cached* hit = nullptr;
+        for (const auto& c : cache)
+            if (!memcmp(c.key, key, sizeof key)) hit = &c;
+        if (hit) {
+            ntiles = hit->ntiles; a.PS = hit->PS; a.RS = hit->RS; a.CHS = hit->CHS;
+            memcpy(a.col, hit->col, sizeof a.col);
+        } else {
+            if (!twa_layout(a, ntiles)) ntiles = 0;
+            Cached c;
+            memcpy(c.key, key, sizeof key);
+            c.ntiles = ntiles; c.PS = a.PS; c.RS = a.RS; c.CHS = a.CHS;
+            memcpy(c.col, a.col, sizeof a.col);
+            cache.push_back(c);
+        }
+    }
+    if (ntiles < 1) return 0;
+    const int NTW = (ntiles + 3) / 4;
+    a.tiles_y = (g->OH + kBY - 1) / kBY;
+    const int64_t tpi = (int64_t)a.tiles_x * a.tiles_y;
+    a.ntiles = (int)(g->N * tpi);
+    if ((int64_t)a.ntiles * tpi >= (1ll << 32)) return 0;
+    auto magic = [](int64_t d) { return d == 1 ? 0u : (uint32_t)(((1ull << 32) + d - 1) / d); };
+    a.m_tpi = magic(tpi);
+    a.m_tx = magic(a.tiles_x);
+    a.m_4bx = magic(4 * a.BX);
+    a.m_bx = magic(a.BX);
+    a.m_hrp = (uint32_t)(((1ull << 32) + a.HRP - 1) / a.HRP);  // k < 4*kTwaMaxPW: exact
+    static const int dbg = getenv("ISG_TW_DBG") ? atoi(getenv("ISG_TW_DBG")) : 0;
+    a.dbg = dbg;
+    a.dy = *dy; a.x = *x; a.dw = dw; a.dbias = dbias;
+    a.rep_stride = nrep > 1 ? rep_stride : 0;
+    a.nrep = nrep < 1 ? 1 : nrep;
+    const size_t lds = (size_t)(a.C * a.CHS + 16 * a.DQ) * sizeof(float);
+    bool yb = false;
+    for (int i = 0; i < dy->nseg; ++i) yb |= dy->s[i].xform == ISG_XF_BN_BWD;
+    int32_t e;
+    if (NTW <= 4) e = twa_launch<4>(a, lds, yb, st);
+    else if (NTW <= 6) e = twa_launch<6>(a, lds, yb, st);
+    else if (NTW <= 7) e = twa_launch<7>(a, lds, yb, st);
+    else e = twa_launch<8>(a, lds, yb, st);
+    return e ? e : 1;
+}
+
 }  // namespace
 
 // Returns 1 if launched, 0 if the shape is not for this kernel, <0 on error.
@@ -360,6 +751,12 @@ int32_t isg_tap_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_v
                       float* dbias, int64_t rep_stride, int32_t nrep, hipStream_t st) {
     static const bool off = getenv("ISG_NO_TAP_WGRAD") != nullptr;
     if (off || g->groups != 1 || g->Co > 16 || g->Ci > kMaxC) return 0;
+    for (int i = 0; i < x->nseg; ++i)
+        if (x->s[i].xform == ISG_XF_BN_BWD) return 0;
+    if ((int64_t)g->H * g->W * 4 < (1ll << 31) && (int64_t)g->OH * g->OW * 4 < (1ll << 31)) {
+        const int32_t t = twa_try(g, dy, x, dw, dbias, rep_stride, nrep, st);
+        if (t != 0) return t;
+    }
     if (g->SH != g->SW || (g->SH != 1 && g->SH != 2)) return 0;
     const int KK = g->KH * g->KW;
     if (KK > 32) return 0;
