@@ -385,7 +385,7 @@ struct TwaArgs {
     int BX, tiles_x, tiles_y, ntiles;
     int HR, HRP, HCu, PS, RS, CHS, DQ, KPW;
     uint32_t m_tpi, m_tx, m_4bx, m_bx, m_hrp;
-    int dbg;  // ablation bits (ISG_TW_DBG): 1 no MFMA loop, 2 no global loads, 4 no LDS stores
+    int dbg;  // ablation bits (ISG_TW_DBG): 1 no MFMA loop, 2 no global loads, 4 no LDS stores, 8 no dW atomics
     // tile t, lane pl: column id ci*KK + tap, or -1 - (a column id to read) for padding
     int16_t col[kTwaTiles][16];
 };
@@ -551,7 +551,7 @@ __global__ __launch_bounds__(kThreads, 2) void tap_wgrad_all_kernel(TwaArgs a) {
     float* const dwr = a.dw + (int64_t)(blockIdx.x % a.nrep) * a.rep_stride;
 #pragma unroll
     for (int t = 0; t < NTW; ++t) {
-        if (!cval[t]) continue;
+        if (!cval[t] || (a.dbg & 8)) continue;
         const int c = a.col[wave * NTW + t][pl];
         const int ci = c / a.KK, tap = c - ci * a.KK;
 #pragma unroll
