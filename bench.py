@@ -37,6 +37,7 @@ def parse():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--profile-ops", default="", help="write per-op timing table to this path")
     ap.add_argument("--eager", action="store_true", help="no HIP graph capture")
+    ap.add_argument("--no-infer", action="store_true", help="skip the inference leg")
     return ap.parse_args()
 
 
@@ -106,6 +107,69 @@ def pmc_traffic(label, args):
         if r.get("label") == label and r.get("config") == [args.batch, args.cin, args.size]:
             return r.get("hbm_bytes_per_launch")
     return None
+
+
+def infer_bench(dev, reps=20):
+    """BASELINE.json's inference half ("infer masks/sec + NMS p50") on config 4
+    (OCHuman-style crowded scene): K=16 person crops of 480x480 (RGB + 17 keypoint heatmaps,
+    the train_instance.py:139-196 test-path crop size) through Segment(20) in eval mode,
+    sigmoid, bilinear paste-back into a 1024x1024 canvas (isg_mask_paste) and greedy
+    mask-NMS at IoU 0.5 (isg_mask_nms). Boxes are drawn so most pairs overlap heavily.
+    Times the whole pipeline per image (masks/s = K / time) and the NMS alone (p50)."""
+    import numpy as np
+    from instancesegmentation_amd import _lib as L
+    from instancesegmentation_amd.model.segment import Segment
+    from instancesegmentation_amd.runtime import sigmoid
+    K, S, H, W = 16, 480, 1024, 1024
+    torch.manual_seed(99)
+    m = Segment(20).to(dev).eval()
+    rng = np.random.Generator(np.random.PCG64(11))
+    x = torch.from_numpy(rng.standard_normal((K, 20, S, S), dtype=np.float32)).to(dev)
+    cx, cy = rng.integers(420, 600, K), rng.integers(420, 600, K)
+    hw, hh = rng.integers(150, 260, K), rng.integers(200, 320, K)
+    boxes = torch.from_numpy(np.stack([cx - hw, cy - hh, cx + hw, cy + hh], 1).astype(np.int32)).to(dev)
+    out = torch.empty((K, H, W), dtype=torch.uint8, device=dev)
+    ws = L.lib().isg_mask_nms_workspace(K, H, W)
+    work = torch.empty(ws, dtype=torch.uint8, device=dev)
+    sc = torch.empty(K, dtype=torch.float32, device=dev)
+    keep = torch.empty(K, dtype=torch.int32, device=dev)
+    nk = torch.zeros(1, dtype=torch.int32, device=dev)
+    st = L.stream_ptr(dev)
+
+    def nms():
+        L.check(L.lib().isg_mask_nms(out.data_ptr(), K, H, W, 0.5, work.data_ptr(), sc.data_ptr(),
+                                     keep.data_ptr(), nk.data_ptr(), st), "mask_nms")
+
+    def pipeline():
+        with torch.no_grad():
+            prob = sigmoid(m(x))
+        L.check(L.lib().isg_mask_paste(prob.data_ptr(), K, S, boxes.data_ptr(), H, W,
+                                       out.data_ptr(), st), "mask_paste")
+        nms()
+
+    for _ in range(3):
+        pipeline()
+    torch.cuda.synchronize(dev)
+    t_pipe, t_nms = [], []
+    for _ in range(reps):
+        e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+        e0.record()
+        with torch.no_grad():
+            prob = sigmoid(m(x))
+        L.check(L.lib().isg_mask_paste(prob.data_ptr(), K, S, boxes.data_ptr(), H, W,
+                                       out.data_ptr(), st), "mask_paste")
+        e1.record()
+        nms()
+        e2.record()
+        e2.synchronize()
+        t_pipe.append(e0.elapsed_time(e2))
+        t_nms.append(e1.elapsed_time(e2))
+    ms = float(np.median(t_pipe))
+    return {"metric": "infer masks/sec (Segment(20) eval 480x480 crops + paste 1024x1024 + "
+                      "mask-NMS IoU 0.5)", "masks_per_s": round(K / (ms * 1e-3), 1),
+            "ms_per_image": round(ms, 3), "nms_p50_ms": round(float(np.median(t_nms)), 4),
+            "instances": K, "kept": int(nk.item()), "config": "OCHuman-crowded synthetic, K=16",
+            "dtype": "f32", "data": "synthetic"}
 
 
 def cpu_baseline(args):
@@ -225,6 +289,8 @@ def main():
                    "execution": "eager" if args.eager else "hip-graph"},
         "roofline": roof, "loss": round(loss, 6),
     }
+    if rank == 0 and world == 1 and not args.no_infer:
+        out["infer"] = infer_bench(dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:
