@@ -246,11 +246,16 @@ struct CtArgs {
     isg_sink out;    // [N][Co][H*S][W*S]
     const float* w;  // [Ci][Co][2S][2S]
     int N, Ci, H, W;
+    int Co;          // all output channels; blockIdx.y selects CO of them
 };
 
+// CO output channels per thread, channel group blockIdx.y: the small up-sampling convs
+// (bottle4_1up / bottle5_1up, 64^2 and 128^2 inputs) have only 32-128 blocks of input
+// cells, so the output channels are spread over the grid's y dimension instead.
 template <int S, int CO>
 __global__ __launch_bounds__(kThreads) void convT_kernel(CtArgs a) {
     constexpr int K = 2 * S, P = S / 2;
+    const int co0 = blockIdx.y * CO;
     __shared__ float sh[CO][2][4];
     const int64_t hw = (int64_t)a.H * a.W;
     const int64_t cell = (int64_t)blockIdx.x * kThreads + threadIdx.x;
@@ -283,7 +288,7 @@ __global__ __launch_bounds__(kThreads) void convT_kernel(CtArgs a) {
                                  ? seg_load(a.x, kc, n, ci, hw, (int64_t)yy * a.W + xx)
                                  : 0.f;
             }
-        const float* wci = a.w + (int64_t)ci * CO * K * K;
+        const float* wci = a.w + ((int64_t)ci * a.Co + co0) * K * K;
 #pragma unroll
         for (int u = 0; u < S; ++u)
 #pragma unroll
@@ -312,9 +317,9 @@ __global__ __launch_bounds__(kThreads) void convT_kernel(CtArgs a) {
     for (int co = 0; co < CO; ++co) {
         s0[co] = 0.f;
         s1[co] = 0.f;
-        const float b = o.bias ? o.bias[co] : 0.f;
+        const float b = o.bias ? o.bias[co0 + co] : 0.f;
         if (valid) {
-            float* dst = o.p + (int64_t)n * o.n_stride + (int64_t)co * ohw;
+            float* dst = o.p + (int64_t)n * o.n_stride + (int64_t)(co0 + co) * ohw;
 #pragma unroll
             for (int u = 0; u < S; ++u) {
                 float vals[S];
@@ -350,8 +355,8 @@ __global__ __launch_bounds__(kThreads) void convT_kernel(CtArgs a) {
             const float t0 = sh[co][0][0] + sh[co][0][1] + sh[co][0][2] + sh[co][0][3];
             const float t1 = sh[co][1][0] + sh[co][1][1] + sh[co][1][2] + sh[co][1][3];
             double* sp = rep_ptr(o.stats, 4 * o.C);
-            atomicAdd(&sp[co], (double)t0);
-            atomicAdd(&sp[o.C + co], (double)t1);
+            atomicAdd(&sp[co0 + co], (double)t0);
+            atomicAdd(&sp[o.C + co0 + co], (double)t1);
         }
     }
 }
@@ -411,13 +416,21 @@ int32_t isg_convT_fwd(const isg_conv_geom* g, const isg_vtensor* x, const float*
     if (g->SW != S || g->KH != 2 * S || g->KW != 2 * S || g->PH != S / 2 || g->PW != S / 2 ||
         g->OH != g->H * S || g->OW != g->W * S)
         return isg_set_error(ISG_ERR_UNSUPPORTED, "convT fwd: need k=2s, p=s/2");
-    CtArgs a{x->s[0], out->s[0], w, g->N, g->Ci, g->H, g->W};
-    dim3 grid((unsigned)(((int64_t)g->N * g->H * g->W + kThreads - 1) / kThreads));
-    if (S == 2 && g->Co == 16) hipLaunchKernelGGL((convT_kernel<2, 16>), grid, dim3(kThreads), 0, st, a);
-    else if (S == 2 && g->Co == 4) hipLaunchKernelGGL((convT_kernel<2, 4>), grid, dim3(kThreads), 0, st, a);
-    else if (S == 4 && g->Co == 4) hipLaunchKernelGGL((convT_kernel<4, 4>), grid, dim3(kThreads), 0, st, a);
-    else if (S == 4 && g->Co == 1) hipLaunchKernelGGL((convT_kernel<4, 1>), grid, dim3(kThreads), 0, st, a);
-    else if (S == 2 && g->Co == 1) hipLaunchKernelGGL((convT_kernel<2, 1>), grid, dim3(kThreads), 0, st, a);
-    else return isg_set_error(ISG_ERR_UNSUPPORTED, "convT fwd: s=%d Co=%d", S, g->Co);
+    CtArgs a{x->s[0], out->s[0], w, g->N, g->Ci, g->H, g->W, g->Co};
+    const unsigned gx = (unsigned)(((int64_t)g->N * g->H * g->W + kThreads - 1) / kThreads);
+    if (S != 2 && S != 4) return isg_set_error(ISG_ERR_UNSUPPORTED, "convT fwd: s=%d", S);
+    // channels per thread: split the output channels until the grid has ~1024 blocks
+    static const int cob_env = getenv("ISG_CONVT_COB") ? atoi(getenv("ISG_CONVT_COB")) : 0;
+    int cob = g->Co;
+    while (cob > 1 && (int64_t)gx * (g->Co / cob) < 1024 && cob % 2 == 0) cob /= 2;
+    if (cob_env > 0 && g->Co % cob_env == 0) cob = cob_env;
+    if (cob > 4 || g->Co % cob) cob = g->Co % 4 == 0 ? 4 : (g->Co % 2 == 0 ? 2 : 1);
+    const dim3 grid(gx, (unsigned)(g->Co / cob));
+    if (S == 2 && cob == 4) hipLaunchKernelGGL((convT_kernel<2, 4>), grid, dim3(kThreads), 0, st, a);
+    else if (S == 2 && cob == 2) hipLaunchKernelGGL((convT_kernel<2, 2>), grid, dim3(kThreads), 0, st, a);
+    else if (S == 2) hipLaunchKernelGGL((convT_kernel<2, 1>), grid, dim3(kThreads), 0, st, a);
+    else if (cob == 4) hipLaunchKernelGGL((convT_kernel<4, 4>), grid, dim3(kThreads), 0, st, a);
+    else if (cob == 2) hipLaunchKernelGGL((convT_kernel<4, 2>), grid, dim3(kThreads), 0, st, a);
+    else hipLaunchKernelGGL((convT_kernel<4, 1>), grid, dim3(kThreads), 0, st, a);
     return isg_check_launch("convT_kernel");
 }
