@@ -457,3 +457,70 @@ def test_paste_and_nms_bit_exact():
     _, _, sref = MO.mask_stats(ref)
     assert np.array_equal(sc.cpu().numpy(), sref)
     assert np.array_equal(keep.cpu().numpy()[:nk.item()], keep_ref)
+
+
+def _paste_nms_gpu(prob, boxes, H, W, thr):
+    K, S = prob.shape[0], prob.shape[1]
+    P = torch.from_numpy(prob).to(DEV)
+    B = torch.from_numpy(boxes).to(DEV)
+    O = torch.empty((K, H, W), dtype=torch.uint8, device=DEV)
+    call("isg_mask_paste", ptr(P), K, S, ptr(B), H, W, ptr(O), stream())
+    ws = L.lib().isg_mask_nms_workspace(K, H, W)
+    work = torch.empty(max(ws, 1), dtype=torch.uint8, device=DEV)
+    sc = torch.empty(K, dtype=torch.float32, device=DEV)
+    keep = torch.full((K,), -1, dtype=torch.int32, device=DEV)
+    nk = torch.zeros(1, dtype=torch.int32, device=DEV)
+    call("isg_mask_nms", ptr(O), K, H, W, thr, ptr(work), ptr(sc), ptr(keep), ptr(nk), stream())
+    return O.cpu().numpy(), sc.cpu().numpy(), keep.cpu().numpy()[:nk.item()]
+
+
+def _person_probs(rng, K, S):
+    """Ellipse-shaped high-probability blobs with noise (a crowded-scene stand-in)."""
+    yy, xx = np.mgrid[0:S, 0:S].astype(np.float32) / S
+    prob = np.empty((K, S, S), np.float32)
+    for k in range(K):
+        cy, cx = rng.uniform(0.35, 0.65, 2)
+        ry, rx = rng.uniform(0.2, 0.45, 2)
+        inside = ((yy - cy) / ry) ** 2 + ((xx - cx) / rx) ** 2 <= 1.0
+        noise = rng.uniform(0, 0.3, (S, S)).astype(np.float32)
+        prob[k] = np.where(inside, 0.7 + noise, noise)
+    return np.clip(prob, 0, 1).astype(np.float32)
+
+
+@pytest.mark.parametrize("case", ["crowded16_480_to_1024", "max64", "single", "all_empty"])
+def test_paste_and_nms_cases(case):
+    """Config 4 (OCHuman-style crowded scene) at full size plus the edge cases: K at the
+    kernel's maximum (64), one instance, and masks with no pixel above threshold. Paste
+    and keep indices bit-exact to the build-defined oracle (parity with the reference
+    unpinned: it has no NMS)."""
+    from oracle import maskops_oracle as MO
+    rng = np.random.Generator(np.random.PCG64(21))
+    if case == "crowded16_480_to_1024":
+        K, S, H, W, thr = 16, 480, 1024, 1024, 0.5
+        prob = _person_probs(rng, K, S)
+        cx, cy = rng.integers(420, 600, K), rng.integers(420, 600, K)
+        hw, hh = rng.integers(150, 260, K), rng.integers(200, 320, K)
+        boxes = np.stack([cx - hw, cy - hh, cx + hw, cy + hh], 1).astype(np.int32)
+    elif case == "max64":
+        K, S, H, W, thr = 64, 32, 96, 128, 0.3
+        prob = _person_probs(rng, K, S)
+        x0, y0 = rng.integers(-10, W - 20, K), rng.integers(-10, H - 20, K)
+        boxes = np.stack([x0, y0, x0 + rng.integers(10, 60, K), y0 + rng.integers(10, 60, K)],
+                         1).astype(np.int32)
+    elif case == "single":
+        K, S, H, W, thr = 1, 64, 80, 72, 0.5
+        prob = _person_probs(rng, K, S)
+        boxes = np.asarray([[5, 3, 60, 70]], np.int32)
+    else:
+        K, S, H, W, thr = 6, 40, 64, 64, 0.5
+        prob = rng.uniform(0, 0.45, (K, S, S)).astype(np.float32)
+        boxes = np.asarray([[0, 0, 40, 40]] * K, np.int32)
+    ref = MO.paste_masks(prob, boxes, H, W)
+    out, sc, keep = _paste_nms_gpu(prob, boxes, H, W, thr)
+    assert np.array_equal(out, ref)
+    _, _, sref = MO.mask_stats(ref)
+    assert np.array_equal(sc, sref)
+    keep_ref = MO.mask_nms(ref, thr)
+    assert np.array_equal(keep, keep_ref), (keep, keep_ref)
+    if case == "crowded16_480_to_1024":
+        assert len(keep_ref) < K  # the overlap actually suppresses something
