@@ -125,6 +125,7 @@ __global__ __launch_bounds__(kThreads) void tap_conv_kernel(TapArgs a) {
                 miny = min(miny, by);
                 minx = min(minx, bx);
             });
+            if (MX == 2) minx &= ~1;  // column pairs start even (an odd first tap: +1 column)
             for_each_tap(a.q, ph, pw, [&](int i, int by, int bx, int wofs) {
                 const int cy = by - miny, cx = bx - minx;
                 toff[beg + i] = cy * a.RS + (cx % MX) * a.PS + cx / MX;
@@ -459,7 +460,6 @@ int32_t isg_tap_conv(const isg_conv_geom* g, const isg_vtensor* src, const float
     if ((int64_t)a.SrcH * a.SrcW * 4 >= (1ll << 31)) return 0;  // 32-bit buffer offsets
     // tap extents over all phases (the LDS layout serves the widest)
     int ext_y = 0, ext_x = 0;
-    bool even_minx = true;
     for (int p = 0; p < a.nph; ++p) {
         int y0 = 1 << 20, y1 = -(1 << 20), x0 = 1 << 20, x1 = -(1 << 20);
         const int nt = for_each_tap(a.q, p / g->SW, p % g->SW, [&](int, int by, int bx, int) {
@@ -468,11 +468,11 @@ int32_t isg_tap_conv(const isg_conv_geom* g, const isg_vtensor* src, const float
         });
         if (!nt) continue;
         ext_y = std::max(ext_y, y1 - y0);
-        ext_x = std::max(ext_x, x1 - x0);
-        even_minx &= (x0 % 2 == 0);
+        // a stride-2 source is staged in column pairs from an even origin: an odd first
+        // tap column (the k4 s2 p1 ConvTranspose input gradients) widens the halo by one
+        ext_x = std::max(ext_x, x1 - (mx == 2 ? (x0 & ~1) : x0));
     }
-    // a stride-2 source is staged in column pairs: needs even pair origins and widths
-    if (mx == 2 && (!even_minx || a.SrcW % 2)) return 0;
+    if (mx == 2 && a.SrcW % 2) return 0;
     const int THm = dgrad ? (g->H + g->SH - 1) / g->SH : g->OH;
     const int TWm = dgrad ? (g->W + g->SW - 1) / g->SW : g->OW;
     const int mt = (a.M + 15) / 16;
