@@ -128,3 +128,28 @@ def test_nms_ties_break_by_index():
     m = np.zeros((3, 10, 10), np.uint8)
     m[:, 0:5, 0:5] = 200
     assert list(MO.mask_nms(m, 0.5)) == [0]
+
+
+def test_bench_traffic_record_matches_dominant_op():
+    """bench.py reports roofline.traffic from the committed PMC pass (profiles/traffic.json,
+    tools/kbench/traffic.sh): the record must carry the op label bench.py keys on, the bench
+    configuration and the gfx950-corrected byte count (2*FETCH_SIZE + WRITE_SIZE)."""
+    import json
+    import os
+    import types
+
+    import bench
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    runs = json.load(open(os.path.join(root, "profiles", "traffic.json")))
+    by_label = {r["label"]: r for r in runs}
+    assert "dw_init_conv.layer1" in by_label
+    for r in runs:
+        kern = [v for k, v in r["kernels"].items() if not k.startswith("__amd_rocclr")]
+        expect = sum(2.0 * v["FETCH_SIZE_kb_per_dispatch"] + v["WRITE_SIZE_kb_per_dispatch"]
+                     for v in kern) * 1024.0
+        assert abs(r["hbm_bytes_per_launch"] - expect) <= 1e-6 * expect
+    args = types.SimpleNamespace(batch=2, cin=20, size=1024)
+    got = bench.pmc_traffic("dw_init_conv.layer1", args)
+    assert got == by_label["dw_init_conv.layer1"]["hbm_bytes_per_launch"]
+    # another configuration is not covered by the committed pass
+    assert bench.pmc_traffic("dw_init_conv.layer1", types.SimpleNamespace(batch=1, cin=20, size=1024)) is None
