@@ -248,6 +248,42 @@ __global__ __launch_bounds__(kThreads) void maxpool_kernel(PoolArgs a) {
     // (val > maxval) || isnan(val)  -> first maximum wins, NaN propagates
     float best = -INFINITY;
     int bi = 0;
+    if constexpr (!BWD) {
+        // forward, k = 2 / 4: one vector load per window row (the 4x4 pool of the
+        // 20-channel network input, segment.py:23, streams 168 MB), same visiting order
+        const int s = (a.x.nseg > 1 && c >= a.x.s[0].C)
+                          ? ((a.x.nseg > 2 && c >= a.x.s[0].C + a.x.s[1].C) ? 2 : 1) : 0;
+        const int cb = s == 0 ? 0 : (s == 1 ? a.x.s[0].C : a.x.s[0].C + a.x.s[1].C);
+        const isg_vseg& sg = s == 0 ? a.x.s[0] : (s == 1 ? a.x.s[1] : a.x.s[2]);
+        const int xf = sg.xform, act = sg.act;
+        if ((k == 4 || k == 2) && xf != ISG_XF_BN_BWD) {
+            const float* base = sg.p + (int64_t)n * sg.n_stride + (int64_t)(c - cb) * hw;
+            const ChanCoef kc = coef[c];
+            auto tf = [&](float x) {
+                return xf == ISG_XF_PLAIN ? x : apply_act((x - kc.c0) * kc.c1 + kc.c2, act, kc.c3);
+            };
+            for (int dy = 0; dy < k; ++dy) {
+                const float* row = base + (int64_t)(oy * k + dy) * W + ox * k;
+                float v[4];
+                if (k == 4) {
+                    const f32x4 q = *reinterpret_cast<const f32x4*>(row);
+                    v[0] = q[0]; v[1] = q[1]; v[2] = q[2]; v[3] = q[3];
+                } else {
+                    const float2 q = *reinterpret_cast<const float2*>(row);
+                    v[0] = q.x; v[1] = q.y;
+                }
+                for (int dx = 0; dx < k; ++dx) {
+                    const float x = tf(v[dx]);
+                    if (x > best || isnan(x)) {
+                        best = x;
+                        bi = dy * k + dx;
+                    }
+                }
+            }
+            a.out[(int64_t)n * a.out_n_stride + (int64_t)c * ohw + op] = best;
+            return;
+        }
+    }
     for (int dy = 0; dy < k; ++dy)
         for (int dx = 0; dx < k; ++dx) {
             const int64_t pix = (int64_t)(oy * k + dy) * W + ox * k + dx;
