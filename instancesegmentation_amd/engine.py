@@ -658,7 +658,8 @@ class PoolOp:
         r = Record(L.OP_MAXPOOL_FWD, L.PoolRec,
                    {"x": vtensor(segs, g.N, self.x.H, self.x.W), "k": self.k,
                     "out": self.out.ptr(self.c0), "out_ns": self.out.n_stride},
-                   label=self.out.name)
+                   label=self.out.name,
+                   nbytes=4 * g.N * self.x.C * (self.x.H * self.x.W + self.out.H * self.out.W))
         # bytes this op writes (for _fork_pools): its channels of every image
         o = self.out.ptr(self.c0)
         hw = self.out.H * self.out.W
@@ -681,7 +682,8 @@ class PoolOp:
         ops.add(Record(L.OP_MAXPOOL_BWD, L.PoolRec,
                        {"x": vtensor(segs, g.N, self.x.H, self.x.W), "k": self.k,
                         "dout": d.ptr(self.c0), "dout_ns": d.n_stride,
-                        "dx": sinks_spec(sinks)}, label="dx_" + self.out.name))
+                        "dx": sinks_spec(sinks)}, label="dx_" + self.out.name,
+                       nbytes=4 * g.N * self.x.C * (2 * self.x.H * self.x.W + self.out.H * self.out.W)))
 
 
 class TailOp:
