@@ -41,10 +41,31 @@ def parse():
     return ap.parse_args()
 
 
-def setup_dist():
+def launch_ranks(args):
+    """`python bench.py --gpus N` outside a launcher: start N ranks (one process per GPU)
+    with torch.distributed.run and exit with its status. This parent never touches the
+    GPU (the children initialise HIP themselves)."""
+    import socket
+    import subprocess
+    import sys
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+           "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def setup_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} "
+                         "rank(s); run it without a launcher or with --nproc-per-node "
+                         f"{args.gpus}")
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -207,7 +228,9 @@ def cpu_baseline(args):
 
 def main():
     args = parse()
-    world, rank, local = setup_dist()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(launch_ranks(args))
+    world, rank, local = setup_dist(args)
     dev = torch.device("cuda", local)
     from instancesegmentation_amd import _lib as L
     from instancesegmentation_amd.data import device_batch

@@ -6,6 +6,7 @@ hipcc cross-compiles on a CPU-only host; the resulting .so travels to the GPU bo
 with the repo snapshot (it is git-ignored, not gpurun-ignored).
 """
 import os
+import re
 import subprocess
 import sys
 
@@ -18,12 +19,29 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall",
          "-Wno-unused-function", "-Wno-pass-failed"]
 
 
+_INCLUDE = re.compile(r'^\s*#\s*include\s*"([^"]+)"', re.M)
+
+
+def _deps(src, seen=None):
+    """`src` and every quoted header it includes, transitively (so an edit to stage.h,
+    common.h or isg.h rebuilds exactly the objects that include it)."""
+    seen = set() if seen is None else seen
+    src = os.path.normpath(src)
+    if src in seen or not os.path.exists(src):
+        return seen
+    seen.add(src)
+    with open(src, errors="replace") as f:
+        text = f.read()
+    for inc in _INCLUDE.findall(text):
+        _deps(os.path.join(os.path.dirname(src), inc), seen)
+    return seen
+
+
 def _stale(obj, src):
     if not os.path.exists(obj):
         return True
-    deps = [src, os.path.join(CSRC, "common.h"),
-            os.path.join(os.path.dirname(HERE), "include", "isg.h")]
-    return any(os.path.getmtime(d) > os.path.getmtime(obj) for d in deps)
+    t = os.path.getmtime(obj)
+    return any(os.path.getmtime(d) > t for d in _deps(src))
 
 
 def build(verbose=False, jobs=4):

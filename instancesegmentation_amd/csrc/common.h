@@ -285,9 +285,8 @@ ISG_DEV bool sinks_need_red(const isg_sinks& sk) {
 
 // ---- fused BatchNorm finalisation ---------------------------------------------------
 // Every thread of every workgroup of a launch whose sinks carry fin_mode calls this LAST
-// (no early return before it). The statistics are written only by device-scope atomics,
-// which are performed at the memory side: once a workgroup's waves have retired them
-// (vmcnt(0)) no release fence is needed, the ticket alone publishes. Tickets are two
+// (no early return before it). After the workgroup barrier, an agent-scope release fence
+// orders the workgroup's statistics atomics before its ticket; the last arriver acquires. Tickets are two
 // level — 32 sub-counters, the last arriver of each bumps the top counter — so at most
 // ~nb/32 workgroups contend on one address. The workgroup that completes the top counter
 // acquires and evaluates the coefficients (fp64, isg_bn_finalize's math), then re-zeroes
@@ -298,6 +297,9 @@ ISG_DEV bool fin_last_block(uint32_t* ctr) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0 && threadIdx.y == 0) {
+        // release: every statistics write of this workgroup is ordered before its ticket
+        // (the HIP memory model's guarantee, not an assumption about where atomics land)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         const unsigned nb = gridDim.x * gridDim.y * gridDim.z;
         const unsigned b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
         bool last;

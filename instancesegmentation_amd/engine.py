@@ -161,6 +161,18 @@ class Buf:
         return Ptr(self.slot, (self.off + c0 * self.H * self.W) * 4)
 
 
+MAX_TENSOR_ELEMS = 2 ** 31 - 1
+
+
+def check_elems(b):
+    """The kernels address a tensor's elements (image stride x image + pixel) with 32-bit
+    offsets; a tensor at or above 2^31 elements is refused here, at plan time."""
+    if b.numel > MAX_TENSOR_ELEMS:
+        raise RuntimeError(f"{b.name}: {b.N}x{b.C}x{b.H}x{b.W} = {b.numel} elements exceeds "
+                           f"the kernels' 32-bit element offsets ({MAX_TENSOR_ELEMS}); "
+                           "split the batch")
+
+
 class BNRef:
     def __init__(self, mod, C, count, stats_off, names):
         self.mod, self.C, self.count, self.stats_off = mod, C, count, stats_off
@@ -261,6 +273,7 @@ class Graph:
     # -- allocation ----------------------------------------------------------------------
     def act_buf(self, C, H, W, name):
         b = Buf(S_ACT, self.N, C, H, W, name, off=self.act_size)
+        check_elems(b)
         self.act_size += (b.numel + ALIGN - 1) // ALIGN * ALIGN
         self.act_bufs.append(b)
         return b
@@ -315,6 +328,7 @@ class Graph:
     # -- ops -----------------------------------------------------------------------------
     def input(self, idx, C, H, W, grad):
         b = Buf(S_IN[idx], self.N, C, H, W, f"in{idx}")
+        check_elems(b)
         return Value([Val(b, 0, C, grad=grad)])
 
     def conv(self, conv, x, bn=None, act="none", slope=None, name=""):
@@ -484,6 +498,7 @@ class GradState:
 
     def alloc(self, like, name):
         b = Buf(S_GRAD, like.N, like.C, like.H, like.W, name, off=self.size)
+        check_elems(b)
         self.size += (b.numel + ALIGN - 1) // ALIGN * ALIGN
         return b
 
@@ -787,6 +802,64 @@ class Plan:
         if need_grad:
             self._build_backward(g, ins)
 
+    @staticmethod
+    def _late_prefix(g):
+        """Module-name prefix of the late gradient bucket: the owner's first child module
+        (Segment: `init_conv.`, whose parameters lead the parameter order and whose
+        backward runs last), or None when the owner has no children with parameters."""
+        for name, child in g.owner.named_children():
+            if any(True for _ in child.parameters()):
+                return name + "."
+            return None
+        return None
+
+    def _bucket_split(self, g, gs, recs):
+        """(cut, split): bucket 2 = the parameters under the late prefix, a leading range
+        [0, cut) of the flat gradient; split = the first backward op after which no op
+        touches (by any pointer) bucket 1's gradient replicas or the statistics its
+        finalisation reads. Returns (0, len(recs)) when no such split exists."""
+        late = self._late_prefix(g)
+        if late is None or not g.train:
+            return 0, len(recs)
+        cut = 0
+        for k in g.param_names:
+            if not k.startswith(late):
+                break
+            n = 1
+            for s in g.param_shapes[k]:
+                n *= s
+            cut += n
+        if any(k.startswith(late) for k in g.param_names[len([1 for k in g.param_names
+                                                               if k.startswith(late)]):]):
+            return 0, len(recs)  # late parameters are not a leading range
+        # statistics ranges (bytes in S_STATS) of bucket-1 modules
+        early_stats = []
+        for b in g.bns:
+            if not g.mod_names[id(b.mod)].startswith(late):
+                n = (4 * b.C * L.STAT_REP + 7) // 8 * 8
+                early_stats.append((b.stats_off * 8, (b.stats_off + n) * 8))
+                early_stats.append((b.coef_off * 8, (b.ctr_bwd + 24) * 8))
+        for sl in g.slopes.values():
+            if not g.mod_names[id(sl.mod)].startswith(late):
+                early_stats.append((sl.acc_off * 8, (sl.acc_off + sl.C * L.STAT_REP) * 8))
+        for mod, out, _ in gs.bias_sums:
+            if not g.mod_names[id(mod)].startswith(late):
+                early_stats.append((out.need_sum * 8, (out.need_sum + 4 * out.C * L.STAT_REP) * 8))
+
+        def touches_early(r):
+            for _, slot, off in r.fix:
+                if slot in (S_PGRAD, S_WREP) and off >= cut * 4:
+                    return True
+                if slot == S_STATS and any(lo <= off < hi for lo, hi in early_stats):
+                    return True
+            return False
+
+        split = 0
+        for i, r in enumerate(recs):
+            if touches_early(r):
+                split = i + 1
+        return cut, split
+
     def _emit_output(self, g, o, ob):
         # route the value into the output slot with a tail (copy / BN+act)
         c = 0
@@ -820,23 +893,17 @@ class Plan:
         for r in body.recs:
             if r.kind == L.OP_CONV_WGRAD:
                 r.flags |= Record.OPF_SIDE  # nothing later in the list reads a weight gradient
-            bw.add(r)
         self.din_written = [v.grad and bool(gs.inited.get(id(v.segs[0].buf)))
                             for v in ins]
-        fold = Record(L.OP_SUM_REP, L.SumRepRec, {"dst": Ptr(S_PGRAD), "src": Ptr(S_WREP),
-                                                  "n": g.pgrad_size, "stride": g.pgrad_size,
-                                                  "nrep": L.WREP}, label="sum_wgrad_replicas")
-        fold.flags |= Record.OPF_JOIN  # every forked weight gradient is in the replicas
-        bw.add(fold)
-        # finalisation of BN / PReLU / conv-bias-before-BN gradients
+        # finalisation of BN / PReLU / conv-bias-before-BN gradients: (module, item)
         conv_before = {id(bnr): mod for mod, bnr in gs.bias_from_bn}
         items = []
         # bias of a convT with no BN after it (segment.py:435-436): the per-channel sum
         # of its output gradient, accumulated by the consumers' gradient sinks
         for mod, out, dy in gs.bias_sums:
-            items.append({"slope_acc": Ptr(S_STATS, out.need_sum * 8),
-                          "dslope": g.gptr(mod, "bias"), "C": out.C,
-                          "slope_stride": 4 * out.C})
+            items.append((mod, {"slope_acc": Ptr(S_STATS, out.need_sum * 8),
+                                "dslope": g.gptr(mod, "bias"), "C": out.C,
+                                "slope_stride": 4 * out.C}))
         for b in g.bns:
             it = {"stats": Ptr(S_STATS, b.stats_off * 8), "gamma": b.names["gamma"],
                   "running_mean": b.names["rm"], "running_var": b.names["rv"],
@@ -845,15 +912,52 @@ class Plan:
                   "eps": float(b.mod.eps)}
             if id(b) in conv_before:
                 it["dconv_bias"] = g.gptr(conv_before[id(b)], "bias")
-            items.append(it)
+            items.append((b.mod, it))
         for sl in g.slopes.values():
             if sl.used_in_bwd:
-                items.append({"slope_acc": Ptr(S_STATS, sl.acc_off * 8),
-                              "dslope": g.gptr(sl.mod, "weight"), "C": sl.C,
-                              "slope_stride": sl.C})
-        for i in range(0, len(items), L.LIST_CHUNK):
-            chunk = items[i:i + L.LIST_CHUNK]
-            bw.add(Record(L.OP_GRAD_FINAL, L.ListRec, {"n": len(chunk)}, L.GradFinal, chunk))
+                items.append((sl.mod, {"slope_acc": Ptr(S_STATS, sl.acc_off * 8),
+                                       "dslope": g.gptr(sl.mod, "weight"), "C": sl.C,
+                                       "slope_stride": sl.C}))
+        cut, split = self._bucket_split(g, gs, body.recs)
+        late = self._late_prefix(g)
+
+        def is_late(mod):
+            return late is not None and g.mod_names[id(mod)].startswith(late)
+
+        def close(ol, lo, hi, its):
+            """Fold the weight-gradient replicas of parameter range [lo, hi) (floats) and
+            finalise the statistics-derived gradients of that range."""
+            if hi > lo:
+                fold = Record(L.OP_SUM_REP, L.SumRepRec,
+                              {"dst": Ptr(S_PGRAD, lo * 4), "src": Ptr(S_WREP, lo * 4),
+                               "n": hi - lo, "stride": g.pgrad_size, "nrep": L.WREP},
+                              label="sum_wgrad_replicas")
+                fold.flags |= Record.OPF_JOIN  # every forked weight gradient is in the replicas
+                ol.add(fold)
+            for i in range(0, len(its), L.LIST_CHUNK):
+                chunk = its[i:i + L.LIST_CHUNK]
+                ol.add(Record(L.OP_GRAD_FINAL, L.ListRec, {"n": len(chunk)}, L.GradFinal, chunk))
+
+        # Two gradient buckets for data parallelism (SURVEY.md §8e): bucket 1 = parameters
+        # [cut, n), final once body[:split] has run; bucket 2 = [0, cut) (the stem, whose
+        # backward runs last). The Trainer all-reduces bucket 1 on RCCL's stream while the
+        # stem backward (body[split:]) runs. split == len(body): one bucket at the end.
+        part1, part2 = OpList(), OpList()
+        part1.add(bw.recs[0])  # the replica memset
+        for r in body.recs[:split]:
+            part1.add(r)
+        if split < len(body.recs):
+            close(part1, cut, g.pgrad_size, [it for m, it in items if not is_late(m)])
+            for r in body.recs[split:]:
+                part2.add(r)
+            close(part2, 0, cut, [it for m, it in items if is_late(m)])
+        else:
+            cut = 0
+            close(part1, 0, g.pgrad_size, [it for _, it in items])
+        for r in part1.recs[1:] + part2.recs:
+            bw.add(r)
+        self.bucket_cut = cut
+        self.bwd_parts = [part1.compile()] + ([part2.compile()] if part2.recs else [])
         self.stats_size = max(g.stats_size, 8)
         self.bwd = bw.compile()
         self.grad_size = gs.size

@@ -4,16 +4,18 @@
     loss.backward(); optimizer.step(); loss.item()
 
 One `Trainer.step` runs, on one HIP stream and without torch autograd:
-  forward op list -> fused sigmoid+BCE (loss + dlogits) -> backward op list ->
-  [RCCL all-reduce(avg) of the flat 1.06 MB gradient bucket when world_size > 1] ->
+  forward op list -> fused sigmoid+BCE (loss + dlogits) -> backward part 1 ->
+  [world > 1: RCCL SUM of gradient bucket 1 + running statistics, asynchronous] ->
+  backward part 2 (the stem) -> [world > 1: bucket 2, wait] ->
   multi-tensor Adam over the flat parameter buffer.
 Parameters, gradients and BN running statistics live in flat buffers (module tensors
-are re-bound as views), so the optimizer is one kernel and the gradient exchange is one
-collective. The whole step is capturable into a HIP graph (`capture()`).
+are re-bound as views), so the optimizer is one kernel and the exchange is two
+collectives over one buffer. The step is captured into HIP graphs (`capture()`): one
+graph at world 1, three at world > 1 with the collectives issued between them.
 
 Data parallelism: one process per GPU, image-batch sharded, local BN
-statistics per replica, running stats broadcast from rank 0 each step (DDP's
-broadcast_buffers default), gradient mean over ranks.
+statistics per replica, rank 0's running statistics on every replica after each step
+(DDP's broadcast_buffers), gradient mean over ranks.
 """
 import ctypes
 
@@ -26,35 +28,45 @@ from .engine import (S_ACT, S_DOUT, S_GRAD, S_IN, S_OUT, S_PGRAD, S_STATS, S_TEN
 
 
 class GradSync:
-    """The data-parallel exchange of one step, one process per GPU:
-    rank 0's BatchNorm running statistics are broadcast before the step (DDP
-    broadcast_buffers), and the flat gradient bucket is averaged over the ranks after
-    the backward (one collective: RCCL AVG on "nccl"; SUM then scale on gloo, which has no
-    AVG). BN batch statistics stay local to each replica, as in the reference run per
-    replica."""
+    """The data-parallel exchange of one step, one process per GPU.
+
+    Both gradient buckets and the BatchNorm running statistics travel in SUM all-reduces
+    over one flat buffer `comm = [grad bucket 2 | grad bucket 1 | float buffers]`:
+      * gradients arrive pre-divided by the world size (the BCE gradient scale is
+        1/(pixels * world)), so the SUM is the replica mean DDP computes;
+      * every rank but 0 zeroes its buffer slice first, so the SUM hands every replica
+        rank 0's running statistics — DDP's `broadcast_buffers`, folded into the
+        gradient collective instead of a second eager broadcast per step.
+    Bucket 1 (every parameter but the stem's) is launched asynchronously as soon as the
+    backward has finalised it, and overlaps the stem's backward; bucket 2 (the stem)
+    follows the last weight gradient. On "nccl" (RCCL) the collectives run on the process
+    group's own stream behind an event of the current stream and `wait()` makes the
+    current stream wait for them; on gloo (CPU tests) they complete on the host. BN batch
+    statistics stay local to each replica, as in the reference run per replica."""
 
     def __init__(self, process_group=None):
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
-        self.avg = self.world > 1 and dist.get_backend(process_group) == "nccl"
+        self.rank = dist.get_rank(process_group) if dist.is_initialized() else 0
+        self._pending = []
 
-    def buffers(self, flatb):
-        if self.world > 1:
-            dist.broadcast(flatb, 0, group=self.pg)
+    def begin(self, bucket):
+        """Launch the SUM all-reduce of `bucket` (a view of comm) asynchronously."""
+        if self.world > 1 and bucket.numel():
+            self._pending.append(dist.all_reduce(bucket, op=dist.ReduceOp.SUM, group=self.pg,
+                                                 async_op=True))
 
-    def grads(self, grad_flat):
-        if self.world == 1:
-            return
-        if self.avg:
-            dist.all_reduce(grad_flat, op=dist.ReduceOp.AVG, group=self.pg)
-        else:
-            dist.all_reduce(grad_flat, op=dist.ReduceOp.SUM, group=self.pg)
-            grad_flat.div_(self.world)
+    def end(self):
+        """Make the current stream (or host, on gloo) wait for every launched bucket."""
+        for w in self._pending:
+            w.wait()
+        self._pending = []
 
 
-def flatten_module(model, device):
+def flatten_module(model, device, flatb=None):
     """Re-bind every parameter and floating buffer of `model` as a view of one flat
-    buffer (params) / (float buffers); returns (flat_params, flat_bufs, param_index)."""
+    buffer (params) / (float buffers, into `flatb` when given: the Trainer passes the
+    tail of its exchange buffer); returns (flat_params, flat_bufs, param_index)."""
     params = [p for _, p in model.named_parameters()]
     n = sum(p.numel() for p in params)
     flat = torch.empty(n, dtype=torch.float32, device=device)
@@ -70,7 +82,10 @@ def flatten_module(model, device):
     fbufs = [(m, name, b) for m in model.modules() for name, b in m._buffers.items()
              if b is not None and b.is_floating_point()]
     nb = sum(b.numel() for _, _, b in fbufs)
-    flatb = torch.empty(max(nb, 1), dtype=torch.float32, device=device)
+    if flatb is None:
+        flatb = torch.empty(max(nb, 1), dtype=torch.float32, device=device)
+    elif flatb.numel() < nb:
+        raise ValueError(f"flatten_module: buffer storage of {flatb.numel()} < {nb} floats")
     off = 0
     with torch.no_grad():
         for m, name, b in fbufs:
@@ -85,41 +100,57 @@ def flatten_module(model, device):
     return flat, flatb, index
 
 
+def _float_buffer_count(model):
+    return sum(b.numel() for m in model.modules() for b in m._buffers.values()
+               if b is not None and b.is_floating_point())
+
+
 class Trainer:
-    """train_instance.py:294-382 step body on the MI355X (Segment + BCELoss + Adam)."""
+    """train_instance.py:294-382 step body on the MI355X (Segment + BCELoss + Adam).
+
+    The flat parameter gradient and the flat BN running statistics share one buffer
+    (`comm`), the data-parallel exchange unit (GradSync). A Trainer can be constructed
+    on a CPU device (tests drive its exchange over gloo); `step()` needs the GPU."""
 
     def __init__(self, model, batch, in_shapes, device=None, lr=1e-3, betas=(0.9, 0.999),
                  eps=1e-8, weight_decay=0.0, process_group=None):
         self.device = torch.device(device or "cuda")
-        self.model = model.to(self.device).train()
-        self.flat, self.flatb, self.index = flatten_module(self.model, self.device)
+        dev = self.device
+        self.model = model.to(dev).train()
+        self.sync = GradSync(process_group)
+        self.world, self.rank = self.sync.world, self.sync.rank
+        n = sum(p.numel() for p in self.model.parameters())
+        nb = _float_buffer_count(self.model)
+        self.comm = torch.zeros(n + max(nb, 1), dtype=torch.float32, device=dev)
+        self.flat, self.flatb, self.index = flatten_module(self.model, dev, self.comm[n:])
         self.in_shapes = [tuple(s) for s in in_shapes]
         self.plan = Plan(self.model, self.in_shapes, True, True,
                          tuple(False for _ in self.in_shapes))
         g = self.plan.graph
+        assert g.pgrad_size == n
         self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
-        self.pg = process_group
-        self.sync = GradSync(process_group)
-        self.world = self.sync.world
-        dev = self.device
         self.act = torch.empty(max(self.plan.act_size, 1), dtype=torch.float32, device=dev)
         self.stats = torch.empty(self.plan.stats_size, dtype=torch.float64, device=dev)
         self.gradarena = torch.empty(max(self.plan.grad_size, 1), dtype=torch.float32, device=dev)
         # the plan's packed param-grad layout is exactly the flat buffer's order
-        self.grad_flat = torch.zeros_like(self.flat)
+        self.grad_flat = self.comm[:n]
         self.pgrad = self.grad_flat
+        cut = self.plan.bucket_cut
+        self.buckets = [self.comm[cut:], self.comm[:cut]]  # launch order: 1 (+buffers), 2
         self.wrep = torch.empty(L.WREP * g.pgrad_size, dtype=torch.float32, device=dev)
-        assert g.pgrad_size == self.flat.numel()
         self.logits = torch.empty(self.plan.out_shapes[0], dtype=torch.float32, device=dev)
         self.dlogits = torch.empty_like(self.logits)
+        # BCELoss mean over this replica's pixels, pre-divided by the world size so the
+        # exchange's SUM is the replica mean (GradSync)
+        self.grad_scale = 1.0 / (self.logits.numel() * self.world)
         self.loss_acc = torch.zeros(1, dtype=torch.float64, device=dev)
         self._pg_views = []
-        for (k, p), (off, n) in zip(self.model.named_parameters(), self.index):
-            self._pg_views.append((g.pgrad_off[k], off, n, k in self.plan.used_params))
+        for (k, p), (off, cnt) in zip(self.model.named_parameters(), self.index):
+            self._pg_views.append((g.pgrad_off[k], off, cnt, k in self.plan.used_params))
         live = torch.zeros(self.flat.numel(), dtype=torch.uint8)
-        for _, off, n, used in self._pg_views:
+        for _, off, cnt, used in self._pg_views:
             if used:
-                live[off:off + n] = 1
+                live[off:off + cnt] = 1
         self.live = live.to(dev)
         self.exp_avg = torch.zeros_like(self.flat)
         self.exp_avg_sq = torch.zeros_like(self.flat)
@@ -151,18 +182,6 @@ class Trainer:
         return tab
 
     # ---- the step body -------------------------------------------------------------
-    def _fwd_bwd(self):
-        """forward -> sigmoid+BCE (loss, dlogits) -> backward; HIP work only."""
-        lib = L.lib()
-        st = L.stream_ptr(self.device)
-        self.plan.fwd.run(self.table, st)
-        n = self.logits.numel()
-        L.check(lib.isg_fill_f64(self.loss_acc.data_ptr(), 1, 0.0, st), "fill")
-        L.check(lib.isg_bce_sigmoid(self.logits.data_ptr(), self.target.data_ptr(), n,
-                                    self.loss_acc.data_ptr(), self.dlogits.data_ptr(),
-                                    1.0 / n, st), "bce")
-        self.plan.bwd.run(self.table, st, L.side_stream_ptr(self.device))
-
     def _adam(self):
         L.check(L.lib().isg_adam_dev(self.flat.data_ptr(), self.grad_flat.data_ptr(),
                                      self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(),
@@ -178,18 +197,40 @@ class Trainer:
         L.check(lib.isg_fill_f64(self.loss_acc.data_ptr(), 1, 0.0, st), "fill")
         L.check(lib.isg_bce_sigmoid(self.logits.data_ptr(), self.target.data_ptr(), n,
                                     self.loss_acc.data_ptr(), self.dlogits.data_ptr(),
-                                    1.0 / n, st), "bce")
+                                    self.grad_scale, st), "bce")
+
+    def _mask_buffers(self):
+        """DDP broadcast_buffers through the SUM exchange: ranks > 0 contribute zeros."""
+        if self.rank != 0:
+            self.flatb.zero_()
+
+    # exchange markers: run eagerly between captured graphs (RCCL is not captured)
+    def exchange_begin(self):
+        """Bucket 1 (all parameters but the stem's, plus the running statistics)."""
+        self.sync.begin(self.buckets[0])
+
+    def exchange_end(self):
+        """Bucket 2 (the stem), then wait for both."""
+        self.sync.begin(self.buckets[1])
+        self.sync.end()
 
     def _schedule(self, split=None):
         """The step as a list of units: callables issuing HIP work, or the markers
-        'coll' (eager RCCL all-reduce), 'tic'/'toc' (timing events around one op).
-        split=(phase, idx) isolates op `idx` of the forward/backward list."""
+        'coll1'/'coll2' (eager RCCL bucket exchange), 'tic'/'toc' (timing events around
+        one op). split=(phase, idx) isolates op `idx` of the forward/backward list."""
         def run_list(ol):
             return lambda: ol.run(self.table, L.stream_ptr(self.device), L.side_stream_ptr(self.device))
+        dp = self.world > 1
+        lists = [("fwd", self.plan.fwd)] + [("bwd", p) for p in self.plan.bwd_parts]
         units = []
-        for phase, ol in (("fwd", self.plan.fwd), ("bwd", self.plan.bwd)):
+        base = 0  # index of the current backward part's first op in the whole backward
+        for j, (phase, ol) in enumerate(lists):
+            i = None
             if split and split[0] == phase:
-                i = split[1]
+                i = split[1] - (base if phase == "bwd" else 0)
+                if not 0 <= i < len(ol.recs):
+                    i = None
+            if i is not None:
                 if i > 0:
                     units.append(run_list(ol.slice(0, i)))
                 units += ["tic", run_list(ol.slice(i, i + 1)), "toc"]
@@ -199,14 +240,36 @@ class Trainer:
                 units.append(run_list(ol))
             if phase == "fwd":
                 units.append(self._loss)
-        if self.world > 1:
-            units.append("coll")
+            else:
+                base += len(ol.recs)
+                if dp and j == 1:
+                    units += [self._mask_buffers, "coll1"]
+        if dp:
+            units.append("coll2")
         units.append(self._adam)
         return units
 
-    def capture(self, split=None):
+    def _state(self):
+        return [self.comm, self.flat, self.exp_avg, self.exp_avg_sq, self.step_dev,
+                self.loss_acc] + [b for _, b in self.model.named_buffers()
+                                  if not b.is_floating_point()]
+
+    def warm(self):
+        """Run the step once eagerly (first-use initialisation in libisg, RCCL
+        communicators) and restore the training state, so a capture can be the first
+        training step."""
+        saved = [t.clone() for t in self._state()]
+        self._run(self._schedule())
+        torch.cuda.synchronize(self.device)
+        with torch.no_grad():
+            for t, v in zip(self._state(), saved):
+                t.copy_(v)
+
+    def capture(self, split=None, warm=True):
         """Record the step into HIP graphs: every run of consecutive HIP units becomes one
         graph; markers between them stay eager (RCCL collectives, timing events)."""
+        if warm:
+            self.warm()
         torch.cuda.synchronize(self.device)
         plan = []
         cur = []
@@ -234,8 +297,10 @@ class Trainer:
                 u.replay()
             elif callable(u):
                 u()
-            elif u == "coll":
-                self.sync.grads(self.grad_flat)
+            elif u == "coll1":
+                self.exchange_begin()
+            elif u == "coll2":
+                self.exchange_end()
             elif u == "tic":
                 ev = torch.cuda.Event(enable_timing=True)
                 ev.record()
@@ -247,13 +312,14 @@ class Trainer:
     def step(self, x=None, target=None):
         """One optimisation step. x: list of input tensors (copied into the static input
         buffers), target: mask. Returns the loss as a device tensor (no host sync)."""
+        if self.device.type != "cuda":
+            raise RuntimeError("Trainer.step runs on the MI355X only (no CPU path)")
         if x is not None:
             for dst, src in zip(self.inputs, x):
                 dst.copy_(src, non_blocking=True)
         if target is not None:
             self.target.copy_(target, non_blocking=True)
         self.step_count += 1
-        self.sync.buffers(self.flatb)  # DDP broadcast_buffers: rank 0's BN running stats
         self._run(self.graphs if self.graphs else self._schedule(self.split))
         return self.loss_acc / self.logits.numel()
 
@@ -261,7 +327,8 @@ class Trainer:
         return (self.loss_acc / self.logits.numel()).item()
 
     def grads(self):
-        """Per-parameter gradient views of the last step (None for unused parameters)."""
+        """Per-parameter gradient views of the last step (None for unused parameters).
+        With world > 1 this is the exchanged replica mean."""
         out = []
         for (k, p), (pgo, off, n, used) in zip(self.model.named_parameters(), self._pg_views):
             out.append(self.grad_flat[off:off + n].view_as(p) if used else None)

@@ -1,0 +1,62 @@
+"""Shared whole-network comparison bars for the GPU parity tests.
+
+Logits: the absolute error against the fp64 reference is reported and must be within
+max(1e-4, 2x the CPU-fp32 reference's own error on the same inputs) — the north_star's
+"fp32 mask logits within 1e-4", relaxed only where the reference's own fp32 result is
+already further than 1e-4 from fp64 — and within 1e-4 * max(1, |logit|max).
+
+Gradients, per parameter tensor: max-abs error <= max(2x the CPU-fp32 reference's own
+error of that tensor, 2e-3 of the tensor's scale). Conv biases that feed a training-mode
+BatchNorm have a mathematically zero gradient (the reference's value is rounding noise,
+SURVEY.md §7): they must be below 1e-4 in magnitude instead.
+"""
+import numpy as np
+import torch
+
+
+def dead_bias(key):
+    return key.endswith(".conv.bias") or (key.split(".")[0].endswith("up")
+                                          and key.endswith("convs.1.bias"))
+
+
+def _t(x):
+    return x.detach().double().cpu() if isinstance(x, torch.Tensor) else \
+        torch.from_numpy(np.asarray(x)).double()
+
+
+def check_logits(got, ref64, ref32, tag=""):
+    got, ref64, ref32 = _t(got), _t(ref64), _t(ref32)
+    err = (got - ref64).abs().max().item()
+    floor = (ref32 - ref64).abs().max().item()
+    scale = max(1.0, ref64.abs().max().item())
+    print(f"{tag}: logits max abs err {err:.3e} (bar 1e-4; CPU-fp32 reference's own err "
+          f"{floor:.3e}; |logit|max {ref64.abs().max().item():.2f})")
+    assert err <= max(1e-4, 2.0 * floor), (err, floor)
+    assert err <= 1e-4 * scale, (err, scale)
+    return err
+
+
+def check_grads(got, ref64, ref32, none_keys, tag=""):
+    """got/ref64/ref32: dicts key -> tensor (or None)."""
+    fails, worst = [], []
+    for k, g in got.items():
+        if k in none_keys:
+            assert g is None, f"{k}: the reference has no gradient"
+            continue
+        assert g is not None, f"{k}: missing gradient"
+        r = _t(ref64[k])
+        gg = _t(g)
+        if dead_bias(k):
+            assert gg.abs().max().item() < 1e-4, k
+            continue
+        sc = max(r.abs().max().item(), 1e-12)
+        err = (gg - r).abs().max().item()
+        floor = (_t(ref32[k]) - r).abs().max().item()
+        allowed = max(2.0 * floor, 2e-3 * sc)
+        worst.append((err / allowed, k, err / sc, floor / sc))
+        if err > allowed:
+            fails.append((k, round(err / allowed, 2)))
+    worst.sort(reverse=True)
+    print(f"{tag}: {len(worst)} gradient tensors, worst (key, err/bar, err/scale, "
+          f"fp32-ref err/scale): {[(k, round(a, 3), f'{e:.1e}', f'{f:.1e}') for a, k, e, f in worst[:4]]}")
+    assert not fails, f"{tag}: gradients above the bar: {fails}"

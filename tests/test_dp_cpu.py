@@ -1,8 +1,9 @@
 """Data-parallel semantics on CPU (gloo, world_size 2), SURVEY.md §8e: each replica runs
 the train step on its own sub-batch with LOCAL BatchNorm statistics; the exchanged
 gradient equals the mean of the per-replica oracle gradients, and rank 0's BN running
-statistics reach every replica (DDP broadcast_buffers). The exchange is the Trainer's own
-GradSync (RCCL AVG on GPUs; SUM + scale on gloo)."""
+statistics reach every replica (DDP broadcast_buffers). What runs is the Trainer's own
+exchange (instancesegmentation_amd/train.py: comm buffer, two buckets, SUM) — the same
+code path as RCCL on the GPUs, over gloo."""
 import os
 import socket
 
@@ -13,7 +14,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from instancesegmentation_amd.model.segment import Segment
-from instancesegmentation_amd.train import GradSync
+from instancesegmentation_amd.train import Trainer
 from oracle import segment_oracle
 from oracle.seeding import synth_batch, synth_params
 
@@ -32,14 +33,19 @@ def _params():
     return synth_params(shapes, 5)
 
 
-def _replica_grads(params, x, mask):
-    # train_step updates BN running statistics in place: give it private copies
+def _replica(params, x, mask):
+    """Oracle fp64 train step of one replica on its sub-batch: (grads by key, params and
+    updated BN buffers by key). train_step updates BN running statistics in place: give
+    it private copies."""
     fresh = {k: np.array(v, copy=True) for k, v in params.items()}
     _, _, g, P = segment_oracle.train_step(fresh, x, mask, torch.float64)
-    keys = sorted(k for k, v in g.items() if v is not None)
-    flat = torch.cat([g[k].reshape(-1) for k in keys])
-    rm = torch.cat([P[k].reshape(-1) for k in sorted(P) if k.endswith("running_mean")])
-    return flat, rm
+    return g, P
+
+
+def _load(m, params):
+    sd = m.state_dict()
+    m.load_state_dict({k: torch.as_tensor(v).to(sd[k].dtype) for k, v in params.items()})
+    return m
 
 
 def _worker(rank, world, port, out):
@@ -49,42 +55,89 @@ def _worker(rank, world, port, out):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         params = _params()
-        x, mask = synth_batch(2 * world, 3, 32, 48, 9)  # global batch, 2 images per replica
-        sl = slice(2 * rank, 2 * rank + 2)
-        g, rm = _replica_grads(params, x[sl], mask[sl])
-        sync = GradSync()
-        gx = g.clone()
-        sync.grads(gx)
-        # reference: mean of every replica's gradient, each from its own sub-batch
-        ref = torch.stack([_replica_grads(params, x[2 * r:2 * r + 2], mask[2 * r:2 * r + 2])[0]
-                           for r in range(world)]).mean(0)
-        err = (gx - ref).abs().max().item() / ref.abs().max().item()
-        # running statistics: each replica updated its own; the broadcast makes rank 0's win
-        rmx = rm.clone()
-        sync.buffers(rmx)
-        rm0 = _replica_grads(params, x[0:2], mask[0:2])[1]
-        berr = (rmx - rm0).abs().max().item()
-        local_differs = rank == 0 or (rm - rm0).abs().max().item() > 0
-        out[rank] = (err, berr, local_differs)
+        n, h, w = 2, 32, 48
+        x, mask = synth_batch(n * world, 3, h, w, 9)  # global batch, 2 images per replica
+        reps = [_replica(params, x[n * r:n * r + n], mask[n * r:n * r + n]) for r in range(world)]
+        # the Trainer's own exchange state on this replica: its flat gradient (as the
+        # step leaves it, pre-divided by the world size through the BCE scale) and its
+        # locally updated BN running statistics, in the Trainer's flat layout
+        tr = Trainer(_load(Segment(3), params), n, [(n, 3, h, w)], device="cpu")
+        assert tr.world == world and tr.rank == rank
+        assert tr.grad_scale == 1.0 / (n * h * w * world)
+        g, P = reps[rank]
+        names = [k for k, _ in tr.model.named_parameters()]
+        with torch.no_grad():
+            for k, (off, cnt) in zip(names, tr.index):
+                gk = g.get(k)
+                tr.grad_flat[off:off + cnt] = 0.0 if gk is None else \
+                    (gk.reshape(-1) * tr.grad_scale * (n * h * w)).float()
+            for k, b in tr.model.named_buffers():
+                b.copy_(P[k].to(b.dtype))
+        assert tr.plan.bucket_cut > 0 and len(tr.plan.bwd_parts) == 2
+        tr._mask_buffers()
+        tr.exchange_begin()
+        tr.exchange_end()
+        # reference: mean of every replica's gradient (each on its own sub-batch) and rank
+        # 0's running statistics
+        gerr = 0.0
+        for k, (off, cnt) in zip(names, tr.index):
+            ref = sum(rp[0][k] for rp in reps) / world if g.get(k) is not None else None
+            got = tr.grad_flat[off:off + cnt].double()
+            if ref is None:
+                assert got.abs().max().item() == 0.0, k
+                continue
+            sc = max(ref.abs().max().item(), 1e-30)
+            gerr = max(gerr, (got - ref.reshape(-1)).abs().max().item() / sc)
+        berr, local_differs = 0.0, rank == 0
+        for k, b in tr.model.named_buffers():
+            if not b.is_floating_point():
+                continue
+            ref0 = reps[0][1][k].float()
+            berr = max(berr, (b - ref0).abs().max().item())
+            local_differs |= bool((P[k].float() - ref0).abs().max().item() > 0)
+        out[rank] = (gerr, berr, local_differs)
     finally:
         dist.destroy_process_group()
 
 
-def test_dp_gradient_mean_and_buffer_broadcast_gloo():
+def test_trainer_exchange_gloo():
+    """The Trainer's own two-bucket exchange (comm buffer, buffer masking, SUM of
+    world-scaled gradients) over gloo, world size 2."""
     world = 2
     mgr = mp.Manager()
     out = mgr.dict()
     mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
     for r in range(world):
-        err, berr, local_differs = out[r]
-        assert err < 1e-12, f"rank {r}: reduced gradient != mean of replicas ({err:.2e})"
+        gerr, berr, local_differs = out[r]
+        assert gerr < 1e-6, f"rank {r}: exchanged gradient != mean of replicas ({gerr:.2e})"
         assert berr == 0.0, f"rank {r}: running stats not rank 0's ({berr})"
         assert local_differs, "replicas must compute LOCAL batch statistics"
 
 
-def test_grad_sync_single_process_is_identity():
-    g = torch.arange(5, dtype=torch.float32)
-    s = GradSync()
-    s.grads(g)
-    s.buffers(g)
-    assert s.world == 1 and torch.equal(g, torch.arange(5, dtype=torch.float32))
+def test_single_process_exchange_is_identity():
+    m = Segment(3)
+    tr = Trainer(m, 2, [(2, 3, 32, 32)], device="cpu")
+    g = torch.arange(tr.comm.numel(), dtype=torch.float32)
+    tr.comm.copy_(g)
+    tr._mask_buffers()
+    tr.exchange_begin()
+    tr.exchange_end()
+    assert tr.world == 1 and torch.equal(tr.comm, g)
+    assert tr.grad_scale == 1.0 / (2 * 32 * 32)
+
+
+def test_bucket_split_covers_parameters():
+    """Bucket 2 is the stem's parameters (a leading range of the flat gradient); the
+    backward parts finalise exactly [cut, n) and [0, cut)."""
+    m = Segment(20)
+    tr = Trainer(m, 2, [(2, 3, 64, 64), (2, 17, 64, 64)], device="cpu")
+    names = [k for k, _ in m.named_parameters()]
+    cut = tr.plan.bucket_cut
+    stem = sum(p.numel() for k, p in m.named_parameters() if k.startswith("init_conv."))
+    assert cut == stem and names[0].startswith("init_conv.")
+    assert tr.buckets[0].numel() + tr.buckets[1].numel() == tr.comm.numel()
+    p1, p2 = tr.plan.bwd_parts
+    assert [r.label for r in p2.recs if r.label.startswith("dw_")] == \
+        ["dw_init_conv.layer2", "dw_init_conv.layer1"]
+    assert not any(r.label.startswith(("dw_init", "dx_init")) for r in p1.recs)
+    assert len(p1.recs) + len(p2.recs) == len(tr.plan.bwd.recs)

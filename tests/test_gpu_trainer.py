@@ -1,0 +1,138 @@
+"""Parity of the BENCHMARKED path: `Trainer.step` (flat parameter/gradient buffers, fused
+sigmoid+BCE kernel, the two-part backward with side-stream weight gradients, HIP-graph
+capture, isg_adam_dev with its device step counter and live mask) against
+
+  * the reference's own outputs (tests/golden/segment20_n2_128.npz, made by importing
+    /root/reference/model/segment.py): logits, loss, every gradient, BN running stats;
+  * the reference optimizer (`torch.optim.Adam(model.parameters())`,
+    train_instance.py:297,380) applied on the CPU to the gradients the GPU produced, for
+    two steps (bias corrections of step 1 and step 2, unused parameters untouched);
+  * the fp64 CPU oracle (oracle/segment_oracle.py) for step 2 on the updated
+    parameters, and at the bench configuration (bs2 1024x1024, Segment(20)).
+
+Bars: logits |err| <= max(2x the CPU-fp32 reference's own error vs fp64,
+1e-4 absolute) and <= 1e-4 * max(1, |logit|max); loss within 1e-5; gradients as
+tests/test_gpu_segment.py.
+"""
+import numpy as np
+import pytest
+import torch
+
+from instancesegmentation_amd.model.segment import Segment
+from instancesegmentation_amd.train import Trainer
+from oracle import segment_oracle
+from tests.golden_util import SegmentFixture
+from tests.grad_check import check_grads, check_logits
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _model(fx):
+    m = Segment(fx.cin)
+    sd = m.state_dict()
+    m.load_state_dict({k: torch.as_tensor(v).to(sd[k].dtype) for k, v in fx.params.items()})
+    return m
+
+
+def _inputs(x):
+    xt = torch.from_numpy(x).to(DEV)
+    return [xt[:, :3].contiguous(), xt[:, 3:].contiguous()]
+
+
+def _cpu_state(model):
+    return {k: v.detach().cpu().numpy().copy() for k, v in model.state_dict().items()}
+
+
+def _grads_by_key(tr):
+    return {k: (g.detach().cpu().clone() if g is not None else None)
+            for (k, _), g in zip(tr.model.named_parameters(), tr.grads())}
+
+
+@pytest.mark.parametrize("captured", [False, True], ids=["eager", "graph"])
+def test_trainer_two_steps_match_reference(captured):
+    fx = SegmentFixture("segment20_n2_128.npz")
+    model = _model(fx)
+    cpu_model = _model(fx)  # the reference optimizer runs on this copy
+    opt = torch.optim.Adam(cpu_model.parameters())  # train_instance.py:297
+    tr = Trainer(model, fx.n, [(fx.n, 3, fx.h, fx.w), (fx.n, 17, fx.h, fx.w)], device=DEV)
+    if captured:
+        tr.capture()
+    xs = _inputs(fx.x)
+    y = torch.from_numpy(fx.mask).to(DEV)
+
+    # ---- step 1 against the reference's own outputs -------------------------------
+    tr.step(xs, y)
+    torch.cuda.synchronize()
+    check_logits(tr.logits.cpu(), fx.z["logits64"], fx.z["logits32"], "step1")
+    assert abs(tr.loss() - float(fx.z["loss64"])) < 1e-5
+    g1 = _grads_by_key(tr)
+    ref1 = {k: torch.from_numpy(fx.grad(k).copy()) for k in fx.param_names}
+    flo1 = {k: torch.from_numpy(fx.grad(k, "grad32").copy()) for k in fx.param_names}
+    check_grads(g1, ref1, flo1, fx.grad_none, "step1")
+    sd = tr.model.state_dict()
+    for k, v in fx.buffers64().items():
+        got = sd[k].double().cpu().numpy()
+        if k.endswith("num_batches_tracked"):
+            assert int(got) == int(v), k
+        else:
+            np.testing.assert_allclose(got, v, rtol=1e-4, atol=1e-5, err_msg=k)
+
+    # Adam step 1 (bias corrections at step 1) on the GPU's own gradients
+    for (k, p) in cpu_model.named_parameters():
+        p.grad = None if g1[k] is None else g1[k].clone()
+    opt.step()
+    for (k, p), (kk, q) in zip(cpu_model.named_parameters(), tr.model.named_parameters()):
+        np.testing.assert_allclose(q.detach().cpu().numpy(), p.detach().numpy(), rtol=2e-6,
+                                   atol=1e-9, err_msg=f"adam step 1: {k}")
+
+    # ---- step 2: the oracle on the updated parameters --------------------------------
+    p1 = _cpu_state(tr.model)
+    ref_l2, ref_loss2, ref_g2, _ = segment_oracle.train_step(dict(p1), fx.x, fx.mask, torch.float64)
+    l32, _, g32, _ = segment_oracle.train_step(dict(p1), fx.x, fx.mask, torch.float32)
+    tr.step()  # same static inputs
+    torch.cuda.synchronize()
+    check_logits(tr.logits.cpu(), ref_l2.numpy(), l32.numpy(), "step2")
+    assert abs(tr.loss() - ref_loss2.item()) < 1e-5
+    g2 = _grads_by_key(tr)
+    check_grads(g2, ref_g2, g32, fx.grad_none, "step2")
+    assert int(tr.step_dev.item()) == 2
+
+    # Adam step 2 (bias corrections at step 2; exp_avg/exp_avg_sq carried over)
+    for (k, p) in cpu_model.named_parameters():
+        p.grad = None if g2[k] is None else g2[k].clone()
+    opt.step()
+    for (k, p), (kk, q) in zip(cpu_model.named_parameters(), tr.model.named_parameters()):
+        np.testing.assert_allclose(q.detach().cpu().numpy(), p.detach().numpy(), rtol=2e-6,
+                                   atol=1e-9, err_msg=f"adam step 2: {k}")
+    for k in fx.grad_none:  # torch.optim.Adam skips parameters whose grad is None
+        np.testing.assert_array_equal(dict(tr.model.named_parameters())[k].detach().cpu().numpy(),
+                                      fx.params[k].astype(np.float32), err_msg=k)
+
+
+@pytest.mark.parametrize("cin,n,h,w", [(20, 2, 1024, 1024), (20, 2, 800, 1344),
+                                       (20, 1, 1536, 2048)],
+                         ids=["bench_bs2_1024", "coco_bs2_1344x800", "supervisely_bs1_2048x1536"])
+def test_trainer_full_size_step_matches_oracle(cin, n, h, w):
+    """BASELINE configs 2, 3 (per replica, 1333x800 padded to 1344x800) and 5 (per GPU) on
+    the captured Trainer step: logits and loss against the fp64 oracle, every gradient
+    with the whole-net bars. Weights are the model's own init (weights_init,
+    segment.py:451-464) under the bench's seed; data is the bench's synthetic batch."""
+    from instancesegmentation_amd.data import device_batch
+    torch.manual_seed(1234)
+    model = Segment(cin)
+    params = _cpu_state(model)
+    xs, mask = device_batch(n, h, w, DEV, seed=100, cin=cin)
+    tr = Trainer(model, n, [tuple(x.shape) for x in xs], device=DEV).capture()
+    tr.step(xs, mask)
+    torch.cuda.synchronize()
+    assert torch.isfinite(tr.logits).all() and torch.isfinite(tr.grad_flat).all()
+    x = torch.cat([t.cpu() for t in xs], 1).numpy()
+    y = mask.cpu().numpy()
+    torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+    ref_l, ref_loss, ref_g, _ = segment_oracle.train_step(dict(params), x, y, torch.float64)
+    l32, _, g32, _ = segment_oracle.train_step(dict(params), x, y, torch.float32)
+    check_logits(tr.logits.cpu(), ref_l.numpy(), l32.numpy(), f"{n}x{h}x{w}")
+    assert abs(tr.loss() - ref_loss.item()) < 1e-5
+    none = {k for k, v in ref_g.items() if v is None}
+    check_grads(_grads_by_key(tr), ref_g, g32, none, f"{n}x{h}x{w}")

@@ -153,3 +153,13 @@ def test_bench_traffic_record_matches_dominant_op():
     assert got == by_label["dw_init_conv.layer1"]["hbm_bytes_per_launch"]
     # another configuration is not covered by the committed pass
     assert bench.pmc_traffic("dw_init_conv.layer1", types.SimpleNamespace(batch=1, cin=20, size=1024)) is None
+
+
+def test_plan_rejects_32bit_offset_overflow():
+    """The kernels address tensor elements with 32-bit offsets: a tensor of >= 2^31
+    elements (here the stem output of a 64 x 2048^2 batch) is refused at plan time."""
+    import pytest as _pytest
+    from instancesegmentation_amd.model.segment import Segment
+    from instancesegmentation_amd.train import Trainer
+    with _pytest.raises(RuntimeError, match="32-bit"):
+        Trainer(Segment(20), 64, [(64, 3, 2048, 2048), (64, 17, 2048, 2048)], device="cpu")
