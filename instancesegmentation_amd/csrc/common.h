@@ -13,6 +13,7 @@
 #include "../../include/isg.h"
 
 #define ISG_DEV __device__ __forceinline__
+#define ISG_DEV_HOST __host__ __device__ inline
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -24,6 +25,9 @@ typedef const float __attribute__((address_space(1)))* gcfloat_p;
 typedef float __attribute__((address_space(1)))* gfloat_p;
 ISG_DEV float gld(const float* p, int64_t i) { return ((gcfloat_p)p)[i]; }
 ISG_DEV void gst(float* p, int64_t i, float v) { ((gfloat_p)p)[i] = v; }
+typedef const f32x4 __attribute__((address_space(1)))* gcf32x4_p;
+// 16-B global load of 4 consecutive floats at p[i..i+3] (p + i 16-B aligned)
+ISG_DEV f32x4 gld4(const float* p, int64_t i) { return *(gcf32x4_p)((gcfloat_p)p + i); }
 
 // ---- per-channel coefficient table (LDS) -------------------------------------
 // BN_FWD : v = act((x - c0) * c1 + c2)          c0=mean  c1=gamma*rstd  c2=beta, c3=slope
