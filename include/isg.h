@@ -294,13 +294,33 @@ int32_t isg_fill_f64(double* p, int64_t n, double v, isg_stream_t stream);
 int32_t isg_mask_paste(const float* prob, int32_t K, int32_t S, const int32_t* boxes,
                        int32_t H, int32_t W, uint8_t* out, isg_stream_t stream);
 
-/* A14: per-mask count/sum/score and greedy mask-NMS (K <= 64). keep[K] receives the
+/* A14: per-mask count/sum/score and greedy mask-NMS (K <= 256). keep[K] receives the
  * kept indices in keep order, *nkeep their number (both device memory).
  * work: isg_mask_nms_workspace(K,H,W) bytes, caller-owned. */
 int64_t isg_mask_nms_workspace(int32_t K, int32_t H, int32_t W);
 int32_t isg_mask_nms(const uint8_t* masks, int32_t K, int32_t H, int32_t W, float iou_thr,
                      void* work, float* scores_out, int32_t* keep, int32_t* nkeep,
                      isg_stream_t stream);
+
+/* ---- infer pre-process ----------------------------- */
+
+/* Per-instance crop: window k = (x0,y0,x1,y1) of an HxWx3 uint8 RGB image (instance box
+ * +/- 16 px, may reach outside the image) resampled to SxS, rounded to uint8 and
+ * normalised to [-1,1] into out[K][3][S][S]; pixels outside valid[k] = (x0,y0,x1,y1)
+ * (the image minus what the centring translation moved out of the frame) read as the
+ * fill value 0. Replaces the reference's translate + CropAndPad + Resize +
+ * ToTensor/Normalize test branch (train_instance.py:139-196, :80-85; imgaug/cv2 absent:
+ * contract frozen in oracle/infer_oracle.py, bit-exact). */
+int32_t isg_instance_crop(const uint8_t* image, int32_t H, int32_t W, const int32_t* windows,
+                          const int32_t* valid, int32_t K, int32_t S, float* out,
+                          isg_stream_t stream);
+
+/* keypoint2heatmaps (train_instance.py:33-68) for K instances: keypoints[K][nparts][3] =
+ * (x, y, visible) in double, out[K][nparts][H][W] float32 (zeroed, then each visible
+ * keypoint's window written with the float32 of the double-precision Gaussian). */
+int32_t isg_keypoint_heatmaps(const double* keypoints, int32_t K, int32_t nparts, int32_t H,
+                              int32_t W, double sigma, double threshold, float* out,
+                              isg_stream_t stream);
 
 /* ---- plan executor ------------------------------------------------------ */
 

@@ -158,6 +158,10 @@ SIGNATURES = {
     "isg_mask_nms_workspace": (c_int64, [c_int32, c_int32, c_int32]),
     "isg_mask_nms": (c_int32, [c_void_p, c_int32, c_int32, c_int32, c_float, c_void_p, c_void_p,
                                c_void_p, c_void_p, c_void_p]),
+    "isg_instance_crop": (c_int32, [c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_int32,
+                                    c_int32, c_void_p, c_void_p]),
+    "isg_keypoint_heatmaps": (c_int32, [c_void_p, c_int32, c_int32, c_int32, c_int32, c_double,
+                                        c_double, c_void_p, c_void_p]),
     "isg_exec": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p]),
     "isg_exec_ms": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p]),
     "isg_last_error": (c_char_p, []),

@@ -38,12 +38,47 @@ class Conv(EngineModule):
 
     def emit(self, g, x):
         kind, slope = g.act_of(self.act)
-        return g.conv(self.conv, x, bn=self.bn, act=kind, slope=slope,
+        return g.conv(self.conv, x, bn=getattr(self, "bn", None), act=kind, slope=slope,
                       name=g.mod_names.get(id(self), "conv"))
 
     def fuseforward(self, x):
-        """segment.py:47-48 (BN already folded into conv): act(conv(x))."""
-        return _FuseForward(self)(x)
+        """segment.py:47-48 (BN already folded into conv): act(conv(x)). The traced
+        plan is cached on the module (one trace per input shape)."""
+        ff = self.__dict__.get("_ff")
+        if ff is None:
+            ff = _FuseForward(self)
+            object.__setattr__(self, "_ff", ff)  # not a submodule: no state_dict keys
+        return ff(x)
+
+    def fuse_(self):
+        """Fold the BatchNorm (eval statistics) into the conv weights and bias and drop
+        it, the yolov5-style fusion `fuseforward` presumes (segment.py:47-48):
+        W' = W * g/sqrt(v+eps) per output channel, b' = (b - m) * g/sqrt(v+eps) + beta."""
+        bn = getattr(self, "bn", None)
+        if bn is None:
+            return self
+        fold_bn_(self.conv, bn, transposed=False)
+        del self.bn
+        self._plans.clear()
+        return self
+
+
+@torch.no_grad()
+def fold_bn_(conv, bn, transposed):
+    """Fold an eval-mode BatchNorm2d into the preceding (transposed) conv, in place, in
+    double precision. Output channels: dim 0 of a Conv2d weight, dim 1 of a
+    ConvTranspose2d weight."""
+    scale = bn.weight.double() / torch.sqrt(bn.running_var.double() + bn.eps)
+    w = conv.weight.double()
+    shape = [1] * w.dim()
+    shape[1 if transposed else 0] = -1
+    conv.weight.copy_((w * scale.view(shape)).to(conv.weight.dtype))
+    b = conv.bias.double() if conv.bias is not None else torch.zeros_like(scale)
+    nb = (b - bn.running_mean.double()) * scale + bn.bias.double()
+    if conv.bias is None:
+        conv.bias = nn.Parameter(nb.to(conv.weight.dtype))
+    else:
+        conv.bias.copy_(nb.to(conv.bias.dtype))
 
 
 class _FuseForward(EngineModule):
@@ -246,7 +281,8 @@ class BottleneckUp_Res(EngineModule):
             raise NotImplementedError("uppool must be nearest x2 followed by a 1x1 conv")
         y = self.convs[0].emit(g, x)
         kind, slope = g.act_of(self.convs[3])
-        y = g.conv_transpose(self.convs[1], y, bn=self.convs[2], act=kind, slope=slope,
+        bn = self.convs[2] if isinstance(self.convs[2], nn.BatchNorm2d) else None
+        y = g.conv_transpose(self.convs[1], y, bn=bn, act=kind, slope=slope,
                              name=name + ".convT")
         y = self.convs[4].emit(g, y)
         r = self.conv2[0].emit(g, x)
@@ -355,6 +391,29 @@ class Segment(EngineModule):
         y = self.bottle5_2.emit(g, y)                                  # :501
         y = g.conv_transpose(self.bottle6_1, y, name="bottle6_1")      # :504
         return g.conv(self.bottle6_2, y, name="logits")                # :505
+
+    def fuse(self):
+        """Inference form (Conv.fuseforward, segment.py:47-48): every BatchNorm folded
+        into the conv / transposed conv in front of it, in place; the module stays in
+        eval mode (the folded weights bake the running statistics in). Returns self."""
+        self.eval()
+        for m in list(self.modules()):
+            if isinstance(m, Conv):
+                m.fuse_()
+            elif isinstance(m, BottleneckUp_Res) and isinstance(m.convs[2], nn.BatchNorm2d):
+                fold_bn_(m.convs[1], m.convs[2], transposed=True)
+                m.convs[2] = nn.Identity()
+        self.clear_plans()
+        for m in self.modules():
+            if isinstance(m, EngineModule):
+                m.clear_plans()
+        self.fused = True
+        return self
+
+    def train(self, mode=True):
+        if mode and getattr(self, "fused", False):
+            raise RuntimeError("a fused Segment (BatchNorm folded) is inference-only")
+        return super().train(mode)
 
     def train_batch(self, x, heatmaps):
         """segment.py:531-534: sigmoid(forward(cat([x, heatmaps], 1))); the concat is read

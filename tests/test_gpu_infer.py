@@ -1,0 +1,197 @@
+"""The infer product path on the MI355X (instancesegmentation_amd/infer.py):
+
+  * isg_instance_crop   bit-exact to oracle/infer_oracle.crop_instances (the build's
+                        contract for the reference's translate/crop/pad/resize test
+                        branch, train_instance.py:139-196 — imgaug/cv2 absent: parity
+                        with the reference unpinned);
+  * isg_keypoint_heatmaps bit-exact to the reference's OWN outputs
+                        (tests/golden/heatmaps.npz, train_instance.py:33-68) and to the
+                        oracle on random keypoints (out of frame, not visible);
+  * Segment.fuse()      (BN folded, Conv.fuseforward segment.py:47-48) against the
+                        unfused eval path and the fp64 oracle;
+  * InstanceSegmenter   (one HIP graph: crop -> heatmaps -> fused Segment -> sigmoid ->
+                        paste -> NMS): every stage against the oracle on the same inputs
+                        (the post-process bit-exact on the GPU's own probabilities)."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from instancesegmentation_amd import _lib as L
+from instancesegmentation_amd.model.segment import Segment
+from oracle import infer_oracle as IO
+from oracle import maskops_oracle as MO
+from oracle import segment_oracle
+from oracle.seeding import synth_params
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def stream():
+    return L.stream_ptr()
+
+
+def _crop_gpu(img, win, valid, S):
+    I = torch.from_numpy(np.ascontiguousarray(img)).to(DEV)
+    Wn = torch.from_numpy(np.asarray(win, np.int32)).to(DEV)
+    V = torch.from_numpy(np.asarray(valid, np.int32)).to(DEV)
+    K = len(win)
+    out = torch.empty((K, 3, S, S), dtype=torch.float32, device=DEV)
+    L.check(L.lib().isg_instance_crop(I.data_ptr(), img.shape[0], img.shape[1], Wn.data_ptr(),
+                                      V.data_ptr(), K, S, out.data_ptr(), stream()), "crop")
+    return out.cpu().numpy()
+
+
+def _heatmaps_gpu(kp, H, W):
+    K = kp.shape[0]
+    T = torch.from_numpy(np.ascontiguousarray(kp, np.float64)).to(DEV)
+    out = torch.full((K, kp.shape[1], H, W), 7.0, dtype=torch.float32, device=DEV)  # poisoned
+    L.check(L.lib().isg_keypoint_heatmaps(T.data_ptr(), K, kp.shape[1], H, W, 10.0, 0.01,
+                                          out.data_ptr(), stream()), "heatmaps")
+    return out.cpu().numpy()
+
+
+@pytest.mark.parametrize("S", [480, 37])
+def test_crop_bit_exact(S):
+    rng = np.random.Generator(np.random.PCG64(3))
+    H, W = 300, 410
+    img = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+    boxes = np.array([[40, 30, 200, 290], [-30, -20, 90, 150], [350, 200, 460, 330],
+                      [100, 100, 101, 101], [0, 0, W, H], [5, 5, 5, 50]], np.int64)
+    win = IO.instance_windows(boxes)
+    win[-1] = (10, 10, 10, 40)  # empty window: all fill
+    valid = IO.valid_rects(boxes, H, W)
+    ref = IO.crop_instances(img, win, valid, S)
+    got = _crop_gpu(img, win, valid, S)
+    assert np.array_equal(got, ref), np.abs(got - ref).max()
+    assert np.all(got[-1] == -1.0)
+
+
+def test_heatmaps_match_reference_golden():
+    """The reference's own keypoint2heatmaps outputs (train_instance.py:33-68): 480^2,
+    96x128 and 64x64 with keypoints on the frame edge, outside it and not visible."""
+    z = np.load(os.path.join(GOLDEN, "heatmaps.npz"))
+    cases = json.loads(str(z["meta"]))
+    for ci, case in enumerate(cases):
+        h, w = case["h"], case["w"]
+        kp = np.zeros((1, 17, 3), np.float64)
+        for j, (x, y) in case["points"].items():
+            kp[0, int(j)] = (x, y, 1.0)
+        got = _heatmaps_gpu(kp, h, w).reshape(-1)
+        ref = np.zeros(17 * h * w, np.float32)
+        ref[z[f"idx{ci}"]] = z[f"val{ci}"]
+        assert np.array_equal(got, ref), (ci, np.abs(got - ref).max(),
+                                          int((got != ref).sum()))
+
+
+def test_heatmaps_random_keypoints_match_oracle():
+    rng = np.random.Generator(np.random.PCG64(17))
+    K, S = 5, 120
+    kp = np.zeros((K, 17, 3), np.float64)
+    kp[:, :, 0] = rng.uniform(-40, S + 40, (K, 17))
+    kp[:, :, 1] = rng.uniform(-40, S + 40, (K, 17))
+    kp[:, :, 2] = (rng.uniform(size=(K, 17)) < 0.7).astype(np.float64)
+    ref = IO.instance_heatmaps(kp, S)
+    got = _heatmaps_gpu(kp, S, S)
+    assert np.array_equal(got, ref)
+
+
+def _calibrated(model_cin=20, seed=41):
+    m = Segment(model_cin)
+    shapes = [(k, tuple(v.shape)) for k, v in m.state_dict().items()]
+    params = synth_params(shapes, seed)
+    sd = m.state_dict()
+    m.load_state_dict({k: torch.as_tensor(v).to(sd[k].dtype) for k, v in params.items()})
+    return m, params
+
+
+def test_fused_eval_matches_unfused_and_oracle():
+    import copy
+    m, params = _calibrated()
+    m = m.to(DEV).eval()
+    f = copy.deepcopy(m).fuse()
+    assert not any(isinstance(x, torch.nn.BatchNorm2d) for x in f.modules())
+    from oracle.seeding import synth_batch
+    x, _ = synth_batch(2, 20, 64, 96, 8)
+    xt = torch.from_numpy(x).to(DEV)
+    with torch.no_grad():
+        a = m(xt).double().cpu()
+        b = f(xt).double().cpu()
+    ref, _ = segment_oracle.forward(params, x, train=False, dtype=torch.float64)
+    ref32, _ = segment_oracle.forward(params, x, train=False, dtype=torch.float32)
+    scale = ref.abs().max().item()
+    floor = (ref32.double() - ref).abs().max().item()
+    ea, eb = (a - ref).abs().max().item(), (b - ref).abs().max().item()
+    print(f"eval logits |max| {scale:.1f}: unfused err {ea:.2e}, fused err {eb:.2e}, "
+          f"CPU-fp32 err {floor:.2e}")
+    assert eb <= max(1e-4 * max(1.0, scale), 2.0 * floor)
+    with pytest.raises(RuntimeError):
+        f.train()
+
+
+def _scene(rng, H, W, n, dup):
+    """A crowded synthetic scene: n person boxes + keypoints, `dup` of them duplicated
+    with a few-pixel jitter (an over-complete detector's output: NMS should drop them)."""
+    img = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+    boxes, kps = [], []
+    for i in range(n):
+        cx, cy = rng.uniform(0.3, 0.7) * W, rng.uniform(0.3, 0.7) * H
+        bw, bh = rng.uniform(0.15, 0.3) * W, rng.uniform(0.3, 0.5) * H
+        b = [int(cx - bw / 2), int(cy - bh / 2), int(cx + bw / 2), int(cy + bh / 2)]
+        kp = np.zeros((17, 3))
+        kp[:, 0] = rng.uniform(b[0], b[2], 17)
+        kp[:, 1] = rng.uniform(b[1], b[3], 17)
+        kp[:, 2] = rng.uniform(size=17) < 0.8
+        boxes.append(b)
+        kps.append(kp)
+    for i in range(dup):
+        j = i % n
+        boxes.append([v + int(rng.integers(-3, 4)) for v in boxes[j]])
+        kps.append(kps[j] + np.array([rng.uniform(-2, 2), rng.uniform(-2, 2), 0.0]))
+    return img, np.asarray(boxes, np.int64), np.asarray(kps)
+
+
+def test_instance_segmenter_pipeline_matches_oracle():
+    from instancesegmentation_amd.infer import InstanceSegmenter
+    rng = np.random.Generator(np.random.PCG64(23))
+    H, W = 256, 320
+    m, params = _calibrated()
+    img, boxes, kps = _scene(rng, H, W, 4, 3)
+    eng = InstanceSegmenter(m, (H, W), max_instances=8, iou_thr=0.5)
+    masks, keep, scores = eng(img, boxes, kps)
+    n = len(boxes)
+    # stage 1: the network inputs
+    win = IO.instance_windows(boxes)
+    valid = IO.valid_rects(boxes, H, W)
+    x_ref = IO.crop_instances(img, win, valid)
+    hm_ref = IO.instance_heatmaps(IO.crop_keypoints(kps, win))
+    assert np.array_equal(eng.x[:n].cpu().numpy(), x_ref)
+    assert np.array_equal(eng.hm[:n].cpu().numpy(), hm_ref)
+    assert np.all(eng.x[n:].cpu().numpy() == -1.0)  # padded slots: empty windows
+    # stage 2: logits of the fused network against the fp64 oracle (eval, running stats)
+    xin = np.concatenate([x_ref, hm_ref], 1)
+    ref, _ = segment_oracle.forward(params, xin, train=False, dtype=torch.float64)
+    ref32, _ = segment_oracle.forward(params, xin, train=False, dtype=torch.float32)
+    got = eng.logits[:n].double().cpu()
+    err = (got - ref).abs().max().item()
+    floor = (ref32.double() - ref).abs().max().item()
+    print(f"pipeline logits err {err:.2e} (CPU-fp32 {floor:.2e}, |max| {ref.abs().max():.1f})")
+    assert err <= max(1e-4 * max(1.0, ref.abs().max().item()), 2.0 * floor)
+    # stage 3: paste + NMS bit-exact to the oracle on the GPU's own probabilities
+    prob = eng.prob[:n, 0].cpu().numpy()
+    m_ref = MO.paste_masks(prob, win, H, W)
+    assert np.array_equal(masks.cpu().numpy(), m_ref)
+    keep_ref = MO.mask_nms(m_ref, 0.5)
+    assert keep == [int(i) for i in keep_ref], (keep, keep_ref)
+    _, _, s_ref = MO.mask_stats(m_ref)
+    assert np.array_equal(scores, s_ref)
+    # a second image through the same graph (replay) agrees with a fresh eager engine
+    img2, boxes2, kps2 = _scene(rng, H, W, 5, 2)
+    masks2, keep2, _ = eng(img2, boxes2, kps2)
+    eager = InstanceSegmenter(m, (H, W), max_instances=8, iou_thr=0.5, capture=False)
+    masks3, keep3, _ = eager(img2, boxes2, kps2)
+    assert keep2 == keep3 and torch.equal(masks2, masks3)

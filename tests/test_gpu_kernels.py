@@ -490,12 +490,13 @@ def _person_probs(rng, K, S):
     return np.clip(prob, 0, 1).astype(np.float32)
 
 
-@pytest.mark.parametrize("case", ["crowded16_480_to_1024", "max64", "single", "all_empty"])
+@pytest.mark.parametrize("case", ["crowded16_480_to_1024", "max64", "max256", "single",
+                                  "all_empty"])
 def test_paste_and_nms_cases(case):
     """Config 4 (OCHuman-style crowded scene) at full size plus the edge cases: K at the
     kernel's maximum (64), one instance, and masks with no pixel above threshold. Paste
     and keep indices bit-exact to the build-defined oracle (parity with the reference
-    unpinned: it has no NMS)."""
+    unpinned: it has no NMS). max256: the kernel's instance capacity."""
     from oracle import maskops_oracle as MO
     rng = np.random.Generator(np.random.PCG64(21))
     if case == "crowded16_480_to_1024":
@@ -506,6 +507,12 @@ def test_paste_and_nms_cases(case):
         boxes = np.stack([cx - hw, cy - hh, cx + hw, cy + hh], 1).astype(np.int32)
     elif case == "max64":
         K, S, H, W, thr = 64, 32, 96, 128, 0.3
+        prob = _person_probs(rng, K, S)
+        x0, y0 = rng.integers(-10, W - 20, K), rng.integers(-10, H - 20, K)
+        boxes = np.stack([x0, y0, x0 + rng.integers(10, 60, K), y0 + rng.integers(10, 60, K)],
+                         1).astype(np.int32)
+    elif case == "max256":
+        K, S, H, W, thr = 256, 24, 120, 136, 0.4
         prob = _person_probs(rng, K, S)
         x0, y0 = rng.integers(-10, W - 20, K), rng.integers(-10, H - 20, K)
         boxes = np.stack([x0, y0, x0 + rng.integers(10, 60, K), y0 + rng.integers(10, 60, K)],

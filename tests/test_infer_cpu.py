@@ -1,0 +1,157 @@
+"""Host-side pieces of the infer path and the data reader (no GPU): the infer.py command
+line (infer.py:12-29), the common-dataset reader and filter (train_instance.py:71-226,
+dataset/transfer_coco.py:118-227), the CPU crop (same contract as the GPU kernel and the
+oracle), and BatchNorm folding (Conv.fuseforward, segment.py:47-48)."""
+import copy
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from instancesegmentation_amd import data as D
+from instancesegmentation_amd import infer as I
+from instancesegmentation_amd.model.segment import Conv, Segment
+from oracle import infer_oracle as IO
+from oracle.heatmaps_oracle import keypoint2heatmaps
+
+
+def test_infer_command_line_matches_reference():
+    a = I.parse_args(["-i", "in", "-o", "out", "--continue-test"])
+    assert (a.test_image_dir, a.output_dir, a.continue_test) == ("in", "out", True)
+    a = I.parse_args(["--test-image-dir", "x", "--output-dir", "y"])
+    assert a.continue_test is False
+    with pytest.raises(SystemExit):
+        I.parse_args(["-o", "y"])  # -i is required (infer.py:14-15)
+    assert I.path_decompose("/a/b/c.jpg") == ("/a/b", "c", "jpg")
+
+
+def test_list_images(tmp_path):
+    for n in ("a.jpg", "b.png", "c.txt", "d.jpgerr", "e.JPG"):
+        (tmp_path / n).write_bytes(b"")
+    got = [os.path.basename(p) for p in I.list_images(str(tmp_path))]
+    assert got == ["a.jpg", "b.png", "e.JPG"]
+
+
+def test_windows_and_keypoints_match_oracle():
+    boxes = np.array([[10, 20, 110, 220], [-5, 0, 40, 60]])
+    assert np.array_equal(I.instance_windows(boxes), IO.instance_windows(boxes))
+    assert np.array_equal(I.valid_rects(boxes, 300, 200), IO.valid_rects(boxes, 300, 200))
+    kp = np.random.default_rng(0).uniform(0, 200, (2, 17, 3))
+    w = I.instance_windows(boxes)
+    assert np.array_equal(I.crop_keypoints(kp, w), IO.crop_keypoints(kp, w))
+
+
+def test_cpu_crop_matches_oracle():
+    rng = np.random.default_rng(4)
+    img = rng.integers(0, 256, (90, 120, 3), dtype=np.uint8)
+    win = np.array([[-10, 5, 70, 100], [30, 30, 31, 31], [100, -20, 150, 40]])
+    valid = np.array([[0, 0, 120, 90], [0, 10, 100, 90], [5, 0, 120, 80]])
+    ref = IO.crop_instances(img, win, valid, 48)
+    for k in range(len(win)):
+        q = D.crop_resample(img, win[k], valid[k], 48).astype(np.float32)
+        x = ((q / np.float32(255.0)) - np.float32(0.5)) / np.float32(0.5)
+        assert np.array_equal(x.transpose(2, 0, 1), ref[k])
+
+
+def _write_dataset(root, rng):
+    from PIL import Image
+    os.makedirs(root / "data")
+    os.makedirs(root / "image")
+    os.makedirs(root / "instance_mask" / "a")
+    H, W = 120, 160
+    Image.fromarray(rng.integers(0, 256, (H, W, 3), dtype=np.uint8)).save(root / "image" / "a.png")
+    objs = []
+    for i, (box, nvis) in enumerate([((20, 10, 100, 110), 12), ((30, 30, 60, 60), 12),
+                                     ((10, 5, 140, 115), 8)]):
+        m = np.zeros((H, W), np.uint8)
+        m[box[1] + 5:box[3] - 5, box[0] + 5:box[2] - 5] = 255
+        Image.fromarray(m).save(root / "instance_mask" / "a" / f"{i}.png")
+        kp = {}
+        for j, name in enumerate(D.ORDER_PART_NAMES):
+            st = "vis" if j < nvis else "missing"
+            kp[name + "|sub_dict"] = {"status|keypoint_status": st,
+                                      "point|point_xy": [box[0] + 3 * j, box[1] + 4 * j]}
+        objs.append({"box|box_xyxy": list(box), "class|class": "person",
+                     "instance_mask|mask_path": f"instance_mask/a/{i}.png",
+                     "body_keypoint|sub_dict": kp})
+    with open(root / "data" / "a.json", "w") as f:
+        json.dump({"image|image_path": "image/a.png", "object|sub_list": objs}, f)
+    return H, W
+
+
+def test_common_dataset_reader(tmp_path):
+    rng = np.random.default_rng(9)
+    _write_dataset(tmp_path, rng)
+    ds = D.InstanceCommonDataset(str(tmp_path), test=True)
+    # object 1: box 30x30 (<= 50 px); object 2: 8 non-missing keypoints (<= 9)
+    assert len(ds) == 1
+    img_t, mask_t, out = ds[0]
+    assert img_t.shape == (3, 480, 480) and mask_t.shape == (1, 480, 480)
+    assert float(img_t.min()) >= -1.0 and float(img_t.max()) <= 1.0
+    assert float(mask_t.min()) >= 0.0 and float(mask_t.max()) <= 1.0 and float(mask_t.max()) > 0.9
+    assert out["heatmaps"].shape == (17, 480, 480)
+    # heatmaps: the reference rule on the projected visible keypoints
+    r = ds.results[0]
+    mb = D.mask_box(np.asarray(__import__("PIL.Image", fromlist=["Image"]).open(
+        tmp_path / "instance_mask" / "a" / "0.png")))
+    win = (mb[0] - 16, mb[1] - 16, mb[2] + 16, mb[3] + 16)
+    kp = D._keypoint_table(D.ckey(r, "body_keypoint"))
+    pts = {j: ((kp[j, 0] - win[0]) * 480 / (win[2] - win[0]),
+               (kp[j, 1] - win[1]) * 480 / (win[3] - win[1])) for j in range(17) if kp[j, 2] > 0}
+    ref = np.stack(keypoint2heatmaps(pts, (480, 480)))
+    assert np.array_equal(out["heatmaps"].numpy(), ref)
+    b = D.collate_fn([ds[0], ds[0]])
+    assert b[0].shape == (2, 3, 480, 480) and isinstance(b[2], list)
+
+
+def test_read_instances(tmp_path):
+    rng = np.random.default_rng(2)
+    _write_dataset(tmp_path, rng)
+    boxes, kps = D.read_instances(str(tmp_path / "data" / "a.json"))
+    assert boxes.shape == (3, 4) and kps.shape == (3, 17, 3)
+    assert list(boxes[0]) == [20, 10, 100, 110]
+    assert kps[0, :, 2].sum() == 12 and kps[2, :, 2].sum() == 8
+    b, k = D.read_instances(str(tmp_path / "missing.json"))
+    assert b.shape == (0, 4) and k.shape == (0, 17, 3)
+
+
+def test_bn_folding_math():
+    """conv -> BatchNorm2d(eval) -> act equals act(conv') with the folded weights, for a
+    Conv and for the ConvTranspose2d + BN of BottleneckUp_Res (CPU, torch functional)."""
+    torch.manual_seed(0)
+    c = Conv(6, 5, k=3, act=torch.nn.PReLU(5))
+    with torch.no_grad():
+        c.bn.running_mean.uniform_(-0.3, 0.3)
+        c.bn.running_var.uniform_(0.5, 2.0)
+        c.bn.weight.uniform_(0.5, 1.5)
+        c.bn.bias.uniform_(-0.2, 0.2)
+    x = torch.randn(2, 6, 9, 11, dtype=torch.float64)
+    w, b = c.conv.weight.double(), c.conv.bias.double()
+    ref = F.batch_norm(F.conv2d(x, w, b, padding=1), c.bn.running_mean.double(),
+                       c.bn.running_var.double(), c.bn.weight.double(), c.bn.bias.double(),
+                       training=False, eps=c.bn.eps)
+    f = copy.deepcopy(c).fuse_()
+    assert not hasattr(f, "bn")
+    got = F.conv2d(x, f.conv.weight.double(), f.conv.bias.double(), padding=1)
+    assert (got - ref).abs().max().item() < 1e-5
+    m = Segment(20)
+    with torch.no_grad():
+        for mod in m.modules():
+            if isinstance(mod, torch.nn.BatchNorm2d):
+                mod.running_mean.uniform_(-0.2, 0.2)
+                mod.running_var.uniform_(0.5, 2.0)
+    up = m.bottle4_1up
+    ct, bn = copy.deepcopy(up.convs[1]), copy.deepcopy(up.convs[2])
+    y = torch.randn(2, ct.in_channels, 6, 7, dtype=torch.float64)
+    ref = F.batch_norm(F.conv_transpose2d(y, ct.weight.double(), ct.bias.double(), stride=2,
+                                          padding=1),
+                       bn.running_mean.double(), bn.running_var.double(), bn.weight.double(),
+                       bn.bias.double(), training=False, eps=bn.eps)
+    m.fuse()
+    ft = m.bottle4_1up.convs[1]
+    got = F.conv_transpose2d(y, ft.weight.double(), ft.bias.double(), stride=2, padding=1)
+    assert (got - ref).abs().max().item() < 1e-5
+    assert not any(isinstance(x, torch.nn.BatchNorm2d) for x in m.modules())
