@@ -130,66 +130,78 @@ def pmc_traffic(label, args):
     return None
 
 
+def infer_scene(H, W, persons, dups, seed=11):
+    """A crowded synthetic image (BASELINE config 4, OCHuman-style): `persons` overlapping
+    person boxes with 17 keypoints each, plus `dups` near-duplicate detections (box and
+    keypoints jittered by a few pixels) that mask-NMS is expected to suppress."""
+    import numpy as np
+    rng = np.random.Generator(np.random.PCG64(seed))
+    img = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+    boxes, kps = [], []
+    for _ in range(persons):
+        cx, cy = rng.uniform(0.3, 0.7) * W, rng.uniform(0.3, 0.7) * H
+        bw, bh = rng.uniform(0.15, 0.3) * W, rng.uniform(0.35, 0.6) * H
+        b = [int(cx - bw / 2), int(cy - bh / 2), int(cx + bw / 2), int(cy + bh / 2)]
+        kp = np.zeros((17, 3))
+        kp[:, 0] = rng.uniform(b[0], b[2], 17)
+        kp[:, 1] = rng.uniform(b[1], b[3], 17)
+        kp[:, 2] = rng.uniform(size=17) < 0.8
+        boxes.append(b)
+        kps.append(kp)
+    for i in range(dups):
+        j = i % persons
+        boxes.append([v + int(rng.integers(-3, 4)) for v in boxes[j]])
+        kps.append(kps[j] + np.array([rng.uniform(-2, 2), rng.uniform(-2, 2), 0.0]))
+    return img, np.asarray(boxes), np.asarray(kps)
+
+
 def infer_bench(dev, reps=20):
     """BASELINE.json's inference half ("infer masks/sec + NMS p50") on config 4
-    (OCHuman-style crowded scene): K=16 person crops of 480x480 (RGB + 17 keypoint heatmaps,
-    the train_instance.py:139-196 test-path crop size) through Segment(20) in eval mode,
-    sigmoid, bilinear paste-back into a 1024x1024 canvas (isg_mask_paste) and greedy
-    mask-NMS at IoU 0.5 (isg_mask_nms). Boxes are drawn so most pairs overlap heavily.
-    Times the whole pipeline per image (masks/s = K / time) and the NMS alone (p50)."""
+    (OCHuman-style crowded scene): one 1024x1024 image with K=16 person instances (8 people
+    + 8 near-duplicate detections) through the infer.py product path as ONE HIP graph
+    (instancesegmentation_amd/infer.py): per-instance crop to 480x480 + 17 keypoint
+    heatmaps on the GPU, Segment(20) eval with BatchNorm folded, sigmoid, paste-back onto
+    the 1024x1024 canvas, greedy mask-NMS at IoU 0.5. masks/s = K / (graph time per
+    image, inputs resident); NMS p50 = the NMS launches alone, on the same masks."""
     import numpy as np
     from instancesegmentation_amd import _lib as L
+    from instancesegmentation_amd.infer import InstanceSegmenter
     from instancesegmentation_amd.model.segment import Segment
-    from instancesegmentation_amd.runtime import sigmoid
-    K, S, H, W = 16, 480, 1024, 1024
+    K, H, W = 16, 1024, 1024
     torch.manual_seed(99)
-    m = Segment(20).to(dev).eval()
-    rng = np.random.Generator(np.random.PCG64(11))
-    x = torch.from_numpy(rng.standard_normal((K, 20, S, S), dtype=np.float32)).to(dev)
-    cx, cy = rng.integers(420, 600, K), rng.integers(420, 600, K)
-    hw, hh = rng.integers(150, 260, K), rng.integers(200, 320, K)
-    boxes = torch.from_numpy(np.stack([cx - hw, cy - hh, cx + hw, cy + hh], 1).astype(np.int32)).to(dev)
-    out = torch.empty((K, H, W), dtype=torch.uint8, device=dev)
-    ws = L.lib().isg_mask_nms_workspace(K, H, W)
-    work = torch.empty(ws, dtype=torch.uint8, device=dev)
-    sc = torch.empty(K, dtype=torch.float32, device=dev)
-    keep = torch.empty(K, dtype=torch.int32, device=dev)
-    nk = torch.zeros(1, dtype=torch.int32, device=dev)
-    st = L.stream_ptr(dev)
-
-    def nms():
-        L.check(L.lib().isg_mask_nms(out.data_ptr(), K, H, W, 0.5, work.data_ptr(), sc.data_ptr(),
-                                     keep.data_ptr(), nk.data_ptr(), st), "mask_nms")
-
-    def pipeline():
-        with torch.no_grad():
-            prob = sigmoid(m(x))
-        L.check(L.lib().isg_mask_paste(prob.data_ptr(), K, S, boxes.data_ptr(), H, W,
-                                       out.data_ptr(), st), "mask_paste")
-        nms()
-
+    model = Segment(20)
+    img, boxes, kps = infer_scene(H, W, 8, 8)
+    eng = InstanceSegmenter(model, (H, W), max_instances=K, iou_thr=0.5, device=dev)
+    eng.load(img, boxes, kps)
     for _ in range(3):
-        pipeline()
+        eng.run()
     torch.cuda.synchronize(dev)
-    t_pipe, t_nms = [], []
+    t_pipe = []
     for _ in range(reps):
-        e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        with torch.no_grad():
-            prob = sigmoid(m(x))
-        L.check(L.lib().isg_mask_paste(prob.data_ptr(), K, S, boxes.data_ptr(), H, W,
-                                       out.data_ptr(), st), "mask_paste")
+        eng.run()
         e1.record()
-        nms()
-        e2.record()
-        e2.synchronize()
-        t_pipe.append(e0.elapsed_time(e2))
-        t_nms.append(e1.elapsed_time(e2))
+        e1.synchronize()
+        t_pipe.append(e0.elapsed_time(e1))
+    _, keep, _ = eng.result()
+    st = L.stream_ptr(dev)
+    t_nms = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        L.check(L.lib().isg_mask_nms(eng.masks.data_ptr(), K, H, W, 0.5, eng.work.data_ptr(),
+                                     eng.scores.data_ptr(), eng.keep.data_ptr(),
+                                     eng.nkeep.data_ptr(), st), "mask_nms")
+        e1.record()
+        e1.synchronize()
+        t_nms.append(e0.elapsed_time(e1))
     ms = float(np.median(t_pipe))
-    return {"metric": "infer masks/sec (Segment(20) eval 480x480 crops + paste 1024x1024 + "
-                      "mask-NMS IoU 0.5)", "masks_per_s": round(K / (ms * 1e-3), 1),
-            "ms_per_image": round(ms, 3), "nms_p50_ms": round(float(np.median(t_nms)), 4),
-            "instances": K, "kept": int(nk.item()), "config": "OCHuman-crowded synthetic, K=16",
+    return {"metric": "infer masks/sec (crop 480x480 + heatmaps + Segment(20) eval, BN folded "
+                      "+ sigmoid + paste 1024x1024 + mask-NMS IoU 0.5, one HIP graph)",
+            "masks_per_s": round(K / (ms * 1e-3), 1), "ms_per_image": round(ms, 3),
+            "nms_p50_ms": round(float(np.median(t_nms)), 4), "instances": K, "kept": len(keep),
+            "config": "OCHuman-crowded synthetic: 8 people + 8 near-duplicate detections",
             "dtype": "f32", "data": "synthetic"}
 
 

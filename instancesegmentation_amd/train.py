@@ -333,3 +333,70 @@ class Trainer:
         for (k, p), (pgo, off, n, used) in zip(self.model.named_parameters(), self._pg_views):
             out.append(self.grad_flat[off:off + n].view_as(p) if used else None)
         return out
+
+    # ---- checkpoint interchange with the reference loop (train_instance.py:320-328, :497-503)
+    def optimizer_state_dict(self):
+        """The Adam state as `torch.optim.Adam(model.parameters()).state_dict()` would hold
+        it (parameter indices in model.parameters() order; no entry for a parameter that
+        never had a gradient, like torch's lazily created state)."""
+        step = float(self.step_dev.item())
+        state = {}
+        if step > 0:
+            for i, ((k, p), (_, off, n, used)) in enumerate(zip(self.model.named_parameters(),
+                                                                self._pg_views)):
+                if not used:
+                    continue
+                state[i] = {"step": torch.tensor(step, dtype=torch.float32),
+                            "exp_avg": self.exp_avg[off:off + n].view_as(p).detach().cpu().clone(),
+                            "exp_avg_sq": self.exp_avg_sq[off:off + n].view_as(p).detach().cpu().clone()}
+        group = {"lr": self.lr, "betas": tuple(self.betas), "eps": self.eps,
+                 "weight_decay": self.wd, "amsgrad": False, "maximize": False, "foreach": None,
+                 "capturable": False, "differentiable": False, "fused": None,
+                 "decoupled_weight_decay": False,
+                 "params": list(range(len(self._pg_views)))}
+        return {"state": state, "param_groups": [group]}
+
+    def load_optimizer_state_dict(self, sd):
+        """Inverse of optimizer_state_dict; accepts the reference's saved optimizer."""
+        groups = sd["param_groups"]
+        if len(groups) != 1 or len(groups[0]["params"]) != len(self._pg_views):
+            raise ValueError("optimizer state does not match Adam(model.parameters()) of this model")
+        g = groups[0]
+        self.lr, self.betas, self.eps, self.wd = (float(g["lr"]), tuple(g["betas"]),
+                                                  float(g["eps"]), float(g["weight_decay"]))
+        steps = []
+        with torch.no_grad():
+            self.exp_avg.zero_()
+            self.exp_avg_sq.zero_()
+            params = [p for _, p in self.model.named_parameters()]
+            for i, st in sd["state"].items():
+                i = int(i)
+                _, off, n, _ = self._pg_views[i]
+                self.exp_avg[off:off + n].copy_(st["exp_avg"].reshape(-1))
+                self.exp_avg_sq[off:off + n].copy_(st["exp_avg_sq"].reshape(-1))
+                steps.append(int(float(st["step"])))
+                assert st["exp_avg"].shape == params[i].shape
+        self.step_dev.fill_(max(steps) if steps else 0)
+        self.step_count = max(steps) if steps else 0
+
+    def load_state_dict(self, sd):
+        """Model weights and buffers, copied into the flat buffers in place (the captured
+        graphs keep pointing at them)."""
+        self.model.load_state_dict(sd)
+
+    # ---- evaluation helpers (train_instance.py:394-417) -------------------------------
+    def probabilities(self):
+        """sigmoid of the last step's logits (train-mode BN), the reference's outmask_ts."""
+        out = torch.empty_like(self.logits)
+        L.check(L.lib().isg_sigmoid_fwd(self.logits.data_ptr(), out.data_ptr(), out.numel(),
+                                        L.stream_ptr(self.device)), "sigmoid")
+        return out
+
+    def predict(self, xs):
+        """model.eval(); train_batch(x, heatmaps) under no_grad (train_instance.py:395-411)."""
+        self.model.eval()
+        try:
+            with torch.no_grad():
+                return self.model.train_batch(*xs)
+        finally:
+            self.model.train()
