@@ -132,8 +132,10 @@ def pmc_traffic(label, args):
 
 def infer_scene(H, W, persons, dups, seed=11):
     """A crowded synthetic image (BASELINE config 4, OCHuman-style): `persons` overlapping
-    person boxes with 17 keypoints each, plus `dups` near-duplicate detections (box and
-    keypoints jittered by a few pixels) that mask-NMS is expected to suppress."""
+    person boxes with 17 keypoints each, plus `dups` repeated detections of the same people
+    that mask-NMS must suppress. (Repeats are exact: the random-init network's masks are
+    high-frequency textures, so a few-pixel jitter already decorrelates them below IoU
+    0.5; a trained network's blob-shaped masks would not need that.)"""
     import numpy as np
     rng = np.random.Generator(np.random.PCG64(seed))
     img = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
@@ -148,17 +150,17 @@ def infer_scene(H, W, persons, dups, seed=11):
         kp[:, 2] = rng.uniform(size=17) < 0.8
         boxes.append(b)
         kps.append(kp)
-    for i in range(dups):
+    for i in range(dups):  # repeated detections of the same people (identical prompts)
         j = i % persons
-        boxes.append([v + int(rng.integers(-3, 4)) for v in boxes[j]])
-        kps.append(kps[j] + np.array([rng.uniform(-2, 2), rng.uniform(-2, 2), 0.0]))
+        boxes.append(list(boxes[j]))
+        kps.append(kps[j].copy())
     return img, np.asarray(boxes), np.asarray(kps)
 
 
 def infer_bench(dev, reps=20):
     """BASELINE.json's inference half ("infer masks/sec + NMS p50") on config 4
     (OCHuman-style crowded scene): one 1024x1024 image with K=16 person instances (8 people
-    + 8 near-duplicate detections) through the infer.py product path as ONE HIP graph
+    + 8 repeated detections) through the infer.py product path as ONE HIP graph
     (instancesegmentation_amd/infer.py): per-instance crop to 480x480 + 17 keypoint
     heatmaps on the GPU, Segment(20) eval with BatchNorm folded, sigmoid, paste-back onto
     the 1024x1024 canvas, greedy mask-NMS at IoU 0.5. masks/s = K / (graph time per
@@ -171,6 +173,22 @@ def infer_bench(dev, reps=20):
     torch.manual_seed(99)
     model = Segment(20)
     img, boxes, kps = infer_scene(H, W, 8, 8)
+    # BatchNorm running statistics calibrated on the scene's own instances (one train-mode
+    # pass with momentum 1: running = batch statistics), so the eval-mode network of the
+    # random-init weights is well conditioned and its masks are not all-empty / all-full
+    calib = InstanceSegmenter(model, (H, W), max_instances=K, device=dev, capture=False)
+    calib.load(img, boxes, kps)
+    calib.run()
+    model = model.to(dev).train()
+    bns = [m for m in model.modules() if isinstance(m, torch.nn.BatchNorm2d)]
+    for b in bns:
+        b.momentum = 1.0
+    with torch.no_grad():
+        model(calib.x[:len(boxes)].contiguous(), calib.hm[:len(boxes)].contiguous())
+    for b in bns:
+        b.momentum = 0.1
+    model.eval()
+    del calib
     eng = InstanceSegmenter(model, (H, W), max_instances=K, iou_thr=0.5, device=dev)
     eng.load(img, boxes, kps)
     for _ in range(3):
@@ -184,7 +202,8 @@ def infer_bench(dev, reps=20):
         e1.record()
         e1.synchronize()
         t_pipe.append(e0.elapsed_time(e1))
-    _, keep, _ = eng.result()
+    masks, keep, scores = eng.result()
+    nonempty = int((scores > 0).sum())
     st = L.stream_ptr(dev)
     t_nms = []
     for _ in range(reps):
@@ -201,7 +220,9 @@ def infer_bench(dev, reps=20):
                       "+ sigmoid + paste 1024x1024 + mask-NMS IoU 0.5, one HIP graph)",
             "masks_per_s": round(K / (ms * 1e-3), 1), "ms_per_image": round(ms, 3),
             "nms_p50_ms": round(float(np.median(t_nms)), 4), "instances": K, "kept": len(keep),
-            "config": "OCHuman-crowded synthetic: 8 people + 8 near-duplicate detections",
+            "nonempty_masks": nonempty,
+            "config": "OCHuman-crowded synthetic: 8 people + 8 repeated detections; "
+                      "random-init Segment(20), BN statistics calibrated on the scene",
             "dtype": "f32", "data": "synthetic"}
 
 
