@@ -79,3 +79,160 @@ def check_grads(got, ref64, ref32, none_keys, tag="", full_size=False):
         print(f"{tag}: GPU/fp32-reference error ratio median {med:.2f}, "
               f"p90 {ratios[int(0.9 * len(ratios))]:.2f}, max {ratios[-1]:.2f}")
         assert med <= 1.5, f"{tag}: systematic gradient error (median ratio {med:.2f})"
+
+
+# ---- activation ties ---------------------------------------------------------------------
+# ReLU / PReLU have a discontinuous derivative at 0. A pre-activation within the fp32
+# rounding band of 0 (|x| of a few 1e-6 at the fixture sizes: ~1e5-1e6 activations, fp32
+# pre-activation error ~1e-5 after the BN stack) takes either branch in a correct fp32
+# implementation, and the branch decides whether that pixel's whole gradient passes
+# (one pixel of a 4-channel 16x16 layer moves the BN gradients upstream of it by ~5e-3 of
+# their scale). The fp64 oracle is then ambiguous: `resolve_ties` finds the branch choices
+# at such ties that the GPU's gradients follow, and returns the oracle's gradients
+# recomputed EXACTLY under those choices (plus the fp32 reference under the same branches,
+# so the fp32 floor measures rounding only). Candidates are restricted to elements inside
+# twice the measured fp32 error band of their own activation site, and a flip is accepted
+# only if it explains most of its own effect, so a kernel bug cannot hide behind it.
+
+
+class _ActTap:
+    """Stand-in for torch.nn.functional inside oracle.segment_oracle: relu/prelu calls are
+    numbered in call order (sites), their inputs/outputs kept (graph retained); `branches`
+    (site -> bool tensor) forces the derivative branch (True = the x>0 branch) without
+    changing the forward value."""
+
+    def __init__(self, branches=None):
+        self.sites = []
+        self.branches = branches
+
+    def __getattr__(self, name):
+        return getattr(torch.nn.functional, name)
+
+    def relu(self, x):
+        return self._act(x, None)
+
+    def prelu(self, x, w):
+        return self._act(x, w)
+
+    def _act(self, x, w):
+        import torch.nn.functional as F
+        i = len(self.sites)
+        pos = x.detach() > 0
+        out = F.relu(x) if w is None else F.prelu(x, w)
+        if self.branches is not None:
+            br = self.branches[i]
+            if not torch.equal(br, pos):
+                lo = 0.0 if w is None else (w.detach().view(1, -1, 1, 1) if w.numel() > 1
+                                            else w.detach().reshape(()))
+                d_nat = torch.where(pos, torch.ones_like(x), lo * torch.ones_like(x))
+                d_br = torch.where(br, torch.ones_like(x), lo * torch.ones_like(x))
+                out = out + (x - x.detach()) * (d_br - d_nat).detach()
+        if out.requires_grad:
+            out.retain_grad()
+        self.sites.append((x, out, w))
+        return out
+
+
+def _oracle_pass(params, x, target, dtype, branches=None):
+    """The oracle's train step (oracle.segment_oracle.train_step) with the activation tap
+    installed and the graph kept: (grads by key, tap, P)."""
+    from oracle import segment_oracle as O
+    P = {}
+    for k, v in params.items():
+        t = torch.as_tensor(np.asarray(v))
+        P[k] = t.to(dtype) if t.is_floating_point() else t.clone()
+        if k.endswith(("weight", "bias")):
+            P[k].requires_grad_(True)
+    tap = _ActTap(branches)
+    saved = O.F
+    O.F = tap
+    try:
+        logits = O.segment_forward(O.Ctx(P, train=True), torch.as_tensor(x).to(dtype))
+        loss = O.bce_loss(torch.sigmoid(logits), torch.as_tensor(target).to(dtype))
+        loss.backward(retain_graph=True)
+    finally:
+        O.F = saved
+    grads = {k: (t.grad.detach().clone() if t.grad is not None else None)
+             for k, t in P.items() if t.requires_grad}
+    return grads, tap, P
+
+
+def resolve_ties(params, x, target, got, band=2.0, tag=""):
+    """(ref64, ref32, number of resolved ties): gradient dicts for the GPU gradients `got` at (params, x, target),
+    with activation ties resolved to the branches the GPU took (module comment above)."""
+    g64, tap64, P64 = _oracle_pass(params, x, target, torch.float64)
+    nat = [(xx.detach() > 0) for xx, _, _ in tap64.sites]
+    g32, tap32, _ = _oracle_pass(params, x, target, torch.float32, branches=nat)
+    keys = [k for k in g64 if g64[k] is not None and k in got and got[k] is not None
+            and not dead_bias(k)]
+    scale = {k: max(g64[k].abs().max().item(), 1e-12) for k in keys}
+    resid = {k: (_t(got[k]) - g64[k]) / scale[k] for k in keys}
+    # candidates: elements inside `band` x the site's own fp32 error band
+    cands = []
+    for s, ((x64, o64, w), (x32, _, _)) in enumerate(zip(tap64.sites, tap32.sites)):
+        e = (x64.detach() - x32.detach().double()).abs().max().item()
+        idx = torch.nonzero(x64.detach().abs().reshape(-1) < band * e).reshape(-1)
+        for j in idx.tolist():
+            cands.append((s, j))
+    params_t = [P64[k] for k in keys]
+    deltas = []
+    for s, j in cands:
+        x64, o64, w = tap64.sites[s]
+        go = o64.grad.reshape(-1)[j].item()  # dL/d(activation output) at the element
+        xv = x64.detach().reshape(-1)[j].item()
+        if w is None:
+            lo = 0.0
+        else:
+            c = (j // (x64.shape[2] * x64.shape[3])) % x64.shape[1]
+            lo = w.detach().reshape(-1)[c if w.numel() > 1 else 0].item()
+        dd = (lo - 1.0) if xv > 0 else (1.0 - lo)  # d(new branch) - d(natural branch)
+        v = torch.zeros_like(x64).reshape(-1)
+        v[j] = go * dd
+        gr = torch.autograd.grad(x64, params_t, grad_outputs=v.view_as(x64),
+                                 retain_graph=True, allow_unused=True)
+        deltas.append({k: (g / scale[k] if g is not None else None) for k, g in zip(keys, gr)})
+
+    def sq(d):
+        return sum((v * v).sum().item() for v in d.values() if v is not None)
+
+    chosen = []
+    r2 = sq(resid)
+    while True:
+        best = None
+        for i, d in enumerate(deltas):
+            if i in chosen:
+                continue
+            dn = sq(d)
+            if dn == 0.0:
+                continue
+            nr = sum(((resid[k] - d[k]) ** 2).sum().item() if d[k] is not None
+                     else (resid[k] ** 2).sum().item() for k in keys)
+            if nr < r2 - 0.5 * dn and (best is None or nr < best[1]):
+                best = (i, nr)
+        if best is None:
+            break
+        i, r2 = best
+        chosen.append(i)
+        resid = {k: resid[k] - (deltas[i][k] if deltas[i][k] is not None else 0) for k in keys}
+    print(f"{tag}: {len(cands)} activation elements inside {band}x the fp32 error band, "
+          f"{len(chosen)} resolved to the GPU's branch "
+          f"{[(cands[i][0], round(tap64.sites[cands[i][0]][0].detach().reshape(-1)[cands[i][1]].item(), 8)) for i in chosen]}")
+    if not chosen:
+        return g64, g32, 0
+    br = [b.clone() for b in nat]
+    for i in chosen:
+        s, j = cands[i]
+        br[s].view(-1)[j] = ~br[s].view(-1)[j]
+    r64, _, _ = _oracle_pass(params, x, target, torch.float64, branches=br)
+    r32, _, _ = _oracle_pass(params, x, target, torch.float32, branches=br)
+    return r64, r32, len(chosen)
+
+
+def reference_grads(params, x, target, got, fixture=None, tag=""):
+    """(ref64, ref32) for check_grads: the reference's own fixture gradients when no
+    activation tie needs resolving, else the oracle's under the GPU's branch choices."""
+    r64, r32, n = resolve_ties(params, x, target, got, tag=tag)
+    if n == 0 and fixture is not None:
+        return ({k: torch.from_numpy(fixture.grad(k).copy()) for k in fixture.param_names},
+                {k: torch.from_numpy(fixture.grad(k, "grad32").copy()) for k in fixture.param_names})
+    return r64, r32
