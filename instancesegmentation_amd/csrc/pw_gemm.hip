@@ -264,7 +264,374 @@ __global__ __launch_bounds__(kThreads) void pw_kernel(PwArgs a) {
     sinks_finalize(a.out);
 }
 
+// ---- pwx: whole-K slab kernel (the path every aligned layer takes) ----------------------
+// The chunked kernel above serialises one load round trip per 32-channel chunk behind a
+// barrier, with 4-B loads: at 64 pixels x 32 channels per trip the 1x1 layers ran at
+// 0.3-0.5 TB/s. This variant moves the whole problem of a workgroup into LDS at once:
+//   * the BM x K weight slice (16-B loads along whichever of m / k is contiguous) and the
+//     K x BP activation slab (16-B loads, lane = 4 consecutive pixels of one channel, the
+//     producer's BatchNorm/activation or BatchNorm-backward applied on the way in), with
+//     up to 8 loads per lane in flight per batch;
+//   * then one branch-free MFMA loop over K. The A fragment is read 4 k-steps at a time
+//     with one ds_read_b128: MFMA step j of k-group g gives lane slot kk the channel
+//     16g + 4kk + j, for A and B alike (a permutation of the reduction order only).
+// Bank layout: As row stride = 8 mod 64 floats (conflict-free b128 fragment reads), Xs row
+// stride = 16 mod 32 (conflict-free b32 B reads).
+constexpr int kPxMaxLds = 160 * 1024 - 256;  // + the static LDS of sinks_finalize
+
+struct PwxArgs {
+    isg_vtensor src;
+    isg_sinks out;
+    const float* w;
+    int rs, cs;
+    int HW, M, K, Kp, BM, AS, XS;
+    int off_k, off_ri, off_a, off_x;  // dynamic LDS byte offsets (tabA at 0)
+    int wmode;                        // 1: f32x4 along k (forward), 2: f32x4 along m (dgrad)
+    int fast;                         // every record is plain loads (finalised BN coefficients)
+    int64_t P;
+};
+
+// Phases (each a single memory round trip; loads are never behind a branch, see stage.h):
+//   1. per-channel coefficient + per-row sink loads, the BM x K weight slice (<= 8 x 16 B
+//      per lane, clamped duplicates past the end) and the LDS addressing table;
+//   2. barrier; the K x BP activation slab (<= 8 x 16 B per lane, + the saved forward
+//      output when HY), while phase-1 results are written to LDS;
+//   3. the producer transform on the way into Xs; 4. MFMA; 5. epilogue with its sink
+//      operands (saved y / old value) loaded for all accumulator elements at once.
+template <int TPW, int BP, bool HY>
+__global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
+    extern __shared__ f32x4 pwx_smem[];
+    char* const smem = reinterpret_cast<char*>(pwx_smem);
+    ChSrc* const tabA = reinterpret_cast<ChSrc*>(smem);  // kThreads entries (clamped past K)
+    ChanCoef* const tabK = reinterpret_cast<ChanCoef*>(smem + a.off_k);
+    RowInfo* const ri = reinterpret_cast<RowInfo*>(smem + a.off_ri);
+    float* const As = reinterpret_cast<float*>(smem + a.off_a);
+    float* const Xs = reinterpret_cast<float*>(smem + a.off_x);
+    constexpr int QPR = BP / 4;          // pixel quads per channel row
+    constexpr int CPP = kThreads / QPR;  // channel rows per staging pass
+    constexpr int CT = BP / 16;          // pixel tiles
+    constexpr int XU = 8, WU = 8;        // activation / weight loads per lane
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = wave_id();
+    const int kk = lane >> 4, pl = lane & 15;
+    const int BM = a.BM, K = a.K, Kp = a.Kp, AS = a.AS, XS = a.XS;
+    const int m0 = blockIdx.y * BM;
+    const int Mb = min(BM, a.M - m0);
+    const int64_t p0 = (int64_t)blockIdx.x * BP;
+    const float* __restrict__ w = a.w;
+    STAMP(0);
+
+    if (!a.fast) {  // fp64 evaluation from the statistics (eval / direct ABI calls)
+        for (int c = tid; c < K; c += kThreads) tabK[c] = vt_coef(a.src, c);
+        for (int r = tid; r < Mb; r += kThreads) {
+            const SinkRow q = sink_row(a.out, m0 + r, a.HW);
+            RowInfo& d = ri[r];
+            d.p = q.p; d.y = q.y; d.ns = (int)q.ns; d.yns = (int)q.yns;
+            d.mode = q.mode; d.act = q.act; d.bias = q.bias; d.f = q.f;
+        }
+    }
+    // ---- phase 1 ------------------------------------------------------------------------
+    const VtSel vs = vt_sel(a.src);
+    const SkSel ks = sk_sel(a.out);
+    const int tc = min(tid, K - 1);
+    const CoefLoad cfl = coef_issue(vs, tc);
+    const int trow = min(tid, Mb - 1);
+    const SinkLoad skl = sink_issue(ks, m0 + trow, w);
+    f32x4 wv[WU];
+    {
+        const int kq = Kp / 4, mq = BM / 4;
+        const int nq = BM * kq;  // == mq * Kp
+#pragma unroll
+        for (int u = 0; u < WU; ++u) {
+            const int i = min(tid + u * kThreads, nq - 1);
+            // forward: (m, k4) with k contiguous; dgrad: (k, m4) with m contiguous
+            const int m1 = i / kq, k1 = (i - m1 * kq) * 4;
+            const int k2 = i / mq, m2 = (i - k2 * mq) * 4;
+            const int64_t o1 = (int64_t)(m0 + min(m1, Mb - 1)) * a.rs + min(k1, K - 4);
+            const int64_t o2 = (int64_t)min(k2, K - 1) * a.cs + m0 + min(m2, Mb - 4);
+            wv[u] = gld4(w, a.wmode == 1 ? o1 : o2);
+        }
+    }
+    tabA[tid] = ch_addr(vs, tc, a.HW);
+    __syncthreads();
+    STAMP(1);
+
+    // ---- phase 2: activation slab loads -------------------------------------------------
+    const int q = tid % QPR, cr = tid / QPR;
+    const int64_t pg = p0 + 4 * q;
+    const bool pv = pg < a.P;
+    const int n = pv ? (int)(pg / a.HW) : 0;
+    const int pix = pv ? (int)(pg - (int64_t)n * a.HW) : 0;
+    f32x4 xv[XU], yv[XU];
+#pragma unroll
+    for (int u = 0; u < XU; ++u) {
+        const ChSrc t = tabA[min(cr + u * CPP, K - 1)];
+        xv[u] = gld4(t.p, (int64_t)n * t.ns + pix);
+        if (HY) yv[u] = gld4(t.y, (int64_t)n * t.yns + pix);
+    }
+    // phase-1 results -> LDS (waits for phase-1 loads only)
+    if (a.fast) {
+        if (tid < K) tabK[tid] = coef_finish(vs, tid, cfl);
+        if (tid < Mb) {
+            const SinkRow sq = sink_finish(ks, m0 + tid, a.HW, skl);
+            RowInfo& d = ri[tid];
+            d.p = sq.p; d.y = sq.y; d.ns = (int)sq.ns; d.yns = (int)sq.yns;
+            d.mode = sq.mode; d.act = sq.act; d.bias = sq.bias; d.f = sq.f;
+        }
+    }
+    if (tid >= Mb && tid < BM) ri[tid].mode = -1;
+    {
+        const int kq = Kp / 4, mq = BM / 4;
+        const int nq = BM * kq;
+#pragma unroll
+        for (int u = 0; u < WU; ++u) {
+            const int i = tid + u * kThreads;
+            if (i < nq) {
+                if (a.wmode == 1) {
+                    const int m = i / kq, k4 = (i - m * kq) * 4;
+                    const bool ok = m < Mb && k4 < K;
+                    *reinterpret_cast<f32x4*>(&As[m * AS + k4]) = ok ? wv[u] : f32x4{0.f, 0.f, 0.f, 0.f};
+                } else {
+                    const int k = i / mq, m4 = (i - k * mq) * 4;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        As[(m4 + e) * AS + k] = (k < K && m4 + e < Mb) ? wv[u][e] : 0.f;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    STAMP(2);
+
+    // ---- phase 3: producer transform into Xs[k][p] --------------------------------------
+#pragma unroll
+    for (int u = 0; u < XU; ++u) {
+        const int c = cr + u * CPP;
+        if (c < Kp) {
+            f32x4 o = {0.f, 0.f, 0.f, 0.f};
+            if (c < K && pv) {
+                const ChSrc t = tabA[c];
+                const ChanCoef k = tabK[c];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) o[e] = ch_xform(t.xf, t.act, k, xv[u][e], HY ? yv[u][e] : xv[u][e]);
+            }
+            *reinterpret_cast<f32x4*>(&Xs[c * XS + 4 * q]) = o;
+        }
+    }
+    __syncthreads();
+    STAMP(3);
+
+    // ---- phase 4: MFMA, tile t = wave + 4i -> row tile t / CT, pixel tile t % CT ---------
+    const int nt = (BM / 16) * CT;
+    int aoff[TPW], boff[TPW];
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) {
+        const int t = min(wave + 4 * i, nt - 1);  // surplus tiles recompute the last one
+        aoff[i] = ((t / CT) * 16 + pl) * AS + 4 * kk;
+        boff[i] = (4 * kk) * XS + (t % CT) * 16 + pl;
+    }
+    f32x4 acc[TPW];
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int g = 0; g < Kp; g += 16) {
+        f32x4 a4[TPW];
+#pragma unroll
+        for (int i = 0; i < TPW; ++i) a4[i] = *reinterpret_cast<const f32x4*>(&As[aoff[i] + g]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int i = 0; i < TPW; ++i) {
+                const float bv = Xs[boff[i] + (g + j) * XS];
+                acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[i][j], bv, acc[i], 0, 0, 0);
+            }
+    }
+    STAMP(4);
+
+    // ---- phase 5: epilogue; lane holds D[row = rt*16 + kk*4 + r][pixel = ct*16 + pl] ----
+    // sink operands first (saved forward output for ACTBWD, old value for ACCUM), all in
+    // flight together; other rows load a dummy word
+    float pre[TPW][4];
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) {
+        const int t = min(wave + 4 * i, nt - 1);
+        const int rt = t / CT, ct = t % CT;
+        const int64_t pe = p0 + ct * 16 + pl;
+        const bool pve = pe < a.P;
+        const int ne = pve ? (int)(pe / a.HW) : 0;
+        const int pixe = pve ? (int)(pe - (int64_t)ne * a.HW) : 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const RowInfo& qi = ri[rt * 16 + kk * 4 + r];
+            const float* src = w;
+            int64_t off = 0;
+            if (qi.mode == ISG_SINK_ACTBWD) { src = qi.y; off = (int64_t)ne * qi.yns + pixe; }
+            if (qi.mode == ISG_SINK_ACCUM) { src = qi.p; off = (int64_t)ne * qi.ns + pixe; }
+            if (!pve) { src = w; off = 0; }
+            pre[i][r] = gld(src, off);
+        }
+    }
+    const bool need_red = sinks_need_red(a.out);
+    float (*red)[3][kMaxBM] = reinterpret_cast<float (*)[3][kMaxBM]>(Xs);
+    if (need_red) {
+        __syncthreads();  // every wave is past its Xs reads
+        for (int i = tid; i < 4 * 3 * kMaxBM; i += kThreads) (&red[0][0][0])[i] = 0.f;
+        __syncthreads();
+    }
+    STAMP(5);
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) {
+        const int t = wave + 4 * i;
+        if (t >= nt) continue;  // wave-uniform
+        const int rt = t / CT, ct = t % CT;
+        if (rt * 16 >= Mb) continue;
+        const int64_t pe = p0 + ct * 16 + pl;
+        const bool pve = pe < a.P;
+        const int ne = pve ? (int)(pe / a.HW) : 0;
+        const int pixe = pve ? (int)(pe - (int64_t)ne * a.HW) : 0;
+        float s0[4], s1[4], s2[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            s0[r] = s1[r] = s2[r] = 0.f;
+            const int rl = rt * 16 + kk * 4 + r;
+            const RowInfo& qi = ri[rl];
+            if (!pve || qi.mode < 0 || qi.mode == ISG_SINK_NONE) continue;
+            float v = acc[i][r];
+            const int64_t off = (int64_t)ne * qi.ns + pixe;
+            if (qi.mode == ISG_SINK_STORE) {
+                v += qi.bias;
+                gst(qi.p, off, v);
+                s0[r] = v;
+                s1[r] = v * v;
+            } else if (qi.mode == ISG_SINK_ACCUM) {
+                gst(qi.p, off, pre[i][r] + v);
+                s0[r] = v;
+                s1[r] = v * v;
+            } else {
+                const float y = pre[i][r];
+                const float z = (y - qi.f.mean) * qi.f.scale + qi.f.beta;
+                float gv = v;
+                if (qi.act == ISG_ACT_RELU) {
+                    gv = z > 0.f ? v : 0.f;
+                } else if (qi.act == ISG_ACT_PRELU) {
+                    gv = z > 0.f ? v : v * qi.f.slope;
+                    s2[r] = z > 0.f ? 0.f : z * v;
+                }
+                gst(qi.p, off, gv);
+                s0[r] = gv;
+                s1[r] = gv * (y - qi.f.mean);
+            }
+        }
+        if (need_red) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float t0 = row16_sum(s0[r]);
+                const float t1 = row16_sum(s1[r]);
+                const float t2 = row16_sum(s2[r]);
+                const int rl = rt * 16 + kk * 4 + r;
+                if (pl == 0 && rl < Mb) {
+                    red[wave][0][rl] += t0;
+                    red[wave][1][rl] += t1;
+                    red[wave][2][rl] += t2;
+                }
+            }
+        }
+    }
+    if (need_red) {
+        __syncthreads();
+        STAMP(6);
+        for (int rl = tid; rl < Mb; rl += kThreads) {
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+                red[0][j][rl] = ((red[0][j][rl] + red[1][j][rl]) + red[2][j][rl]) + red[3][j][rl];
+            sink_row_flush(a.out, m0 + rl, red[0][0][rl], red[0][1][rl], red[0][2][rl]);
+        }
+    }
+    sinks_finalize(a.out);
+    STAMP(7);
+}
+
+int pwx_align16(int v) { return (v + 15) & ~15; }
+
+int pwx_min_blocks() {
+    static const int v = getenv("ISG_PWX_MINB") ? atoi(getenv("ISG_PWX_MINB")) : 256;
+    return v;
+}
+
+// LDS bytes of a (BP, BM) configuration
+int pwx_lds(int K, int Kp, int BM, int BP, int& off_k, int& off_ri, int& off_a, int& off_x, int& AS,
+            int& XS) {
+    AS = Kp + ((8 - Kp % 64) + 64) % 64;
+    XS = BP + ((16 - BP % 32) + 32) % 32;  // 16 mod 32 banks
+    off_k = pwx_align16(kThreads * (int)sizeof(ChSrc));
+    off_ri = pwx_align16(off_k + K * (int)sizeof(ChanCoef));
+    off_a = pwx_align16(off_ri + BM * (int)sizeof(RowInfo));
+    off_x = pwx_align16(off_a + BM * AS * (int)sizeof(float));
+    // the epilogue's BN partials [4][3][kMaxBM] reuse the slab
+    const int xbytes = std::max(Kp * XS, 4 * 3 * kMaxBM) * (int)sizeof(float);
+    return off_x + xbytes;
+}
+
+template <int TPW, int BP, bool HY>
+int32_t pwx_launch(const PwxArgs& a, dim3 grid, int lds, hipStream_t st) {
+    auto k = pwx_kernel<TPW, BP, HY>;
+    static bool attr = false;
+    if (!attr) {
+        if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, kPxMaxLds) != hipSuccess)
+            return isg_check_launch("pwx_kernel: dynamic LDS");
+        attr = true;
+    }
+    hipLaunchKernelGGL(k, grid, dim3(kThreads), lds, st, a);
+    return isg_check_launch("pwx_kernel");
+}
+
+template <int BP, bool HY>
+int32_t pwx_dispatch(const PwxArgs& a, dim3 grid, int lds, int tpw, hipStream_t st) {
+    switch (tpw) {
+        case 1: return pwx_launch<1, BP, HY>(a, grid, lds, st);
+        case 2: return pwx_launch<2, BP, HY>(a, grid, lds, st);
+        case 3: return pwx_launch<3, BP, HY>(a, grid, lds, st);
+        case 4: return pwx_launch<4, BP, HY>(a, grid, lds, st);
+        case 5: case 6: return pwx_launch<6, BP, HY>(a, grid, lds, st);
+        default: return pwx_launch<8, BP, HY>(a, grid, lds, st);
+    }
+}
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+// host mirrors of stage.h vt_fast / sinks_fast
+bool host_seg_fast(const isg_vseg& s) {
+    if (s.xform == ISG_XF_BN_FWD) return s.bn.coef || (!s.bn.stats && s.bn.train);
+    if (s.xform == ISG_XF_BN_BWD) return s.bn.coef != nullptr;
+    return true;
+}
+bool host_vt_fast(const isg_vtensor& v) {
+    for (int s = 0; s < v.nseg; ++s)
+        if (!host_seg_fast(v.s[s])) return false;
+    return true;
+}
+bool host_sinks_fast(const isg_sinks& sk) {
+    for (int s = 0; s < sk.nsink; ++s) {
+        const isg_sink& k = sk.s[s];
+        if (k.mode == ISG_SINK_ACTBWD && !(k.bn.coef || (!k.bn.stats && k.bn.train))) return false;
+    }
+    return true;
+}
+
+// The slab path needs every source channel row 16-B aligned (HW % 4, n_stride % 4, base).
+bool pwx_src_ok(const isg_vtensor& v, int HW) {
+    if (HW % 4) return false;
+    for (int s = 0; s < v.nseg; ++s) {
+        const isg_vseg& g = v.s[s];
+        if (!aligned16(g.p) || g.n_stride % 4) return false;
+        if (g.xform == ISG_XF_BN_BWD && g.y && (!aligned16(g.y) || g.y_n_stride % 4)) return false;
+    }
+    return true;
+}
+
 }  // namespace
+
+ISG_STAMP_ACCESSOR(isg_dbg_stamps_pw)
 
 // 1x1 stride-1 GEMM. dgrad=false: rows = Co (w[co][ci]); dgrad=true: rows = Ci.
 int32_t isg_pw_gemm(const isg_conv_geom* g, const isg_vtensor* src, const float* w,
@@ -284,6 +651,67 @@ int32_t isg_pw_gemm(const isg_conv_geom* g, const isg_vtensor* src, const float*
         return isg_set_error(ISG_ERR_UNSUPPORTED, "pw gemm: K = %d channels > %d", a.K, kMaxK);
     if (a.M > 2 * kMaxBM)
         return isg_set_error(ISG_ERR_UNSUPPORTED, "pw gemm: M = %d rows", a.M);
+    static const bool slab_off = getenv("ISG_PW_CHUNKED") != nullptr;
+    int wmode = 0;
+    if (aligned16(w)) {
+        if (!dgrad && a.K % 4 == 0) wmode = 1;
+        if (dgrad && a.M % 4 == 0) wmode = 2;
+    }
+    // measured (per-op tables, kbench): the slab kernel wins on the wide 256^2 forward
+    // layers; elsewhere its longer per-workgroup phase chain loses to the chunked kernel
+    static const bool slab_all = getenv("ISG_PW_SLAB_ALL") != nullptr;
+    const bool slab_pays = slab_all || (!dgrad && a.P >= 65536);
+    if (!slab_off && slab_pays && wmode && pwx_src_ok(*src, a.HW)) {
+        PwxArgs b{};
+        b.src = a.src; b.out = a.out; b.w = w; b.rs = a.rs; b.cs = a.cs;
+        b.HW = a.HW; b.M = a.M; b.K = a.K; b.Kp = (a.K + 15) / 16 * 16; b.P = a.P;
+        b.wmode = wmode;
+        b.fast = host_vt_fast(*src) && host_sinks_fast(*out);
+        bool hy = false;
+        for (int s = 0; s < src->nseg; ++s)
+            if (src->s[s].xform == ISG_XF_BN_BWD && src->s[s].y && src->s[s].y != src->s[s].p) hy = true;
+        // (BM, BP): rows first (fewer row blocks = fewer slab re-reads), then pixels; the
+        // first configuration that fits the LDS and the per-lane load budget (8 weight and
+        // 8 activation loads of 16 B), keeps >= 4 MFMA tiles per workgroup and gives >= 256
+        // workgroups (one per CU), else the one with the most workgroups
+        const int R = (a.M + 15) / 16;
+        int best_bp = 0, best_bm = 0, best_lds = 0;
+        int64_t best_blocks = -1;
+        bool done = false;
+        static const int env_bm = getenv("ISG_PWX_BM") ? atoi(getenv("ISG_PWX_BM")) : 0;
+        static const int env_bp = getenv("ISG_PWX_BP") ? atoi(getenv("ISG_PWX_BP")) : 0;
+        for (int bm = std::min(R, 8) * 16; bm >= 16 && !done; bm -= 16) {
+            if (env_bm && bm != env_bm) continue;
+            for (int bp : {64, 32, 16}) {
+                if (env_bp && bp != env_bp) continue;
+                if ((bm / 16) * (bp / 16) < 4 || bm * b.Kp > 8 * 4 * kThreads) continue;
+                if (b.Kp > 8 * (kThreads / (bp / 4))) continue;
+                int o0, o1, o2, o3, as, xs;
+                const int lds = pwx_lds(a.K, b.Kp, bm, bp, o0, o1, o2, o3, as, xs);
+                if (lds > kPxMaxLds) continue;
+                const int64_t blocks = ((a.P + bp - 1) / bp) * ((a.M + bm - 1) / bm);
+                if (blocks > best_blocks) {
+                    best_bp = bp; best_bm = bm; best_lds = lds; best_blocks = blocks;
+                }
+                if (blocks >= pwx_min_blocks()) { done = true; break; }
+            }
+        }
+        if (best_bp) {
+            b.BM = best_bm;
+            pwx_lds(a.K, b.Kp, best_bm, best_bp, b.off_k, b.off_ri, b.off_a, b.off_x, b.AS, b.XS);
+            const int tpw = ((best_bm / 16) * (best_bp / 16) + 3) / 4;
+            const dim3 grid((unsigned)((a.P + best_bp - 1) / best_bp), (unsigned)((a.M + best_bm - 1) / best_bm));
+            int32_t rc;
+            if (best_bp == 64) rc = hy ? pwx_dispatch<64, true>(b, grid, best_lds, tpw, st)
+                                       : pwx_dispatch<64, false>(b, grid, best_lds, tpw, st);
+            else if (best_bp == 32) rc = hy ? pwx_dispatch<32, true>(b, grid, best_lds, tpw, st)
+                                            : pwx_dispatch<32, false>(b, grid, best_lds, tpw, st);
+            else rc = hy ? pwx_dispatch<16, true>(b, grid, best_lds, tpw, st)
+                         : pwx_dispatch<16, false>(b, grid, best_lds, tpw, st);
+            if (rc == 0 && out->fin_counter) isg_fin_note_handled();
+            return rc;
+        }
+    }
     const int64_t pblocks = (a.P + kBP - 1) / kBP;
     // rows per block: up to 128, halved while that keeps more workgroups in flight
     int bm = std::min(kMaxBM, (a.M + 15) / 16 * 16);

@@ -222,6 +222,207 @@ ISG_DEV void sink_row_apply(const SinkRow& q, int n, int64_t pix, float v, float
     }
 }
 
+// ---- branch-free table construction ----------------------------------------------------
+// With finalised BatchNorm coefficients (isg_bn.coef, written by the per-layer
+// finalisation) every per-channel record is a few plain loads. The *_issue helpers issue
+// them with no control flow (a NULL pointer is replaced by an always-valid one and the
+// value discarded in *_finish), so a kernel can put them in flight together with its
+// weight and activation loads: any branch around a load makes the compiler drain the
+// whole memory queue (s_waitcnt vmcnt(0)) at the join, which serialised the first slab
+// kernels into one HBM round trip per load.
+ISG_DEV bool seg_fast(const isg_vseg& s) {
+    if (s.xform == ISG_XF_BN_FWD) return s.bn.coef || (!s.bn.stats && s.bn.train);
+    if (s.xform == ISG_XF_BN_BWD) return s.bn.coef != nullptr;
+    return true;
+}
+ISG_DEV bool vt_fast(const isg_vtensor& v) {
+    bool ok = seg_fast(v.s[0]);
+    if (v.nseg > 1) ok = ok && seg_fast(v.s[1]);
+    if (v.nseg > 2) ok = ok && seg_fast(v.s[2]);
+    return ok;
+}
+ISG_DEV bool sink_fast(const isg_sink& k) {
+    return k.mode != ISG_SINK_ACTBWD || k.bn.coef || (!k.bn.stats && k.bn.train);
+}
+ISG_DEV bool sinks_fast(const isg_sinks& sk) {
+    bool ok = sink_fast(sk.s[0]);
+    if (sk.nsink > 1) ok = ok && sink_fast(sk.s[1]);
+    if (sk.nsink > 2) ok = ok && sink_fast(sk.s[2]);
+    return ok;
+}
+
+// Per-lane segment selection must not select between kernel-argument fields directly:
+// hipcc turns "select of two kernarg loads" into "load of a selected kernarg address",
+// i.e. a per-lane global load (and a wait) for every field. The fields are first made
+// opaque scalars (readfirstlane), then selected with v_cndmask.
+ISG_DEV int sgpr_i(int v) { return __builtin_amdgcn_readfirstlane(v); }
+template <class T>
+ISG_DEV T* sgpr_p(T* p) { return uniform_ptr(p); }
+
+struct SegLite {
+    const float *p, *y, *coef, *slope;
+    int ns, yns, xf, act, bnC, C;
+};
+ISG_DEV SegLite seg_lite(const isg_vseg& g) {
+    SegLite l;
+    l.p = sgpr_p(g.p); l.y = sgpr_p(g.y); l.coef = sgpr_p((const float*)g.bn.coef);
+    l.slope = sgpr_p(g.slope);
+    l.ns = sgpr_i((int)g.n_stride); l.yns = sgpr_i((int)g.y_n_stride);
+    l.xf = sgpr_i(g.xform); l.act = sgpr_i(g.act); l.bnC = sgpr_i(g.bn.C); l.C = sgpr_i(g.C);
+    return l;
+}
+struct VtSel {
+    SegLite s0, s1, s2;
+    int nseg;
+};
+ISG_DEV VtSel vt_sel(const isg_vtensor& vt) {
+    VtSel v;
+    v.nseg = sgpr_i(vt.nseg);
+    v.s0 = seg_lite(vt.s[0]);
+    v.s1 = seg_lite(vt.s[1]);
+    v.s2 = seg_lite(vt.s[2]);
+    return v;
+}
+#define ISG_SEL3(s, f, v) ((s) == 2 ? (v).s2.f : ((s) == 1 ? (v).s1.f : (v).s0.f))
+
+struct CoefLoad {
+    f32x4 f;
+    float sl;
+};
+
+ISG_DEV int vt_seg(const VtSel vt, int c, int& cl) {
+    const int c1 = vt.nseg > 1 ? vt.s0.C : 1 << 30;
+    const int c2 = vt.nseg > 2 ? vt.s0.C + vt.s1.C : 1 << 30;
+    const int s = c >= c2 ? 2 : (c >= c1 ? 1 : 0);
+    cl = c - (s == 2 ? c2 : (s == 1 ? c1 : 0));
+    return s;
+}
+
+ISG_DEV CoefLoad coef_issue(const VtSel vt, int c) {
+    int cl;
+    const int s = vt_seg(vt, c, cl);
+    const float* coef = ISG_SEL3(s, coef, vt);
+    const float* slope = ISG_SEL3(s, slope, vt);
+    const float* p = ISG_SEL3(s, p, vt);
+    const int xf = ISG_SEL3(s, xf, vt);
+    const int bnC = ISG_SEL3(s, bnC, vt);
+    const int idx = xf == ISG_XF_BN_BWD ? bnC + cl : cl;
+    const float* cp = coef ? coef + 4 * (int64_t)idx : p;
+    const float* sp = slope ? slope + cl : p;
+    CoefLoad r;
+    r.f = f32x4{gld(cp, 0), gld(cp, 1), gld(cp, 2), gld(cp, 3)};
+    r.sl = gld(sp, 0);
+    return r;
+}
+
+ISG_DEV ChanCoef coef_finish(const VtSel vt, int c, const CoefLoad& r) {
+    int cl;
+    const int s = vt_seg(vt, c, cl);
+    const bool has_coef = ISG_SEL3(s, coef, vt) != nullptr;
+    const bool has_slope = ISG_SEL3(s, slope, vt) != nullptr;
+    const int xf = ISG_SEL3(s, xf, vt);
+    ChanCoef k = {0.f, 1.f, 0.f, 0.f};
+    if (xf == ISG_XF_BN_FWD) {
+        if (has_coef) { k.c0 = r.f[0]; k.c1 = r.f[1]; k.c2 = r.f[2]; }
+        k.c3 = has_slope ? r.sl : 0.f;
+    } else if (xf == ISG_XF_BN_BWD) {
+        k = ChanCoef{r.f[0], r.f[1], r.f[2], r.f[3]};
+    }
+    return k;
+}
+
+// addressing part of channel c (kernel arguments only, no memory access)
+ISG_DEV ChSrc ch_addr(const VtSel vt, int c, int64_t hw) {
+    int cl;
+    const int s = vt_seg(vt, c, cl);
+    ChSrc r;
+    r.p = ISG_SEL3(s, p, vt) + (int64_t)cl * hw;
+    r.ns = ISG_SEL3(s, ns, vt);
+    r.yns = ISG_SEL3(s, yns, vt);
+    r.xf = ISG_SEL3(s, xf, vt);
+    r.act = ISG_SEL3(s, act, vt);
+    const float* y = ISG_SEL3(s, y, vt);
+    r.y = (r.xf == ISG_XF_BN_BWD && y) ? y + (int64_t)cl * hw : r.p;
+    return r;
+}
+
+struct SinkLite {
+    float *p;
+    const float *y, *coef, *bias, *slope;
+    int ns, yns, mode, act, c0;
+};
+ISG_DEV SinkLite sink_lite(const isg_sink& k) {
+    SinkLite l;
+    l.p = sgpr_p(k.p); l.y = sgpr_p(k.y); l.coef = sgpr_p((const float*)k.bn.coef);
+    l.bias = sgpr_p(k.bias); l.slope = sgpr_p(k.slope);
+    l.ns = sgpr_i((int)k.n_stride); l.yns = sgpr_i((int)k.y_n_stride);
+    l.mode = sgpr_i(k.mode); l.act = sgpr_i(k.act); l.c0 = sgpr_i(k.c0);
+    return l;
+}
+struct SkSel {
+    SinkLite s0, s1, s2;
+    int nsink;
+};
+ISG_DEV SkSel sk_sel(const isg_sinks& sk) {
+    SkSel v;
+    v.nsink = sgpr_i(sk.nsink);
+    v.s0 = sink_lite(sk.s[0]);
+    v.s1 = sink_lite(sk.s[1]);
+    v.s2 = sink_lite(sk.s[2]);
+    return v;
+}
+
+struct SinkLoad {
+    f32x4 f;
+    float bias, sl;
+};
+
+ISG_DEV int sk_seg(const SkSel sk, int m, int& cl) {
+    int s = 0;
+    if (sk.nsink > 1 && m >= sk.s1.c0) s = 1;
+    if (sk.nsink > 2 && m >= sk.s2.c0) s = 2;
+    cl = m - ISG_SEL3(s, c0, sk);
+    return s;
+}
+
+// `any` is a valid global address (stands in for NULL pointers)
+ISG_DEV SinkLoad sink_issue(const SkSel sk, int m, const float* any) {
+    int cl;
+    const int s = sk_seg(sk, m, cl);
+    const float* coef = ISG_SEL3(s, coef, sk);
+    const float* bias = ISG_SEL3(s, bias, sk);
+    const float* slope = ISG_SEL3(s, slope, sk);
+    const float* cp = coef ? coef + 4 * (int64_t)cl : any;
+    const float* bp = bias ? bias + cl : any;
+    const float* sp = slope ? slope + cl : any;
+    SinkLoad r;
+    r.f = f32x4{gld(cp, 0), gld(cp, 1), gld(cp, 2), gld(cp, 3)};
+    r.bias = gld(bp, 0);
+    r.sl = gld(sp, 0);
+    return r;
+}
+
+ISG_DEV SinkRow sink_finish(const SkSel sk, int m, int64_t hw, const SinkLoad& l) {
+    int cl;
+    const int s = sk_seg(sk, m, cl);
+    SinkRow q = {};
+    float* p = ISG_SEL3(s, p, sk);
+    const float* y = ISG_SEL3(s, y, sk);
+    q.p = p ? p + (int64_t)cl * hw : nullptr;
+    q.y = y ? y + (int64_t)cl * hw : nullptr;
+    q.ns = ISG_SEL3(s, ns, sk);
+    q.yns = ISG_SEL3(s, yns, sk);
+    q.mode = ISG_SEL3(s, mode, sk);
+    q.act = ISG_SEL3(s, act, sk);
+    q.bias = ISG_SEL3(s, bias, sk) ? l.bias : 0.f;
+    q.f = SinkCoef{0.f, 1.f, 0.f, 0.f};
+    if (q.mode == ISG_SINK_ACTBWD) {
+        if (ISG_SEL3(s, coef, sk)) { q.f.mean = l.f[0]; q.f.scale = l.f[1]; q.f.beta = l.f[2]; }
+        q.f.slope = ISG_SEL3(s, slope, sk) ? l.sl : 0.f;
+    }
+    return q;
+}
+
 // Fold row m's block-reduced sums into the sink's replicated fp64 accumulators.
 ISG_DEV void sink_row_flush(const isg_sinks& sk, int m, float r0, float r1, float r2) {
     const int s = sink_of(sk, m);

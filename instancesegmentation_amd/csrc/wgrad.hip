@@ -310,6 +310,268 @@ __global__ __launch_bounds__(kThreads) void wgrad_kernel(WgArgs a) {
     STAMP(4);
 }
 
+// ---- 1x1 stride-1 weight gradient on pixel slabs (pwg) ----------------------------------
+// dW[r][c] = sum_p dy[r][p] * x[c][p]. A workgroup owns BR rows x BC columns of dW and a
+// contiguous range of 64-pixel tiles. Per tile, ALL its loads are issued together, with no
+// branch around any of them (stage.h): lane = 4 consecutive pixels of one channel row
+// (16-B loads), 16 channel rows per pass, the dy rows (BatchNorm backward rebuilt on load)
+// and the x rows (producer BatchNorm + activation) in one slab; passes past the last row
+// repeat it (L1 hits). The next tile's loads are issued before this tile's MFMAs. Both
+// MFMA operands are read 4 k-steps (pixels) at a time with ds_read_b128 (step j of pixel
+// group g gives lane slot kk pixel 16g + 4kk + j); row stride 72 floats = 8 mod 64.
+constexpr int kGTP = 64;            // pixels per tile
+constexpr int kGS = kGTP + 8;       // LDS row stride (floats)
+constexpr int kGMaxRows = 192;      // BR + BC
+
+struct PwgArgs {
+    isg_vtensor dy, x;
+    float* dw;
+    float* dbias;
+    int64_t rep_stride;
+    int nrep;
+    int HW, R, C, BR, BC, ncb;
+    int fast;   // finalised BatchNorm coefficients everywhere (stage.h vt_fast)
+    int off_k, off_x;  // byte offsets: coefficient table, slab (addressing table at 0)
+    int64_t P, ntiles, tiles_per_block;
+};
+
+template <int NU, bool HY>
+ISG_DEV void pwg_issue(const PwgArgs& a, const ChSrc* tabA, int NR, int q, int cr, int64_t tl,
+                       f32x4* v, f32x4* yv, bool& pv) {
+    const int64_t pg = tl * kGTP + 4 * q;
+    pv = pg < a.P;
+    const int n = pv ? (int)(pg / a.HW) : 0;
+    const int pix = pv ? (int)(pg - (int64_t)n * a.HW) : 0;
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+        const ChSrc t = tabA[min(cr + 16 * u, NR - 1)];
+        v[u] = gld4(t.p, (int64_t)n * t.ns + pix);
+        if (HY) yv[u] = gld4(t.y, (int64_t)n * t.yns + pix);
+    }
+}
+
+template <int TPW, int NU, bool HY>
+__global__ __launch_bounds__(kThreads) void pwg_kernel(PwgArgs a) {
+    extern __shared__ f32x4 pwg_smem[];
+    char* const smem = reinterpret_cast<char*>(pwg_smem);
+    ChSrc* const tabA = reinterpret_cast<ChSrc*>(smem);  // kThreads entries: BR dy rows, BC x rows
+    ChanCoef* const tabK = reinterpret_cast<ChanCoef*>(smem + a.off_k);
+    float* const S = reinterpret_cast<float*>(smem + a.off_x);  // [BR + BC][kGS]
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = wave_id();
+    const int kk = lane >> 4, pl = lane & 15;
+    const int rb = blockIdx.y / a.ncb, cb = blockIdx.y - rb * a.ncb;
+    const int r0 = rb * a.BR, c0 = cb * a.BC;
+    const int Rb = min(a.BR, a.R - r0), Cb = min(a.BC, a.C - c0);
+    const int BR = a.BR, NR = a.BR + a.BC;
+    const int64_t rep_off = (int64_t)((blockIdx.x + 7u * blockIdx.y) % (unsigned)a.nrep) * a.rep_stride;
+    float* const dwr = a.dw + rep_off;
+    STAMP(0);
+
+    // ---- tables: row j < BR is dy channel r0 + j, else x channel c0 + j - BR -------------
+    const int jr = min(tid, NR - 1);
+    const bool is_dy = jr < BR;
+    const int cdy = r0 + min(jr, Rb - 1), cx = c0 + min(max(jr - BR, 0), Cb - 1);
+    {
+        const VtSel vd = vt_sel(a.dy), vx = vt_sel(a.x);
+        const ChSrc ad = ch_addr(vd, cdy, a.HW), ax = ch_addr(vx, cx, a.HW);
+        const CoefLoad ld = coef_issue(vd, cdy), lx = coef_issue(vx, cx);
+        ChSrc& e = tabA[tid];  // field by field: a select of whole records goes through scratch
+        e.p = is_dy ? ad.p : ax.p; e.y = is_dy ? ad.y : ax.y;
+        e.ns = is_dy ? ad.ns : ax.ns; e.yns = is_dy ? ad.yns : ax.yns;
+        e.xf = is_dy ? ad.xf : ax.xf; e.act = is_dy ? ad.act : ax.act;
+        if (a.fast) {
+            const ChanCoef kd = coef_finish(vd, cdy, ld), kx = coef_finish(vx, cx, lx);
+            if (tid < NR)
+                tabK[tid] = ChanCoef{is_dy ? kd.c0 : kx.c0, is_dy ? kd.c1 : kx.c1, is_dy ? kd.c2 : kx.c2,
+                                     is_dy ? kd.c3 : kx.c3};
+        } else if (tid < NR) {
+            tabK[tid] = is_dy ? vt_coef(a.dy, cdy) : vt_coef(a.x, cx);
+        }
+    }
+    __syncthreads();
+    STAMP(1);
+
+    const int CTn = a.BC / 16;
+    const int nt = (BR / 16) * CTn;
+    int aoff[TPW], boff[TPW];
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) {
+        const int t = min(wave + 4 * i, nt - 1);  // surplus tiles recompute the last one
+        aoff[i] = ((t / CTn) * 16 + pl) * kGS + 4 * kk;
+        boff[i] = (BR + (t % CTn) * 16 + pl) * kGS + 4 * kk;
+    }
+    f32x4 acc[TPW];
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float bsum = 0.f;
+    const bool do_bias = a.dbias && cb == 0;
+
+    const int q = tid & 15, cr = tid >> 4;
+    const int64_t t0 = (int64_t)blockIdx.x * a.tiles_per_block;
+    const int64_t t1 = min(t0 + a.tiles_per_block, a.ntiles);
+    f32x4 v[NU], yv[NU];
+    bool pv;
+    pwg_issue<NU, HY>(a, tabA, NR, q, cr, t0, v, yv, pv);
+    for (int64_t tl = t0; tl < t1; ++tl) {
+        __syncthreads();  // previous tile's fragment reads are done
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+            const int j = cr + 16 * u;
+            if (j < NR) {
+                const bool live = pv && (j < BR ? j < Rb : j - BR < Cb);
+                f32x4 o = {0.f, 0.f, 0.f, 0.f};
+                if (live) {
+                    const ChSrc t = tabA[j];
+                    const ChanCoef k = tabK[j];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) o[e] = ch_xform(t.xf, t.act, k, v[u][e], HY ? yv[u][e] : v[u][e]);
+                }
+                *reinterpret_cast<f32x4*>(&S[j * kGS + 4 * q]) = o;
+            }
+        }
+        __syncthreads();
+        if (tl == t0) STAMP(2);
+        // next tile's loads (a clamped repeat of the last tile past the range)
+        pwg_issue<NU, HY>(a, tabA, NR, q, cr, min(tl + 1, t1 - 1), v, yv, pv);
+        if (do_bias && tid < Rb) {
+            const float* rowp = S + tid * kGS;
+            float s = 0.f;
+#pragma unroll 16
+            for (int p = 0; p < kGTP; ++p) s += rowp[p];
+            bsum += s;
+        }
+#pragma unroll
+        for (int g = 0; g < kGTP; g += 16) {
+            f32x4 a4[TPW], b4[TPW];
+#pragma unroll
+            for (int i = 0; i < TPW; ++i) {
+                a4[i] = *reinterpret_cast<const f32x4*>(&S[aoff[i] + g]);
+                b4[i] = *reinterpret_cast<const f32x4*>(&S[boff[i] + g]);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int i = 0; i < TPW; ++i)
+                    acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[i][j], b4[i][j], acc[i], 0, 0, 0);
+        }
+    }
+    STAMP(3);
+    // lane holds D[row = rt*16 + kk*4 + r][col = ct*16 + pl]
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) {
+        const int t = wave + 4 * i;
+        if (t >= nt) continue;
+        const int rt = t / CTn, ct = t % CTn;
+        const int col = ct * 16 + pl;
+        if (col >= Cb) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int row = rt * 16 + kk * 4 + r;
+            if (row < Rb) atomicAdd(&dwr[(int64_t)(r0 + row) * a.C + c0 + col], acc[i][r]);
+        }
+    }
+    if (do_bias && tid < Rb) atomicAdd(&a.dbias[rep_off + r0 + tid], bsum);
+    STAMP(4);
+}
+
+bool g_aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+bool pwg_src_ok(const isg_vtensor& v, int HW) {
+    if (HW % 4) return false;
+    for (int s = 0; s < v.nseg; ++s) {
+        const isg_vseg& g = v.s[s];
+        if (!g_aligned16(g.p) || g.n_stride % 4) return false;
+        if (g.xform == ISG_XF_BN_BWD && g.y && (!g_aligned16(g.y) || g.y_n_stride % 4)) return false;
+    }
+    return true;
+}
+
+bool pwg_has_y(const isg_vtensor& v) {
+    for (int s = 0; s < v.nseg; ++s)
+        if (v.s[s].xform == ISG_XF_BN_BWD && v.s[s].y && v.s[s].y != v.s[s].p) return true;
+    return false;
+}
+
+bool pwg_fast(const isg_vtensor& v) {
+    for (int s = 0; s < v.nseg; ++s) {
+        const isg_vseg& g = v.s[s];
+        if (g.xform == ISG_XF_BN_FWD && !(g.bn.coef || (!g.bn.stats && g.bn.train))) return false;
+        if (g.xform == ISG_XF_BN_BWD && !g.bn.coef) return false;
+    }
+    return true;
+}
+
+template <int TPW, int NU, bool HY>
+int32_t pwg_launch(const PwgArgs& a, dim3 grid, size_t lds, hipStream_t st) {
+    auto k = pwg_kernel<TPW, NU, HY>;
+    static bool attr = false;
+    if (!attr) {
+        if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024) != hipSuccess)
+            return isg_check_launch("pwg_kernel: dynamic LDS");
+        attr = true;
+    }
+    hipLaunchKernelGGL(k, grid, dim3(kThreads), lds, st, a);
+    return isg_check_launch("pwg_kernel");
+}
+
+template <int NU, bool HY>
+int32_t pwg_dispatch(const PwgArgs& a, dim3 grid, size_t lds, int tpw, hipStream_t st) {
+    switch (tpw) {
+        case 1: return pwg_launch<1, NU, HY>(a, grid, lds, st);
+        case 2: return pwg_launch<2, NU, HY>(a, grid, lds, st);
+        case 3: return pwg_launch<3, NU, HY>(a, grid, lds, st);
+        case 4: return pwg_launch<4, NU, HY>(a, grid, lds, st);
+        case 5: case 6: return pwg_launch<6, NU, HY>(a, grid, lds, st);
+        default: return pwg_launch<8, NU, HY>(a, grid, lds, st);
+    }
+}
+
+// returns 1 when launched, 0 when the shape is not for this kernel, <0 on error
+int32_t pwg_try(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, float* dw,
+                float* dbias, int64_t rep_stride, int32_t nrep, hipStream_t st) {
+    static const bool off = getenv("ISG_PWG_OFF") != nullptr;
+    if (off) return 0;
+    if (!(g->KH == 1 && g->KW == 1 && g->SH == 1 && g->SW == 1 && g->PH == 0 && g->PW == 0))
+        return 0;
+    if (g->OH != g->H || g->OW != g->W || g->Co < 2) return 0;
+    const int HW = g->H * g->W;
+    if (!pwg_src_ok(*dy, HW) || !pwg_src_ok(*x, HW)) return 0;
+    PwgArgs a{};
+    a.dy = *dy; a.x = *x; a.dw = dw; a.dbias = dbias; a.rep_stride = rep_stride; a.nrep = nrep;
+    a.HW = HW; a.R = g->Co; a.C = g->Ci;
+    a.P = (int64_t)g->N * HW;
+    a.fast = pwg_fast(*dy) && pwg_fast(*x);
+    const bool hy = pwg_has_y(*dy) || pwg_has_y(*x);
+    a.ntiles = (a.P + kGTP - 1) / kGTP;
+    int br = std::min(64, (a.R + 15) / 16 * 16);
+    int bc = std::min(kGMaxRows - br, std::min(128, (a.C + 15) / 16 * 16));
+    auto gy_of = [&](int bcv) {
+        return (int64_t)((a.R + br - 1) / br) * ((a.C + bcv - 1) / bcv);
+    };
+    // narrower column blocks while the grid would not cover the CUs
+    while (bc > 32 && a.ntiles * gy_of(bc) < 256) bc = (bc / 2 + 15) / 16 * 16;
+    a.BR = br; a.BC = bc;
+    a.ncb = (a.C + bc - 1) / bc;
+    const int64_t gy = gy_of(bc);
+    int64_t gx = std::max<int64_t>(1, 512 / gy);
+    if (gx > a.ntiles) gx = a.ntiles;
+    a.tiles_per_block = (a.ntiles + gx - 1) / gx;
+    gx = (a.ntiles + a.tiles_per_block - 1) / a.tiles_per_block;
+    a.off_k = (kThreads * (int)sizeof(ChSrc) + 15) & ~15;
+    a.off_x = (a.off_k + kGMaxRows * (int)sizeof(ChanCoef) + 15) & ~15;
+    const size_t lds = (size_t)a.off_x + (size_t)(br + bc) * kGS * sizeof(float);
+    const int tpw = ((br / 16) * (bc / 16) + 3) / 4;
+    const dim3 grid((unsigned)gx, (unsigned)gy);
+    const int passes = (br + bc + 15) / 16;
+    int32_t rc;
+    if (passes <= 4) rc = hy ? pwg_dispatch<4, true>(a, grid, lds, tpw, st) : pwg_dispatch<4, false>(a, grid, lds, tpw, st);
+    else if (passes <= 8) rc = hy ? pwg_dispatch<8, true>(a, grid, lds, tpw, st) : pwg_dispatch<8, false>(a, grid, lds, tpw, st);
+    else rc = hy ? pwg_dispatch<12, true>(a, grid, lds, tpw, st) : pwg_dispatch<12, false>(a, grid, lds, tpw, st);
+    return rc ? rc : 1;
+}
+
 int vt_channels(const isg_vtensor* v) {
     int c = 0;
     for (int i = 0; i < v->nseg; ++i) c += v->s[i].C;
@@ -331,6 +593,10 @@ int32_t isg_dense_conv_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, cons
     if (!dw) return isg_set_error(ISG_ERR_INVALID, "conv wgrad: dw is NULL");
     if (!(g->KH == 1 && g->KW == 1)) {  // narrow spatial convs: tap_wgrad.hip
         const int32_t t = isg_tap_wgrad(g, dy, x, dw, dbias, rep_stride, nrep, st);
+        if (t != 0) return t < 0 ? t : 0;
+    }
+    {
+        const int32_t t = pwg_try(g, dy, x, dw, dbias, rep_stride, nrep, st);
         if (t != 0) return t < 0 ? t : 0;
     }
     WgArgs a{};

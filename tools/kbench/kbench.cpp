@@ -13,6 +13,7 @@
 #include "../../include/isg.h"
 
 extern "C" void* isg_dbg_stamps_wgrad(void);
+extern "C" void* isg_dbg_stamps_pw(void);
 
 #define CK(x)                                                                   \
     do {                                                                        \
@@ -80,6 +81,22 @@ int main(int argc, char** argv) {
     vx.s[0].p = x; vx.s[0].n_stride = (int64_t)Ci * H * W; vx.s[0].C = Ci;
     vx.s[0].xform = ISG_XF_BN_FWD; vx.s[0].act = ISG_ACT_PRELU; vx.s[0].slope = slope;
     vx.s[0].bn = isg_bn{gam, bet, nullptr, nullptr, stats, Ci, 1, (float)(N * H * W), 1e-5f};
+    // KB_COEF=1: finalised BatchNorm coefficients (isg_bn.coef), as the training graph has them
+    if (getenv("KB_COEF")) {
+        const int Cm = std::max(Ci, Co);
+        std::vector<float> hc(8 * Cm);
+        for (int c = 0; c < Cm; ++c) {
+            float* f = &hc[4 * c];
+            f[0] = 0.1f; f[1] = 1.0f; f[2] = 0.1f; f[3] = 0.f;
+            float* b = &hc[4 * (Cm + c)];
+            b[0] = 1.0f; b[1] = -0.01f; b[2] = 0.1f; b[3] = 0.001f;
+        }
+        float* coef;
+        CK(hipMalloc(&coef, hc.size() * sizeof(float)));
+        CK(hipMemcpy(coef, hc.data(), hc.size() * sizeof(float), hipMemcpyHostToDevice));
+        vdy.s[0].bn.coef = coef; vdy.s[0].bn.C = Cm;
+        vx.s[0].bn.coef = coef; vx.s[0].bn.C = Cm;
+    }
     hipStream_t st;
     CK(hipStreamCreate(&st));
     // forward: STORE sink with BN statistics; dgrad: ACTBWD sink (BN + PReLU backward)
@@ -94,6 +111,7 @@ int main(int argc, char** argv) {
         s0.act = ISG_ACT_PRELU; s0.y = x; s0.y_n_stride = s0.n_stride; s0.slope = slope;
         s0.slope_grad = sgrad;
         s0.bn = isg_bn{gam, bet, nullptr, nullptr, ostats, Ci, 1, (float)(N * H * W), 1e-5f};
+        if (getenv("KB_COEF")) { s0.bn.coef = vx.s[0].bn.coef; s0.bn.C = vx.s[0].bn.C; }
     }
     auto run = [&]() {
         int rc;
@@ -116,13 +134,8 @@ int main(int argc, char** argv) {
     CK(hipEventSynchronize(e1));
     float ms;
     CK(hipEventElapsedTime(&ms, e0, e1));
-    if (strcmp(op, "wgrad")) {
-        printf("%s N%d Ci%d %dx%d -> Co%d %dx%d k%d s%d p%d d%d: %.2f us/launch (%d reps)\n", op, N,
-               Ci, H, W, Co, g.OH, g.OW, k, s, p, d, 1e3 * ms / reps, reps);
-        return 0;
-    }
     // stamped single launch
-    unsigned long long* sp = (unsigned long long*)isg_dbg_stamps_wgrad();
+    unsigned long long* sp = (unsigned long long*)(strcmp(op, "wgrad") ? isg_dbg_stamps_pw() : isg_dbg_stamps_wgrad());
     CK(hipMemset(sp, 0, 65536 * 8 * sizeof(unsigned long long)));
     run();
     CK(hipStreamSynchronize(st));
@@ -133,7 +146,7 @@ int main(int argc, char** argv) {
     for (int b = 0; b < 65536 && h[b * 8]; ++b) {
         nb = b + 1;
         t0 = std::min(t0, h[b * 8]);
-        tend = std::max(tend, h[b * 8 + 4]);
+        for (int k = 4; k < 8; ++k) tend = std::max(tend, h[b * 8 + k]);
     }
     if (nb == 0) {
         printf("%s N%d Ci%d %dx%d -> Co%d %dx%d k%d s%d p%d d%d: %.2f us/launch (%d reps)\n", op, N,
@@ -145,7 +158,7 @@ int main(int argc, char** argv) {
            op, N, Ci, H, W, Co, g.OH, g.OW, k, s, p, d, 1e3 * ms / reps, reps, nb,
            (tend - t0) / 100.0);
     // per-segment medians (10 ns ticks)
-    for (int seg = 0; seg < 4; ++seg) {
+    for (int seg = 0; seg < 7; ++seg) {
         std::vector<double> v;
         for (int b = 0; b < nb; ++b)
             if (h[b * 8 + seg + 1] && h[b * 8 + seg]) v.push_back((h[b * 8 + seg + 1] - h[b * 8 + seg]) / 100.0);
