@@ -38,6 +38,11 @@ def parse():
     ap.add_argument("--profile-ops", default="", help="write per-op timing table to this path")
     ap.add_argument("--eager", action="store_true", help="no HIP graph capture")
     ap.add_argument("--no-infer", action="store_true", help="skip the inference leg")
+    ap.add_argument("--input", default="keypoints", choices=("keypoints", "heatmaps"),
+                    help="what the data loader hands the step: keypoints (the 17 heatmaps "
+                         "synthesised inside the stem, SURVEY.md §8f #1) or dense heatmaps")
+    ap.add_argument("--no-dense-leg", action="store_true",
+                    help="skip the second timing with dense heatmap inputs")
     return ap.parse_args()
 
 
@@ -259,20 +264,18 @@ def cpu_baseline(args):
                       f"bs{args.batch} {args.size}x{args.size} on {threads} host threads"}
 
 
-def main():
-    args = parse()
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        raise SystemExit(launch_ranks(args))
-    world, rank, local = setup_dist(args)
-    dev = torch.device("cuda", local)
-    from instancesegmentation_amd import _lib as L
+def train_leg(args, dev, world, rank, keypoints, roofline):
+    """Time args.steps captured train steps (after args.warmup) on one input form; the
+    dominant op (per-op timing pass) is bracketed by HIP events inside every timed step
+    when `roofline`."""
     from instancesegmentation_amd.data import device_batch
     from instancesegmentation_amd.model.segment import Segment
     from instancesegmentation_amd.train import Trainer
 
     torch.manual_seed(1234)
     model = Segment(args.cin)
-    xs, mask = device_batch(args.batch, args.size, args.size, dev, seed=100 + rank, cin=args.cin)
+    xs, mask = device_batch(args.batch, args.size, args.size, dev, seed=100 + rank, cin=args.cin,
+                            keypoints=keypoints and args.cin == 20)
     in_shapes = [tuple(x.shape) for x in xs]
     trainer = Trainer(model, args.batch, in_shapes, device=dev)
     trainer.step(xs, mask)
@@ -280,7 +283,7 @@ def main():
 
     # ---- dominant op (per-op timing pass, untimed) ----------------------------------
     dom = None
-    if not args.no_roofline:
+    if roofline:
         rows = op_timing(trainer)
         if args.profile_ops and rank == 0:
             with open(args.profile_ops, "w") as f:
@@ -321,8 +324,6 @@ def main():
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
-    loss = trainer.loss()
-
     roof = None
     if ev_pairs and dom_rec is not None:
         ms = sum(a.elapsed_time(b) for a, b in ev_pairs) / len(ev_pairs)
@@ -330,21 +331,49 @@ def main():
         roof["kernel"] = f"{dom[0]}:{dom_rec.label}"
         roof["avg_ms"] = round(ms, 4)
         roof["traffic"] = pmc_traffic(dom_rec.label, args)
+    res = {"value": world * args.batch * args.steps / elapsed,
+           "ms_per_step": 1e3 * elapsed / args.steps, "loss": trainer.loss(), "roofline": roof}
+    del trainer
+    torch.cuda.synchronize()
+    return res
 
-    value = world * args.batch * args.steps / elapsed
+
+def main():
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(launch_ranks(args))
+    world, rank, local = setup_dist(args)
+    dev = torch.device("cuda", local)
+    kp = args.input == "keypoints" and args.cin == 20
+    main_leg = train_leg(args, dev, world, rank, kp, not args.no_roofline)
+    dense_leg = None
+    if kp and not args.no_dense_leg:
+        dense_leg = train_leg(args, dev, world, rank, False, False)
+
+    value = main_leg["value"]
     out = {
         "metric": "train images/sec, COCO-person 1024x1024 synthetic (Segment(20) RGB+17 "
                   "heatmaps, BCE+Adam)",
         "value": round(value, 3), "unit": "images/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+        "warmup": args.warmup, "ms_per_step": round(main_leg["ms_per_step"], 3),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-        "data": "synthetic (seeded image/heatmaps/ellipse masks resident in HBM)",
+        "data": ("synthetic, resident in HBM: seeded image + 17 keypoints per image (the "
+                 "heatmaps synthesised on the GPU inside the stem, bit-identical to "
+                 "keypoint2heatmaps) + ellipse mask" if kp else
+                 "synthetic (seeded image/heatmaps/ellipse masks resident in HBM)"),
         "config": {"workload": f"train_instance.py step, Segment({args.cin}), bs{args.batch}/GPU, "
                                f"{args.size}x{args.size}", "global_batch": world * args.batch,
                    "image_size": args.size, "parallelism": f"dp{world}",
+                   "input": "keypoints" if kp else ("heatmaps" if args.cin == 20 else "image"),
                    "execution": "eager" if args.eager else "hip-graph"},
-        "roofline": roof, "loss": round(loss, 6),
+        "roofline": main_leg["roofline"], "loss": round(main_leg["loss"], 6),
     }
+    if dense_leg is not None:
+        out["dense_heatmaps"] = {"value": round(dense_leg["value"], 3),
+                                 "ms_per_step": round(dense_leg["ms_per_step"], 3),
+                                 "loss": round(dense_leg["loss"], 6),
+                                 "input": "dense 17-channel heatmaps read from HBM "
+                                          "(train_batch(x, heatmaps))"}
     if rank == 0 and world == 1 and not args.no_infer:
         out["infer"] = infer_bench(dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -140,6 +140,11 @@ typedef struct {
     int32_t Co, OH, OW;          /* conv output */
     int32_t KH, KW, SH, SW, PH, PW, DH, DW;
     int32_t groups;              /* 1 (dense) or Ci == Co (depthwise) */
+    /* input channels of the weight tensor when the conv reads only its first Ci (0 = Ci):
+     * the keypoint stem runs the dense conv over the RGB channels of a weight
+     * [Co][w_ci][KH][KW] (isg_kp_stem below); tap_conv forward / tap_wgrad only */
+    int32_t w_ci;
+    int32_t pad_;
 } isg_conv_geom;
 
 /* Residual-block tail: out = act(sum_i term_i), term_i = vtensor channel-aligned
@@ -322,6 +327,42 @@ int32_t isg_keypoint_heatmaps(const double* keypoints, int32_t K, int32_t nparts
                               int32_t W, double sigma, double threshold, float* out,
                               isg_stream_t stream);
 
+/* ---- keypoint stem ------------------------------------ */
+
+/* The stem of Segment(20) (init_head_s4, segment.py:19-31, on cat(image, heatmaps),
+ * segment.py:531-532) with the 17 heatmaps (train_instance.py:33-68) never written to
+ * HBM: map j of image n is exp(-((x-kx)^2+(y-ky)^2)/sigma^2) (double, stored float) inside
+ * keypoint j's window [max(0,int(kx-r)), min(W-1,int(kx+r+1))) x (same in y), where it
+ * exceeds the threshold, and 0 elsewhere; keypoints[n][j] = (kx, ky, visible > 0).
+ *   fwd  : y[n][co] += sum_{j,tap} w[co][c_kp0+j][tap] * map_j   over the output pixels a
+ *          window reaches (y holds the dense conv of the first c_kp0 channels + bias);
+ *          stats (BN sum / sum^2 replicas, 4*Co doubles each) get the change of sum and
+ *          sum^2 of every changed pixel
+ *   wgrad: dw[co][c_kp0+j][tap] += sum_p dy[co][p] * map_j(tap(p)), dy a vtensor
+ *   pool : out[n][c0+j] = max_pool(map_j, k) (k x k windows, stride k)
+ * geom: the conv (Ci = the weight's input channels, Co <= 16, groups 1). */
+typedef struct {
+    const double* kp;            /* [N][nparts][3] */
+    int32_t nparts, c_kp0;
+    double sigma, threshold;
+    isg_conv_geom g;
+    const float* w;              /* fwd */
+    float* y;                    /* fwd: raw conv output [N][Co][OH][OW] */
+    int64_t y_n_stride;
+    double* stats;               /* fwd: NULL or the output's BN statistics block */
+    isg_vtensor dy;              /* wgrad */
+    float* dw;                   /* wgrad: [Co][Ci][KH][KW] (+ replicas) */
+    int64_t rep_stride;
+    int32_t nrep;
+    int32_t k;                   /* pool: window */
+    float* out;                  /* pool */
+    int64_t out_n_stride;
+} isg_kp_stem;
+
+int32_t isg_kp_stem_fwd(const isg_kp_stem* a, isg_stream_t stream);
+int32_t isg_kp_stem_wgrad(const isg_kp_stem* a, isg_stream_t stream);
+int32_t isg_kp_pool(const isg_kp_stem* a, isg_stream_t stream);
+
 /* ---- plan executor ------------------------------------------------------ */
 
 /* A recorded op list (built once per input shape by the Python planner) replayed
@@ -345,7 +386,8 @@ int32_t isg_exec_ms(const void* ops, int32_t nops, void* const* table, isg_strea
 
 /* sizeof() of the ABI structs and executor records (0 vtensor, 1 sinks, 2 conv record,
  * 3 wgrad record, 4 pool record, 5 tail, 6 tail_grad, 7 bn_update, 8 grad_final,
- * 9 bce record, 10 conv_geom, 11 bn, 12 vseg, 13 sink) so bindings can verify layouts. */
+ * 9 bce record, 10 conv_geom, 11 bn, 12 vseg, 13 sink, 14 sum_rep record, 15 kp_stem) so
+ * bindings can verify layouts. */
 int32_t isg_record_size(int32_t which);
 
 const char* isg_last_error(void);

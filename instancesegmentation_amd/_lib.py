@@ -19,7 +19,7 @@ SINK_STORE, SINK_ACCUM, SINK_ACTBWD, SINK_NONE = 0, 1, 2, 3
 MAX_SEGS = 3
 LIST_CHUNK = 32
 STAT_REP = 16     # ISG_STAT_REP: accumulator replicas (isg.h)
-ABI_VERSION = 5
+ABI_VERSION = 6
 WREP = 16         # ISG_WREP: weight-gradient replicas (isg.h)
 
 
@@ -55,7 +55,7 @@ class Sinks(Structure):
 
 class Geom(Structure):
     _fields_ = [(n, c_int32) for n in ("N", "Ci", "H", "W", "Co", "OH", "OW", "KH", "KW", "SH",
-                                       "SW", "PH", "PW", "DH", "DW", "groups")]
+                                       "SW", "PH", "PW", "DH", "DW", "groups", "w_ci", "pad_")]
 
 
 class Tail(Structure):
@@ -83,6 +83,14 @@ class GradFinal(Structure):
                 ("dconv_bias", c_void_p), ("slope_acc", c_void_p), ("dslope", c_void_p),
                 ("C", c_int32), ("train", c_int32), ("count", c_float), ("eps", c_float),
                 ("slope_stride", c_int32), ("pad_", c_int32)]
+
+
+class KpStem(Structure):
+    _fields_ = [("kp", c_void_p), ("nparts", c_int32), ("c_kp0", c_int32), ("sigma", c_double),
+                ("threshold", c_double), ("g", Geom), ("w", c_void_p), ("y", c_void_p),
+                ("y_n_stride", c_int64), ("stats", c_void_p), ("dy", VTensor), ("dw", c_void_p),
+                ("rep_stride", c_int64), ("nrep", c_int32), ("k", c_int32), ("out", c_void_p),
+                ("out_n_stride", c_int64)]
 
 
 # executor records (api.cpp)
@@ -122,10 +130,11 @@ OP_CONV_FWD, OP_CONV_DGRAD, OP_CONV_WGRAD, OP_CONVT_FWD = 1, 2, 3, 4
 OP_MAXPOOL_FWD, OP_MAXPOOL_BWD, OP_TAIL_FWD, OP_TAIL_BWD = 5, 6, 7, 8
 OP_BN_UPDATE, OP_GRAD_FINAL, OP_BCE, OP_MEMSET = 9, 10, 11, 12
 OP_SUM_REP, OP_BN_FINAL = 13, 14
+OP_KP_STEM_FWD, OP_KP_STEM_WGRAD, OP_KP_POOL = 15, 16, 17
 
 _RECORD_CHECK = [(0, VTensor), (1, Sinks), (2, ConvRec), (3, WgradRec), (4, PoolRec), (5, Tail),
                  (6, TailGrad), (7, BnUpdate), (8, GradFinal), (9, BceRec), (10, Geom), (11, Bn),
-                 (12, VSeg), (13, Sink), (14, SumRepRec)]
+                 (12, VSeg), (13, Sink), (14, SumRepRec), (15, KpStem)]
 
 # exported symbol -> (restype, argtypes)
 SIGNATURES = {
@@ -162,6 +171,9 @@ SIGNATURES = {
                                     c_int32, c_void_p, c_void_p]),
     "isg_keypoint_heatmaps": (c_int32, [c_void_p, c_int32, c_int32, c_int32, c_int32, c_double,
                                         c_double, c_void_p, c_void_p]),
+    "isg_kp_stem_fwd": (c_int32, [POINTER(KpStem), c_void_p]),
+    "isg_kp_stem_wgrad": (c_int32, [POINTER(KpStem), c_void_p]),
+    "isg_kp_pool": (c_int32, [POINTER(KpStem), c_void_p]),
     "isg_exec": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p]),
     "isg_exec_ms": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p]),
     "isg_last_error": (c_char_p, []),

@@ -61,18 +61,35 @@ static int32_t check_geom(const isg_conv_geom* g) {
     if (g->groups != 1 && !(g->groups == g->Ci && g->Ci == g->Co))
         return isg_set_error(ISG_ERR_UNSUPPORTED, "conv: groups=%d (dense or depthwise only)",
                              g->groups);
+    if (g->w_ci < 0 || (g->w_ci > 0 && (g->w_ci < g->Ci || g->groups != 1)))
+        return isg_set_error(ISG_ERR_INVALID, "conv: weight input channels %d < Ci %d", g->w_ci,
+                             g->Ci);
     return ISG_OK;
 }
+
+int32_t isg_tap_conv(const isg_conv_geom*, const isg_vtensor*, const float*, const isg_sinks*,
+                     bool, hipStream_t);
+int32_t isg_tap_wgrad(const isg_conv_geom*, const isg_vtensor*, const isg_vtensor*, float*, float*,
+                      int64_t, int32_t, hipStream_t);
+
+// a conv over the first Ci of the weight's w_ci input channels (the keypoint stem's RGB
+// part): only tap_conv / tap_wgrad index the weight with a separate channel count
+static bool partial_w(const isg_conv_geom* g) { return g->w_ci > 0 && g->w_ci != g->Ci; }
 
 extern "C" {
 
 const char* isg_last_error(void) { return g_last_error.c_str(); }
-int32_t isg_abi_version(void) { return 5; }
+int32_t isg_abi_version(void) { return 6; }
 int32_t isg_stat_replicas(void) { return ISG_STAT_REP; }
 
 int32_t isg_conv_fwd(const isg_conv_geom* g, const isg_vtensor* x, const float* w,
                      const isg_sinks* out, isg_stream_t st) {
     if (int32_t e = check_geom(g)) return e;
+    if (partial_w(g)) {
+        const int32_t t = isg_tap_conv(g, x, w, out, false, st);
+        if (t < 0) return t;
+        return t ? ISG_OK : isg_set_error(ISG_ERR_UNSUPPORTED, "conv fwd: w_ci %d != Ci %d off tap_conv", g->w_ci, g->Ci);
+    }
     if (g->groups == 1) return isg_dense_conv_fwd(g, x, w, out, st);
     return isg_depthwise_fwd(g, x, w, out, st);
 }
@@ -80,6 +97,7 @@ int32_t isg_conv_fwd(const isg_conv_geom* g, const isg_vtensor* x, const float* 
 int32_t isg_conv_dgrad(const isg_conv_geom* g, const isg_vtensor* dy, const float* w,
                        const isg_sinks* dx, isg_stream_t st) {
     if (int32_t e = check_geom(g)) return e;
+    if (partial_w(g)) return isg_set_error(ISG_ERR_UNSUPPORTED, "conv dgrad with w_ci != Ci");
     if (g->groups == 1) return isg_dense_conv_dgrad(g, dy, w, dx, st);
     return isg_depthwise_dgrad(g, dy, w, dx, st);
 }
@@ -91,6 +109,11 @@ int32_t isg_conv_wgrad_rep(const isg_conv_geom* g, const isg_vtensor* dy, const 
     if (nrep < 1 || (nrep > 1 && rep_stride <= 0))
         return isg_set_error(ISG_ERR_INVALID, "conv wgrad: bad replicas %d / stride %lld", nrep,
                              (long long)rep_stride);
+    if (partial_w(g)) {
+        const int32_t t = isg_tap_wgrad(g, dy, x, dw, dbias, rep_stride, nrep, st);
+        if (t < 0) return t;
+        return t ? ISG_OK : isg_set_error(ISG_ERR_UNSUPPORTED, "conv wgrad: w_ci %d != Ci %d off tap_wgrad", g->w_ci, g->Ci);
+    }
     if (g->groups == 1) return isg_dense_conv_wgrad(g, dy, x, dw, dbias, rep_stride, nrep, st);
     return isg_depthwise_wgrad(g, dy, x, dw, dbias, rep_stride, nrep, st);
 }
@@ -120,6 +143,9 @@ enum {
     OP_MEMSET = 12,
     OP_SUM_REP = 13,
     OP_BN_FINAL = 14,
+    OP_KP_STEM_FWD = 15,
+    OP_KP_STEM_WGRAD = 16,
+    OP_KP_POOL = 17,
 };
 
 struct ConvRec {
@@ -289,6 +315,15 @@ static int32_t run_op_raw(int32_t kind, char* buf, isg_stream_t st) {
             rc = isg_sum_replicas(r->dst, r->src, r->n, r->nrep, r->stride, st);
             break;
         }
+        case OP_KP_STEM_FWD:
+            rc = isg_kp_stem_fwd((const isg_kp_stem*)buf, st);
+            break;
+        case OP_KP_STEM_WGRAD:
+            rc = isg_kp_stem_wgrad((const isg_kp_stem*)buf, st);
+            break;
+        case OP_KP_POOL:
+            rc = isg_kp_pool((const isg_kp_stem*)buf, st);
+            break;
         case OP_MEMSET: {
             auto* r = (MemsetRec*)buf;
             if (hipMemsetAsync(r->p, 0, (size_t)r->bytes, st) != hipSuccess)
@@ -400,6 +435,7 @@ int32_t isg_record_size(int32_t which) {
         case 12: return (int32_t)sizeof(isg_vseg);
         case 13: return (int32_t)sizeof(isg_sink);
         case 14: return (int32_t)sizeof(SumRepRec);
+        case 15: return (int32_t)sizeof(isg_kp_stem);
         default: return -1;
     }
 }

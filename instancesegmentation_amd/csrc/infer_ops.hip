@@ -75,6 +75,7 @@ __global__ __launch_bounds__(kThreads) void crop_kernel(const uint8_t* __restric
 __global__ __launch_bounds__(kThreads) void heatmap_kernel(const double* __restrict__ kp, int nparts,
                                                             int H, int W, double sigma2, double thr,
                                                             double r, float* __restrict__ out) {
+#pragma clang fp contract(off)  // numpy's double arithmetic, operation for operation
     const int kpart = blockIdx.x;  // instance * nparts + part
     const double* q = kp + (int64_t)kpart * 3;
     if (!(q[2] > 0.0)) return;  // not 'vis'

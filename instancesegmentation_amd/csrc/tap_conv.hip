@@ -452,8 +452,9 @@ int32_t isg_tap_conv(const isg_conv_geom* g, const isg_vtensor* src, const float
     a.nph = dgrad ? g->SH * g->SW : 1;
     if (a.nph > kMaxPh || mx > 2) return 0;
     a.src = *src; a.out = *out; a.w = w; a.N = g->N;
-    a.wm = dgrad ? KK : (int64_t)g->Ci * KK;
-    a.wc = dgrad ? (int64_t)g->Ci * KK : KK;
+    const int64_t wci = g->w_ci > 0 ? g->w_ci : g->Ci;  // weight input channels (isg.h)
+    a.wm = dgrad ? KK : wci * KK;
+    a.wc = dgrad ? wci * KK : KK;
     a.SrcH = dgrad ? g->OH : g->H; a.SrcW = dgrad ? g->OW : g->W;
     a.DstH = dgrad ? g->H : g->OH; a.DstW = dgrad ? g->W : g->OW;
     a.OutH = dgrad ? g->H : g->OH; a.OutW = dgrad ? g->W : g->OW;

@@ -43,6 +43,7 @@ struct TwArgs {
     int64_t rep_stride;
     int nrep;
     int N, C, Co, H, W, OH, OW, KH, KW, SH, SW, PH, PW, DH, DW, KK;
+    int WC;  // the weight's input channels (isg_conv_geom.w_ci; == C but for the keypoint stem)
     int BX, tiles_x, tiles_y, ntiles;
     int HR, HCu, PS, RS, CHS, DQ;  // halo rows / units / LDS layout; dy LDS row stride
     uint32_t m_tpi, m_tx;          // magic divisors (0 = divide by 1)
@@ -228,7 +229,7 @@ __global__ __launch_bounds__(kThreads) void tap_wgrad_kernel(TwArgs a) {
         const int ci = ch * 4 + (l16 >> 2);
         if (co < a.Co && tap >= 0 && ci < a.C) {
             const float s = ((red[e] + red[16 * ncol + e]) + red[32 * ncol + e]) + red[48 * ncol + e];
-            atomicAdd(&dwr[((int64_t)co * a.C + ci) * a.KK + tap], s);
+            atomicAdd(&dwr[((int64_t)co * a.WC + ci) * a.KK + tap], s);
         }
     }
     if (a.dbias && ch == 0) {
@@ -382,6 +383,7 @@ struct TwaArgs {
     int64_t rep_stride;
     int nrep;
     int N, C, Co, H, W, OH, OW, KH, KW, PH, PW, KK;
+    int WC;  // the weight's input channels (isg_conv_geom.w_ci)
     int BX, tiles_x, tiles_y, ntiles;
     int HR, HRP, HCu, PS, RS, CHS, DQ, KPW;
     uint32_t m_tpi, m_tx, m_4bx, m_bx, m_hrp;
@@ -557,7 +559,7 @@ __global__ __launch_bounds__(kThreads, 2) void tap_wgrad_all_kernel(TwaArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int co = kq * 4 + i;
-            if (co < a.Co) atomicAdd(&dwr[((int64_t)co * a.C + ci) * a.KK + tap], acc[t][i]);
+            if (co < a.Co) atomicAdd(&dwr[((int64_t)co * a.WC + ci) * a.KK + tap], acc[t][i]);
         }
     }
     if (a.dbias) {
@@ -675,6 +677,7 @@ int32_t twa_try(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor
     if (g->Ci * KK > 16 * kTwaTiles || g->Ci * KK < 448) return 0;
     TwaArgs a{};
     a.N = g->N; a.C = g->Ci; a.Co = g->Co; a.H = g->H; a.W = g->W; a.OH = g->OH; a.OW = g->OW;
+    a.WC = g->w_ci > 0 ? g->w_ci : g->Ci;
     a.KH = g->KH; a.KW = g->KW; a.PH = g->PH; a.PW = g->PW; a.KK = KK;
     // tile width: a multiple of 4 whose halo (column pairs) fits one 32-lane half-wave
     const int bxmax = (32 * 2 - (g->KW - 1) - 1) / 2 + 1;
@@ -771,6 +774,7 @@ int32_t isg_tap_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_v
     a.rep_stride = nrep > 1 ? rep_stride : 0;
     a.nrep = nrep < 1 ? 1 : nrep;
     a.N = g->N; a.C = g->Ci; a.Co = g->Co; a.H = g->H; a.W = g->W; a.OH = g->OH; a.OW = g->OW;
+    a.WC = g->w_ci > 0 ? g->w_ci : g->Ci;
     a.KH = g->KH; a.KW = g->KW; a.SH = g->SH; a.SW = g->SW; a.PH = g->PH; a.PW = g->PW;
     a.DH = g->DH; a.DW = g->DW; a.KK = KK;
     const int mx = g->SW;

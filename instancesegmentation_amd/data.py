@@ -32,8 +32,10 @@ def keypoint_heatmaps(points, h, w, sigma=10.0, threshold=0.01):
     return maps
 
 
-def synthetic_batch(n, h, w, seed=0, with_heatmaps=True):
-    """Returns (image [n,3,h,w], heatmaps [n,17,h,w] or None, mask [n,1,h,w]) float32."""
+def synthetic_batch(n, h, w, seed=0, with_heatmaps=True, keypoints_out=None):
+    """Returns (image [n,3,h,w], heatmaps [n,17,h,w] or None, mask [n,1,h,w]) float32.
+    keypoints_out: an [n,17,3] float64 array receiving the keypoints (x, y, visible) the
+    heatmaps are drawn from (the same random stream either way)."""
     rng = np.random.Generator(np.random.PCG64(seed))
     img = rng.integers(0, 256, size=(n, 3, h, w)).astype(np.float32)
     img = (img / np.float32(255.0) - np.float32(0.5)) / np.float32(0.5)
@@ -44,17 +46,28 @@ def synthetic_batch(n, h, w, seed=0, with_heatmaps=True):
         cx, cy = rng.uniform(0.35, 0.65) * w, rng.uniform(0.35, 0.65) * h
         ax, ay = rng.uniform(0.15, 0.3) * w, rng.uniform(0.2, 0.4) * h
         mask[b, 0] = (((xx - cx) / ax) ** 2 + ((yy - cy) / ay) ** 2 <= 1.0)
-        if with_heatmaps:
+        if with_heatmaps or keypoints_out is not None:
             pts = {j: (cx + rng.uniform(-0.8, 0.8) * ax, cy + rng.uniform(-0.8, 0.8) * ay)
                    for j in range(N_PARTS) if rng.uniform() < 0.8}
-            hm[b] = keypoint_heatmaps(pts, h, w)
+            if with_heatmaps:
+                hm[b] = keypoint_heatmaps(pts, h, w)
+            if keypoints_out is not None:
+                keypoints_out[b] = 0.0
+                for j, (x, y) in pts.items():
+                    keypoints_out[b, j] = (x, y, 1.0)
     return img, hm, mask
 
 
-def device_batch(n, h, w, device, seed=0, cin=20):
-    img, hm, mask = synthetic_batch(n, h, w, seed, with_heatmaps=(cin == 20))
+def device_batch(n, h, w, device, seed=0, cin=20, keypoints=False):
+    """[image, heatmaps] (or [image, keypoints [n,17,3] float64] with keypoints=True: the
+    stem then synthesises the same heatmaps on the GPU) and the mask, on `device`."""
+    kp = np.zeros((n, N_PARTS, 3), np.float64) if keypoints else None
+    img, hm, mask = synthetic_batch(n, h, w, seed, with_heatmaps=(cin == 20 and not keypoints),
+                                    keypoints_out=kp)
     xs = [torch.from_numpy(img).to(device)]
-    if cin == 20:
+    if keypoints:
+        xs.append(torch.from_numpy(kp).to(device))
+    elif cin == 20:
         xs.append(torch.from_numpy(hm).to(device))
     return xs, torch.from_numpy(mask).to(device)
 

@@ -217,6 +217,22 @@ def cat(*vals):
     return Value(segs)
 
 
+class Keypoints:
+    """Keypoint input [N, nparts, 3] float64 = (x, y, visible > 0) of slot `slot`, standing
+    for `nparts` heatmap channels (train_instance.py:33-68) that are never materialised:
+    the stem synthesises them on the fly (isg_kp_stem, SURVEY.md §8f #1)."""
+
+    def __init__(self, slot, N, nparts, sigma=10.0, threshold=0.01):
+        self.slot, self.N, self.nparts = slot, N, nparts
+        self.sigma, self.threshold = sigma, threshold
+        self.C = nparts
+        self.grad = False
+
+    def spec(self):
+        return {"kp": Ptr(self.slot), "nparts": self.nparts, "sigma": float(self.sigma),
+                "threshold": float(self.threshold)}
+
+
 # ---------------------------------------------------------------------------------
 class Graph:
     """Forward trace of an engine module at one input shape."""
@@ -331,26 +347,44 @@ class Graph:
         check_elems(b)
         return Value([Val(b, 0, C, grad=grad)])
 
-    def conv(self, conv, x, bn=None, act="none", slope=None, name=""):
+    def keypoints(self, idx, N, nparts):
+        return Keypoints(S_IN[idx], N, nparts)
+
+    def kp_pool(self, kp, k, H, W, out, c0=0):
+        """max_pool(k) of the keypoint heatmaps of an H x W image into out[:, c0:c0+parts]."""
+        if H % k or W % k:
+            raise RuntimeError(f"max_pool{k}: {H}x{W} not divisible")
+        self.ops.append(KpPoolOp(self, kp, k, H, W, out, c0))
+        return Value([Val(out, c0, kp.nparts, grad=False)])
+
+    def conv(self, conv, x, bn=None, act="none", slope=None, name="", kp=None):
         """nn.Conv2d (dense or depthwise) on value x, optionally followed by BN/act
-        applied lazily by the consumer."""
+        applied lazily by the consumer. kp (Keypoints): the conv's input is cat(x, the
+        keypoint heatmaps); x feeds the dense conv, the heatmap channels the keypoint
+        stem kernels (isg_kp_stem)."""
         k, s, p, d = conv.kernel_size, conv.stride, conv.padding, conv.dilation
         if isinstance(p, str):
             raise NotImplementedError("string padding")
         H, W = x.H, x.W
         OH = (H + 2 * p[0] - d[0] * (k[0] - 1) - 1) // s[0] + 1
         OW = (W + 2 * p[1] - d[1] * (k[1] - 1) - 1) // s[1] + 1
-        if x.C != conv.in_channels:
-            raise RuntimeError(f"{name}: expected {conv.in_channels} input channels, got {x.C}")
+        ckp = kp.nparts if kp is not None else 0
+        if x.C + ckp != conv.in_channels:
+            raise RuntimeError(f"{name}: expected {conv.in_channels} input channels, got {x.C + ckp}")
+        if kp is not None and (conv.groups != 1 or x.grad):
+            raise NotImplementedError("keypoint stem: dense conv of an input without gradient only")
         if conv.groups not in (1, conv.in_channels) or (conv.groups > 1 and
                                                          conv.in_channels != conv.out_channels):
             raise NotImplementedError("grouped conv other than depthwise")
-        geom = dict(N=self.N, Ci=conv.in_channels, H=H, W=W, Co=conv.out_channels, OH=OH, OW=OW,
+        geom = dict(N=self.N, Ci=x.C, H=H, W=W, Co=conv.out_channels, OH=OH, OW=OW,
                     KH=k[0], KW=k[1], SH=s[0], SW=s[1], PH=p[0], PW=p[1], DH=d[0], DW=d[1],
                     groups=conv.groups)
+        if kp is not None:
+            geom["w_ci"] = conv.in_channels
         out = self.act_buf(conv.out_channels, OH, OW, name)
         bnr = self.bn_ref(bn, self.N * OH * OW) if bn is not None else None
         op = ConvOp(self, "conv", conv, geom, x, out, bnr)
+        op.kp = kp
         self.ops.append(op)
         return Value([Val(out, 0, conv.out_channels, bnr, act, slope, grad=self.need_grad)])
 
@@ -572,6 +606,13 @@ class GradState:
 class ConvOp:
     def __init__(self, g, kind, mod, geom, x, out, bnr):
         self.g, self.kind, self.mod, self.geom, self.x, self.out, self.bnr = g, kind, mod, geom, x, out, bnr
+        self.kp = None
+
+    def _kp_spec(self):
+        """isg_kp_stem fields shared by the forward and weight-gradient records."""
+        ge = dict(self.geom)
+        ge["Ci"] = ge.pop("w_ci")
+        return dict(self.kp.spec(), c_kp0=self.x.C, g=ge)
 
     def _cost(self):
         """(flops, bytes of x, bytes of y, bytes of w) — algorithmic, fp32, each read once."""
@@ -598,7 +639,7 @@ class ConvOp:
         self.fused_final = False
         if self.bnr is not None and g.train:
             sink["stats"] = Ptr(S_STATS, self.bnr.stats_off * 8)
-            if _BN_FUSE:
+            if _BN_FUSE and self.kp is None:  # the keypoint stem finishes the statistics
                 sink["fin_bn"] = bn_spec(self.bnr, True)
                 sink["fin_mode"] = 1
                 sink["_fin_ctr"] = Ptr(S_STATS, self.bnr.ctr_fwd * 8)
@@ -609,6 +650,13 @@ class ConvOp:
         kind = L.OP_CONVT_FWD if self.kind == "convT" else L.OP_CONV_FWD
         fl, xb, yb, wb = self._cost()
         ops.add(Record(kind, L.ConvRec, rec, label=self.out.name, flops=fl, nbytes=xb + yb + wb))
+        if self.kp is not None:
+            ks = dict(self._kp_spec(), w=g.tptr(self.mod, "weight"), y=self.out.ptr(),
+                      y_n_stride=self.out.n_stride)
+            if self.bnr is not None and g.train:
+                ks["stats"] = Ptr(S_STATS, self.bnr.stats_off * 8)
+            ops.add(Record(L.OP_KP_STEM_FWD, L.KpStem, ks, label="kp_" + self.out.name,
+                           nbytes=2 * yb))
 
     def bwd(self, ops, gs):
         g = self.g
@@ -659,8 +707,30 @@ class ConvOp:
                 rec["dbias"] = g.wrep_ptr(self.mod, "bias")
             ops.add(Record(L.OP_CONV_WGRAD, L.WgradRec, rec, label="dw_" + self.out.name,
                            flops=fl, nbytes=dyb + xb + wb))
+            if self.kp is not None:
+                ops.add(Record(L.OP_KP_STEM_WGRAD, L.KpStem,
+                               dict(self._kp_spec(), dy=dyv, dw=dw, **rep),
+                               label="dwkp_" + self.out.name))
         if has_bias and self.bnr is not None:
             gs.bias_from_bn.append((self.mod, self.bnr))
+
+
+class KpPoolOp:
+    """max_pool(k) of the keypoint heatmaps (segment.py:31 on the heatmap channels)."""
+
+    def __init__(self, g, kp, k, H, W, out, c0):
+        self.g, self.kp, self.k, self.H, self.W, self.out, self.c0 = g, kp, k, H, W, out, c0
+
+    def fwd(self, ops):
+        g = self.g
+        ops.add(Record(L.OP_KP_POOL, L.KpStem,
+                       dict(self.kp.spec(), g={"N": g.N, "H": self.H, "W": self.W}, k=self.k,
+                            out=self.out.ptr(self.c0), out_n_stride=self.out.n_stride),
+                       label="kp_pool_" + self.out.name,
+                       nbytes=4 * g.N * self.kp.nparts * self.out.H * self.out.W))
+
+    def bwd(self, ops, gs):
+        return  # keypoints carry no gradient
 
 
 class PoolOp:
@@ -763,7 +833,8 @@ class Plan:
     def __init__(self, owner, in_shapes, train, need_grad, in_grad):
         N = in_shapes[0][0]
         g = Graph(owner, N, train, need_grad)
-        ins = [g.input(i, s[1], s[2], s[3], in_grad[i]) for i, s in enumerate(in_shapes)]
+        ins = [g.input(i, s[1], s[2], s[3], in_grad[i]) if len(s) == 4 else
+               g.keypoints(i, s[0], s[1]) for i, s in enumerate(in_shapes)]
         outs = owner.emit(g, *ins)
         if isinstance(outs, Value):
             outs = (outs,)
@@ -875,7 +946,7 @@ class Plan:
         for i, ob in enumerate(self.out_bufs):
             gs.external[id(ob)] = Buf(S_DOUT[i], ob.N, ob.C, ob.H, ob.W, f"dout{i}")
         for i, v in enumerate(ins):
-            if v.grad:
+            if isinstance(v, Value) and v.grad:
                 b = v.segs[0].buf
                 gs.external[id(b)] = Buf(S_DIN[i], b.N, b.C, b.H, b.W, f"din{i}")
         bw = OpList()
@@ -891,10 +962,10 @@ class Plan:
                 body.add(bn_final_record(gs.pending_final, True))
                 gs.pending_final = []
         for r in body.recs:
-            if r.kind == L.OP_CONV_WGRAD:
+            if r.kind in (L.OP_CONV_WGRAD, L.OP_KP_STEM_WGRAD):
                 r.flags |= Record.OPF_SIDE  # nothing later in the list reads a weight gradient
-        self.din_written = [v.grad and bool(gs.inited.get(id(v.segs[0].buf)))
-                            for v in ins]
+        self.din_written = [isinstance(v, Value) and v.grad and
+                            bool(gs.inited.get(id(v.segs[0].buf))) for v in ins]
         # finalisation of BN / PReLU / conv-bias-before-BN gradients: (module, item)
         conv_before = {id(bnr): mod for mod, bnr in gs.bias_from_bn}
         items = []

@@ -16,7 +16,7 @@ BottleneckUp_Res_Other :338-344, Segment :347-534.
 import torch
 import torch.nn as nn
 
-from ..engine import Value, cat
+from ..engine import Keypoints, Val, Value, cat
 from ..runtime import EngineModule, sigmoid
 
 
@@ -36,10 +36,10 @@ class Conv(EngineModule):
         self.bn = nn.BatchNorm2d(c2)
         self.act = act if act else nn.Identity()
 
-    def emit(self, g, x):
+    def emit(self, g, x, kp=None):
         kind, slope = g.act_of(self.act)
         return g.conv(self.conv, x, bn=getattr(self, "bn", None), act=kind, slope=slope,
-                      name=g.mod_names.get(id(self), "conv"))
+                      name=g.mod_names.get(id(self), "conv"), kp=kp)
 
     def fuseforward(self, x):
         """segment.py:47-48 (BN already folded into conv): act(conv(x)). The traced
@@ -100,12 +100,17 @@ class init_head_s4(EngineModule):
         self.layer2 = Conv(planes, outplanes - inplanes, k=5, s=2, p=2,
                            act=nn.PReLU(outplanes - inplanes))
 
-    def emit(self, g, x):
-        cin = x.C
+    def emit(self, g, x, kp=None):
+        """kp (engine.Keypoints): the input is cat(x, heatmaps of kp) with the heatmaps
+        synthesised inside the stem kernels (SURVEY.md §8f #1) — same values, never in HBM."""
+        cin = x.C + (kp.nparts if kp is not None else 0)
         cout = self.layer2.conv.out_channels
         out = g.act_buf(cin + cout, x.H // 4, x.W // 4, "init_down")
         short = g.maxpool(x, 4, out=out, c0=0)
-        y = self.layer2.emit(g, self.layer1.emit(g, x))
+        if kp is not None:  # one segment over the pooled image and heatmap channels
+            g.kp_pool(kp, 4, x.H, x.W, out, c0=x.C)
+            short = Value([Val(out, 0, cin, grad=short.grad)])
+        y = self.layer2.emit(g, self.layer1.emit(g, x, kp=kp))
         y = g.materialize(y, out=out, c0=cin)
         return cat(short, y)
 
@@ -372,12 +377,15 @@ class Segment(EngineModule):
                     nn.init.zeros_(m.bias)
 
     def emit(self, g, x, heatmaps=None):
-        if heatmaps is not None:
+        kp = None
+        if isinstance(heatmaps, Keypoints):
+            kp = heatmaps  # heatmaps synthesised from keypoints inside the stem
+        elif heatmaps is not None:
             x = cat(x, heatmaps)                                       # segment.py:532
         if x.H % 16 or x.W % 16:
             raise RuntimeError(f"Segment needs H, W multiples of 16, got {x.H}x{x.W} "
                                "(the reference fails in torch.cat otherwise, SURVEY.md §0.5)")
-        init_down = self.init_conv.emit(g, x)                          # :472
+        init_down = self.init_conv.emit(g, x, kp=kp)                   # :472
         b1_down, b1_idx = self.bottle1_1.emit(g, init_down)            # :478
         y = _chain(g, self.bottle1_x, b1_down)                         # :479
         b2_down, b2_idx = self.bottle2_1.emit(g, y)                    # :482
@@ -417,5 +425,7 @@ class Segment(EngineModule):
 
     def train_batch(self, x, heatmaps):
         """segment.py:531-534: sigmoid(forward(cat([x, heatmaps], 1))); the concat is read
-        in place by the first kernels (two input segments), not materialised."""
+        in place by the first kernels (two input segments), not materialised. heatmaps may
+        also be the keypoints they come from, float64 [N, 17, 3] = (x, y, visible)
+        (train_instance.py:33-68): the maps are then synthesised inside the stem."""
         return sigmoid(self(x, heatmaps))

@@ -50,6 +50,17 @@ def _check_inputs(xs):
     for x in xs:
         if not isinstance(x, torch.Tensor):
             raise TypeError(f"expected a Tensor input, got {type(x).__name__}")
+        if x.dim() == 3 and out:
+            # keypoints [N, parts, 3] = (x, y, visible) standing for the heatmap channels
+            # (engine.Keypoints): float64, as the reference's keypoint2heatmaps computes
+            if x.shape[2] != 3 or x.dtype != torch.float64:
+                raise RuntimeError("keypoints: expected a float64 [N, parts, 3] tensor, got "
+                                   f"{x.dtype} {tuple(x.shape)}")
+            if x.device.type != "cuda":
+                raise RuntimeError("instancesegmentation_amd runs on the MI355X only: move the "
+                                   "model and inputs to a GPU device (there is no CPU path)")
+            out.append(x.contiguous())
+            continue
         if x.dim() != 4:
             raise RuntimeError(f"expected a 4-D NCHW input, got shape {tuple(x.shape)}")
         if x.device.type != "cuda":

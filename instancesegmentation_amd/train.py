@@ -156,7 +156,9 @@ class Trainer:
         self.exp_avg_sq = torch.zeros_like(self.flat)
         self.step_count = 0
         self.step_dev = torch.zeros(1, dtype=torch.int32, device=dev)  # Adam's step, on device
-        self.inputs = [torch.empty(s, dtype=torch.float32, device=dev) for s in self.in_shapes]
+        # 4-D: image / heatmaps (float32); 3-D: keypoints [N, parts, 3] (float64, engine.Keypoints)
+        self.inputs = [torch.empty(s, dtype=torch.float32 if len(s) == 4 else torch.float64,
+                                   device=dev) for s in self.in_shapes]
         self.target = torch.empty(self.plan.out_shapes[0], dtype=torch.float32, device=dev)
         self.table = self._make_table()
         self.graphs = None

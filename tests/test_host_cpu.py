@@ -163,3 +163,32 @@ def test_plan_rejects_32bit_offset_overflow():
     from instancesegmentation_amd.train import Trainer
     with _pytest.raises(RuntimeError, match="32-bit"):
         Trainer(Segment(20), 64, [(64, 3, 2048, 2048), (64, 17, 2048, 2048)], device="cpu")
+
+
+def test_keypoint_stem_plan_and_synthetic_keypoints():
+    """Segment(20) traced on (image, keypoints [N,17,3]): the stem's heatmap channels go to
+    the keypoint records (pool, forward fix, weight gradient), the dense conv reads only the
+    image with the weight's 20 input channels (w_ci), and the keypoints the synthetic batch
+    reports redraw exactly its heatmaps."""
+    import numpy as np
+    from instancesegmentation_amd import _lib as L
+    from instancesegmentation_amd.data import N_PARTS, keypoint_heatmaps, synthetic_batch
+    from instancesegmentation_amd.engine import Plan
+    m = Segment(20)
+    p = Plan(m, [(2, 3, 64, 64), (2, 17, 3)], True, True, (False, False))
+    kinds = [r.kind for r in p.fwd.recs]
+    assert kinds.count(L.OP_KP_POOL) == 1 and kinds.count(L.OP_KP_STEM_FWD) == 1
+    bk = [r for r in p.bwd.recs if r.kind == L.OP_KP_STEM_WGRAD]
+    assert len(bk) == 1 and bk[0].flags & 1  # forked onto the side stream like any wgrad
+    conv = next(r for r in p.fwd.recs if r.label == "init_conv.layer1")
+    g = L.ConvRec.from_buffer_copy(conv.body).g
+    assert (g.Ci, g.w_ci) == (3, 20)
+    dense = Plan(m, [(2, 3, 64, 64), (2, 17, 64, 64)], True, True, (False, False))
+    assert p.act_size == dense.act_size and p.graph.pgrad_size == dense.graph.pgrad_size
+    kp = np.zeros((2, N_PARTS, 3))
+    _, hm, mask = synthetic_batch(2, 96, 64, seed=7)
+    _, none, mask2 = synthetic_batch(2, 96, 64, seed=7, with_heatmaps=False, keypoints_out=kp)
+    assert none is None and np.array_equal(mask, mask2)
+    for b in range(2):
+        pts = {j: (kp[b, j, 0], kp[b, j, 1]) for j in range(N_PARTS) if kp[b, j, 2] > 0}
+        assert np.array_equal(keypoint_heatmaps(pts, 96, 64), hm[b])
