@@ -50,6 +50,7 @@ struct KpArgs {
     float* out;
     int64_t out_ns;
     int tiles_x, FH, FW;
+    int dbg;  // ablation bits (ISG_KP_DBG, experiments only): 1 no maps, 2 no MACs, 4 no apply, 8 exit after the ballot
 };
 
 struct Win {
@@ -88,8 +89,11 @@ ISG_DEV int ceil_div(int a, int b) { return -floor_div(-a, b); }
 
 // ---- forward: add the heatmap channels' contribution to the raw conv output -----------
 __global__ __launch_bounds__(kThreads) void kp_fwd_kernel(KpArgs a) {
-    __shared__ float wl[kMaxWl];  // [Co][active slot][KK]
+    // weights of the active parts' channels, [slot][tap][16 co] (co past Co zero): one
+    // broadcast ds_read_b128 per 4 output channels
+    __shared__ f32x4 wl[kMaxWl / 4];
     __shared__ float hl[kMaxFoot * kMaxFoot];
+    __shared__ int toff[kMaxKK];
     __shared__ Win wins[kMaxParts];
     __shared__ uint32_t act_mask;
     __shared__ float red[2][4][kMaxCo];
@@ -111,46 +115,60 @@ __global__ __launch_bounds__(kThreads) void kp_fwd_kernel(KpArgs a) {
     }
     __syncthreads();
     uint32_t mask = act_mask;
-    if (!mask) return;  // block-uniform: no window reaches this tile
-    const int nact = __popc(mask);
-    // weights of the active parts' channels: wl[(co * nact + s) * KK + tap]
+    if (!mask || (a.dbg & 8)) return;  // block-uniform: no window reaches this tile
+    const int KK = a.KK;
     {
+        float* const wf = reinterpret_cast<float*>(wl);
         int s = 0;
         for (uint32_t m = mask; m; m &= m - 1, ++s) {
             const int j = __ffs(m) - 1;
-            for (int i = tid; i < a.Co * a.KK; i += kThreads) {
-                const int co = i / a.KK, tap = i - co * a.KK;
-                wl[(co * nact + s) * a.KK + tap] =
-                    gld(a.w, ((int64_t)co * a.Ci + a.c_kp0 + j) * a.KK + tap);
+            for (int i = tid; i < kMaxCo * KK; i += kThreads) {
+                const int co = i / KK, tap = i - co * KK;
+                wf[(s * KK + tap) * kMaxCo + co] =
+                    co < a.Co ? gld(a.w, ((int64_t)co * a.Ci + a.c_kp0 + j) * KK + tap) : 0.f;
             }
+        }
+        for (int t = tid; t < KK; t += kThreads) {
+            const int kh = t / a.KW, kw = t - kh * a.KW;
+            toff[t] = kh * a.DH * a.FW + kw * a.DW;
         }
     }
     const int py = tid / kTile, px = tid - py * kTile;
-    float acc[kMaxCo];
+    const int hbase = py * a.SH * a.FW + px * a.SW;
+    f32x4 acc[kMaxCo / 4];
 #pragma unroll
-    for (int c = 0; c < kMaxCo; ++c) acc[c] = 0.f;
+    for (int c = 0; c < kMaxCo / 4; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
     int s = 0;
     for (uint32_t m = mask; m; m &= m - 1, ++s) {
         const int j = __ffs(m) - 1;
         const Win w = wins[j];
-        __syncthreads();  // previous part's map consumed (and wl written, first time)
+        __syncthreads();  // previous part's map consumed (and wl / toff written, first time)
         for (int i = tid; i < a.FH * a.FW; i += kThreads) {
             const int r = i / a.FW, c = i - r * a.FW;
-            hl[i] = heat(a, w, iy0 + r, ix0 + c);
+            hl[i] = (a.dbg & 1) ? 0.f : heat(a, w, iy0 + r, ix0 + c);
         }
         __syncthreads();
-        for (int kh = 0; kh < a.KH; ++kh)
-            for (int kw = 0; kw < a.KW; ++kw) {
-                const float h = hl[(py * a.SH + kh * a.DH) * a.FW + px * a.SW + kw * a.DW];
-                const int tap = kh * a.KW + kw;
+        if (a.dbg & 2) continue;
+        const f32x4* wp = wl + s * KK * (kMaxCo / 4);
+        int t = 0;
+        for (; t + 5 <= KK; t += 5) {
+            float h[5];
 #pragma unroll
-                for (int c = 0; c < kMaxCo; ++c)
-                    if (c < a.Co) acc[c] += wl[(c * nact + s) * a.KK + tap] * h;
-            }
+            for (int u = 0; u < 5; ++u) h[u] = hl[hbase + toff[t + u]];
+#pragma unroll
+            for (int u = 0; u < 5; ++u)
+#pragma unroll
+                for (int c = 0; c < kMaxCo / 4; ++c) acc[c] += wp[(t + u) * (kMaxCo / 4) + c] * h[u];
+        }
+        for (; t < KK; ++t) {
+            const float h = hl[hbase + toff[t]];
+#pragma unroll
+            for (int c = 0; c < kMaxCo / 4; ++c) acc[c] += wp[t * (kMaxCo / 4) + c] * h;
+        }
     }
     // apply + statistics change (sum, sum of squares) of the stored values
     const int oy = oy0 + py, ox = ox0 + px;
-    const bool in = oy < a.OH && ox < a.OW;
+    const bool in = oy < a.OH && ox < a.OW && !(a.dbg & 4);
     float d0[kMaxCo], d1[kMaxCo];
 #pragma unroll
     for (int c = 0; c < kMaxCo; ++c) {
@@ -158,7 +176,7 @@ __global__ __launch_bounds__(kThreads) void kp_fwd_kernel(KpArgs a) {
         if (c < a.Co && in) {
             const int64_t o = (int64_t)n * a.y_ns + ((int64_t)c * a.OH + oy) * a.OW + ox;
             const float v = gld(a.y, o);
-            const float nv = v + acc[c];
+            const float nv = v + acc[c >> 2][c & 3];
             gst(a.y, o, nv);
             d0[c] = nv - v;
             d1[c] = (nv - v) * (nv + v);
@@ -239,11 +257,17 @@ __global__ __launch_bounds__(kThreads) void kp_wgrad_kernel(KpArgs a) {
             const int kh = tap / a.KW, kw = tap - kh * a.KW;
             const float* dr = dyl + co * kMaxWgPix;
             const float* hr = hl + kh * a.DH * fw + kw * a.DW;
-            float s = 0.f;
-            for (int pr = 0; pr < nr; ++pr)
-                for (int pc = 0; pc < ncol; ++pc)
-                    s += dr[pr * ncol + pc] * hr[pr * a.SH * fw + pc * a.SW];
-            acc[u] += s;
+            float s4[4] = {0.f, 0.f, 0.f, 0.f};
+            for (int pr = 0; pr < nr; ++pr) {
+                const float* d = dr + pr * ncol;
+                const float* hh = hr + pr * a.SH * fw;
+                int pc = 0;
+                for (; pc + 4 <= ncol; pc += 4)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) s4[q] += d[pc + q] * hh[(pc + q) * a.SW];
+                for (; pc < ncol; ++pc) s4[0] += d[pc] * hh[pc * a.SW];
+            }
+            acc[u] += (s4[0] + s4[1]) + (s4[2] + s4[3]);
         }
     }
     float* const dwr = a.dw + (int64_t)((blockIdx.x + 7u * blockIdx.y) % (unsigned)a.nrep) * a.rep_stride;
@@ -257,18 +281,26 @@ __global__ __launch_bounds__(kThreads) void kp_wgrad_kernel(KpArgs a) {
 }
 
 // ---- max_pool(k) of the heatmap channels (segment.py:31), dense ------------------------
+// The map decreases with the distance to the keypoint, so the maximum over a k x k cell is
+// the value at the cell pixel inside the window nearest to the keypoint (one exp per
+// pooled pixel; a distance tie gives the same value either way).
 __global__ __launch_bounds__(kThreads) void kp_pool_kernel(KpArgs a) {
+    __shared__ Win ws;
     const int j = blockIdx.y, n = blockIdx.z;
+    if (threadIdx.x == 0) ws = part_window(a, n, j);
+    __syncthreads();
+    const Win w = ws;
     const int PH = a.H / a.k, PW = a.W / a.k;
     const int64_t o = (int64_t)blockIdx.x * kThreads + threadIdx.x;
     if (o >= (int64_t)PH * PW) return;
     const int py = (int)(o / PW), px = (int)(o - (int64_t)py * PW);
-    const Win w = part_window(a, n, j);
+    const int xl = max(px * a.k, w.x0), xh = min(px * a.k + a.k, w.x1) - 1;
+    const int yl = max(py * a.k, w.y0), yh = min(py * a.k + a.k, w.y1) - 1;
     float m = 0.f;
-    const int y0 = py * a.k, x0 = px * a.k;
-    if (w.x1 > w.x0 && w.y1 > w.y0 && y0 < w.y1 && y0 + a.k > w.y0 && x0 < w.x1 && x0 + a.k > w.x0) {
-        for (int dy = 0; dy < a.k; ++dy)
-            for (int dx = 0; dx < a.k; ++dx) m = fmaxf(m, heat(a, w, y0 + dy, x0 + dx));
+    if (xl <= xh && yl <= yh) {
+        const int ix = min(max((int)floor(w.kx + 0.5), xl), xh);
+        const int iy = min(max((int)floor(w.ky + 0.5), yl), yh);
+        m = heat(a, w, iy, ix);
     }
     gst(a.out, (int64_t)n * a.out_ns + (int64_t)j * PH * PW + o, m);
 }
@@ -314,8 +346,10 @@ int32_t isg_kp_stem_fwd(const isg_kp_stem* s, isg_stream_t st) {
     if (!s->w || !s->y) return isg_set_error(ISG_ERR_INVALID, "kp_stem_fwd: NULL weight / output");
     a.w = s->w; a.y = s->y; a.y_ns = s->y_n_stride; a.stats = s->stats;
     // the active parts' weights: Co x nact x KK floats in LDS
-    if (a.Co * a.nparts * a.KK > kMaxWl)
+    if (kMaxCo * a.nparts * a.KK > kMaxWl)
         return isg_set_error(ISG_ERR_UNSUPPORTED, "kp_stem_fwd: %d parts x %d taps", a.nparts, a.KK);
+    static const int dbg = getenv("ISG_KP_DBG") ? atoi(getenv("ISG_KP_DBG")) : 0;
+    a.dbg = dbg;
     a.tiles_x = (a.OW + kTile - 1) / kTile;
     const int tiles_y = (a.OH + kTile - 1) / kTile;
     hipLaunchKernelGGL(kp_fwd_kernel, dim3((unsigned)(a.tiles_x * tiles_y), (unsigned)a.N),
