@@ -554,7 +554,7 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
 int pwx_align16(int v) { return (v + 15) & ~15; }
 
 int pwx_min_blocks() {
-    static const int v = getenv("ISG_PWX_MINB") ? atoi(getenv("ISG_PWX_MINB")) : 256;
+    static const int v = getenv("ISG_PWX_MINB") ? atoi(getenv("ISG_PWX_MINB")) : 512;
     return v;
 }
 
@@ -658,9 +658,12 @@ int32_t isg_pw_gemm(const isg_conv_geom* g, const isg_vtensor* src, const float*
         if (dgrad && a.M % 4 == 0) wmode = 2;
     }
     // measured (per-op tables, kbench): the slab kernel wins on the wide 256^2 forward
-    // layers; elsewhere its longer per-workgroup phase chain loses to the chunked kernel
+    // layers and on input gradients with few rows (M = Ci <= 64, K <= 128: the 48 -> 128
+    // expansions' dgrads 17.1 -> 14.9 us, >= 512 workgroups); elsewhere its longer
+    // per-workgroup phase chain loses to the chunked kernel (the 128 -> 48 dgrads
+    // 12.2 -> 17.0 us, the 256 -> 128 resconv forward 27.6 -> 49.5 us)
     static const bool slab_all = getenv("ISG_PW_SLAB_ALL") != nullptr;
-    const bool slab_pays = slab_all || (!dgrad && a.P >= 65536);
+    const bool slab_pays = slab_all || (!dgrad && a.P >= 65536) || (dgrad && a.M <= 64 && a.K <= 128);
     if (!slab_off && slab_pays && wmode && pwx_src_ok(*src, a.HW)) {
         PwxArgs b{};
         b.src = a.src; b.out = a.out; b.w = w; b.rs = a.rs; b.cs = a.cs;
