@@ -125,6 +125,13 @@ ISG_DEV float ch_xform(int xf, int act, const ChanCoef& k, float x, float y) {
     return k.c0 * x + k.c1 * (y - k.c2) + k.c3;
 }
 
+// ch_xform for a WAVE-UNIFORM channel: the transform kind moves to SGPRs, so the
+// per-element selection is a scalar branch (a VGPR kind branches per element with exec
+// masking). Only for callers whose channel is the same in every lane of the wave.
+ISG_DEV float ch_xform_u(int xf, int act, const ChanCoef& k, float x, float y) {
+    return ch_xform(__builtin_amdgcn_readfirstlane(xf), __builtin_amdgcn_readfirstlane(act), k, x, y);
+}
+
 ISG_DEV int wave_id() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }
 
 // A wave-uniform pointer moved into SGPRs (each 32-bit half through readfirstlane), so

@@ -8,6 +8,8 @@
 //
 //   forward: out[m][p] = sum_{c,kh,kw} W[m][c][kh][kw] * x[c][p + (kh*D - P, kw*D - P)]
 //   dgrad  : dx[m][q]  = sum_{c,kh,kw} W[c][m][kh][kw] * dy[c][q + (P - kh*D, P - kw*D)]
+#include <algorithm>
+
 #include "stage.h"
 
 namespace {
@@ -94,6 +96,34 @@ __global__ __launch_bounds__(kThreads) void thin_conv_kernel(ThinArgs a) {
     }
 }
 
+// One window row of the 4-pixel lane: source row iy, columns ox-1 .. ox+4, the producer's
+// transform applied and zero padding outside the plane (after the transform). All loads
+// are unconditional (clamped offsets), so a lane's rows are in flight together.
+ISG_DEV void x4_window(const float* xp, const float* yp, bool bwd, const ChT& t, bool pv, int iy,
+                       int ox, int H, int W, float (&v)[6]) {
+    const bool rok = pv && (unsigned)iy < (unsigned)H;
+    const int64_t o = (int64_t)(rok ? iy : 0) * W + ox;
+    const bool lok = rok && ox > 0, rrok = rok && ox + 4 < W;
+    const f32x4 c4 = gld4(xp, o);
+    const float l = gld(xp, lok ? o - 1 : o), rr = gld(xp, rrok ? o + 4 : o);
+    float y6[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (bwd) {
+        const f32x4 yc = gld4(yp, o);
+        y6[0] = gld(yp, lok ? o - 1 : o);
+        y6[1] = yc[0]; y6[2] = yc[1]; y6[3] = yc[2]; y6[4] = yc[3];
+        y6[5] = gld(yp, rrok ? o + 4 : o);
+    }
+    const float raw[6] = {l, c4[0], c4[1], c4[2], c4[3], rr};
+#pragma unroll
+    for (int i = 0; i < 6; ++i) v[i] = ch_xform_u(t.xf, t.act, t.k, raw[i], y6[i]);
+    if (!lok) v[0] = 0.f;
+    if (!rrok) v[5] = 0.f;
+    if (!rok) {
+#pragma unroll
+        for (int i = 1; i < 5; ++i) v[i] = 0.f;
+    }
+}
+
 // 3x3, pad 1, dilation 1, 4 consecutive output pixels per lane (DstW % 4 == 0): per
 // (channel, window row) one 16-B load of the 4 centre columns plus the two edge columns.
 template <int C, int M>
@@ -134,29 +164,8 @@ __global__ __launch_bounds__(kThreads) void thin_conv3_x4_kernel(ThinArgs a) {
         const bool bwd = t.xf == ISG_XF_BN_BWD;
 #pragma unroll
         for (int kh = 0; kh < 3; ++kh) {
-            const int iy = oy - 1 + kh;
             float v[6];
-            if (pv && (unsigned)iy < (unsigned)a.SrcH) {
-                const int64_t o = (int64_t)iy * a.SrcW + ox;
-                const f32x4 c4 = *reinterpret_cast<const f32x4*>(xp + o);
-                const float l = ox > 0 ? gld(xp, o - 1) : 0.f;
-                const float rr = ox + 4 < a.SrcW ? gld(xp, o + 4) : 0.f;
-                float y4[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-                if (bwd) {
-                    const f32x4 yc = *reinterpret_cast<const f32x4*>(yp + o);
-                    y4[0] = ox > 0 ? gld(yp, o - 1) : 0.f;
-                    y4[1] = yc[0]; y4[2] = yc[1]; y4[3] = yc[2]; y4[4] = yc[3];
-                    y4[5] = ox + 4 < a.SrcW ? gld(yp, o + 4) : 0.f;
-                }
-                const float raw[6] = {l, c4[0], c4[1], c4[2], c4[3], rr};
-#pragma unroll
-                for (int i = 0; i < 6; ++i) v[i] = ch_xform(t.xf, t.act, t.k, raw[i], y4[i]);
-                if (ox == 0) v[0] = 0.f;  // zero padding is applied AFTER the transform
-                if (ox + 4 >= a.SrcW) v[5] = 0.f;
-            } else {
-#pragma unroll
-                for (int i = 0; i < 6; ++i) v[i] = 0.f;
-            }
+            x4_window(xp, yp, bwd, t, pv, oy - 1 + kh, ox, a.SrcH, a.SrcW, v);
 #pragma unroll
             for (int kw = 0; kw < 3; ++kw)
 #pragma unroll
@@ -202,7 +211,92 @@ __global__ __launch_bounds__(kThreads) void thin_conv3_x4_kernel(ThinArgs a) {
     }
 }
 
+// Weight gradient of the thin 3x3 convs (pad 1, dilation 1, stride 1; M*C*9 <= 36):
+//   dW[m][c][kh][kw] += sum_p dy[m][p] * x[c][p + (kh-1, kw-1)],  dbias[m] += sum_p dy[m][p]
+// 4 consecutive pixels per lane (the forward's window rows), grid-stride over the quads;
+// each workgroup reduces its partials (waves in fixed order) and adds them with one atomic
+// per element into one of nrep replicas (include/isg.h ISG_WREP).
+struct ThinWgArgs {
+    isg_vtensor dy, x;
+    float* dw;
+    float* dbias;
+    int64_t rep_stride;
+    int nrep;
+    int N, H, W;
+};
+
+template <int C, int M>
+__global__ __launch_bounds__(kThreads) void thin_wgrad3_x4_kernel(ThinWgArgs a) {
+    constexpr int NA = M * C * 9 + M;  // weight partials + bias partials
+    __shared__ ChT tx[C], ty[M];
+    __shared__ float red[4][NA];
+    const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
+    const int64_t hw = (int64_t)a.H * a.W;
+    if (tid < C) tx[tid] = ch_table_entry(a.x, tid, hw);
+    if (tid < M) ty[tid] = ch_table_entry(a.dy, tid, hw);
+    __syncthreads();
+    float acc[NA];
+#pragma unroll
+    for (int i = 0; i < NA; ++i) acc[i] = 0.f;
+    const int wq = a.W >> 2;
+    const int64_t hwq = (int64_t)a.H * wq, nq = (int64_t)a.N * hwq;
+    for (int64_t q = (int64_t)blockIdx.x * kThreads + tid; q < nq + kThreads - 1; q += (int64_t)gridDim.x * kThreads) {
+        if (q - tid >= nq) break;  // wave-uniform exit once the whole block is past the end
+        const bool pv = q < nq;
+        const int64_t qq = pv ? q : 0;
+        const int n = (int)(qq / hwq);
+        const int r = (int)(qq - (int64_t)n * hwq);
+        const int oy = r / wq, ox = (r - oy * wq) * 4;
+        float d[M][4];
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+            const ChT t = ty[m];
+            const int64_t o = (int64_t)oy * a.W + ox;
+            const f32x4 g4 = gld4(t.p + (int64_t)n * t.ns, o);
+            f32x4 y4 = g4;
+            if (t.xf == ISG_XF_BN_BWD) y4 = gld4(t.y + (int64_t)n * t.yns, o);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) d[m][j] = pv ? ch_xform_u(t.xf, t.act, t.k, g4[j], y4[j]) : 0.f;
+        }
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            const ChT t = tx[c];
+            const float* xp = t.p + (int64_t)n * t.ns;
+            const float* yp = t.y + (int64_t)n * t.yns;
+#pragma unroll
+            for (int kh = 0; kh < 3; ++kh) {
+                float v[6];
+                x4_window(xp, yp, t.xf == ISG_XF_BN_BWD, t, pv, oy - 1 + kh, ox, a.H, a.W, v);
+#pragma unroll
+                for (int m = 0; m < M; ++m)
+#pragma unroll
+                    for (int kw = 0; kw < 3; ++kw) {
+                        float s = acc[(m * C + c) * 9 + kh * 3 + kw];
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) s = fmaf(d[m][j], v[j + kw], s);
+                        acc[(m * C + c) * 9 + kh * 3 + kw] = s;
+                    }
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < M; ++m) acc[M * C * 9 + m] += (d[m][0] + d[m][1]) + (d[m][2] + d[m][3]);
+    }
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+        const float t = wave_sum(acc[i]);
+        if (lane == 0) red[wave][i] = t;
+    }
+    __syncthreads();
+    if (tid < NA) {
+        const float t = ((red[0][tid] + red[1][tid]) + red[2][tid]) + red[3][tid];
+        const int64_t ro = (int64_t)(blockIdx.x % (unsigned)a.nrep) * a.rep_stride;
+        if (tid < M * C * 9) atomicAdd(&a.dw[ro + tid], t);
+        else if (a.dbias) atomicAdd(&a.dbias[ro + tid - M * C * 9], t);
+    }
+}
+
 }  // namespace
+
 
 // Returns 1 if launched, 0 if the shape is not for this kernel, <0 on error.
 int32_t isg_thin_conv(const isg_conv_geom* g, const isg_vtensor* src, const float* w,
@@ -241,5 +335,36 @@ int32_t isg_thin_conv(const isg_conv_geom* g, const isg_vtensor* src, const floa
     else if (C == 4 && M == 4 && K == 3) hipLaunchKernelGGL((thin_conv_kernel<4, 4, 3>), grid, dim3(kThreads), 0, st, a);
     else return 0;
     const int32_t e = isg_check_launch("thin_conv_kernel");
+    return e ? e : 1;
+}
+
+// Returns 1 if launched, 0 if the shape is not for this kernel, <0 on error.
+int32_t isg_thin_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, float* dw,
+                       float* dbias, int64_t rep_stride, int32_t nrep, hipStream_t st) {
+    static const bool off = getenv("ISG_NO_THIN_WGRAD") != nullptr;
+    if (off || g->groups != 1 || g->SH != 1 || g->SW != 1 || g->KH != 3 || g->KW != 3 ||
+        g->PH != 1 || g->PW != 1 || g->DH != 1 || g->DW != 1 || g->OH != g->H || g->OW != g->W ||
+        g->W % 4 || dy->nseg != 1 || x->nseg != 1 || (g->w_ci > 0 && g->w_ci != g->Ci))
+        return 0;
+    auto al = [](const isg_vseg& sg) {
+        return (uintptr_t)sg.p % 16 == 0 && sg.n_stride % 4 == 0 &&
+               (sg.xform != ISG_XF_BN_BWD || ((uintptr_t)sg.y % 16 == 0 && sg.y_n_stride % 4 == 0));
+    };
+    if (!al(dy->s[0]) || !al(x->s[0])) return 0;
+    ThinWgArgs a{};
+    a.dy = *dy; a.x = *x; a.dw = dw; a.dbias = dbias;
+    a.rep_stride = nrep > 1 ? rep_stride : 0;
+    a.nrep = nrep < 1 ? 1 : nrep;
+    a.N = g->N; a.H = g->H; a.W = g->W;
+    const int64_t nq = (int64_t)g->N * g->H * (g->W / 4);
+    // ~4 quads per lane: enough work per workgroup to amortise its reduction
+    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(2048, (nq + 4 * kThreads - 1) / (4 * kThreads)));
+    if (g->Ci == 4 && g->Co == 1)
+        hipLaunchKernelGGL((thin_wgrad3_x4_kernel<4, 1>), dim3((unsigned)blocks), dim3(kThreads), 0, st, a);
+    else if (g->Ci == 1 && g->Co == 4)
+        hipLaunchKernelGGL((thin_wgrad3_x4_kernel<1, 4>), dim3((unsigned)blocks), dim3(kThreads), 0, st, a);
+    else
+        return 0;
+    const int32_t e = isg_check_launch("thin_wgrad3_x4_kernel");
     return e ? e : 1;
 }

@@ -585,14 +585,19 @@ ISG_STAMP_ACCESSOR(isg_dbg_stamps_wgrad)
 int32_t isg_tap_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, float* dw,
                       float* dbias, int64_t rep_stride, int32_t nrep, hipStream_t st);
 
+int32_t isg_thin_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, float* dw,
+                       float* dbias, int64_t rep_stride, int32_t nrep, hipStream_t st);
+
 int32_t isg_dense_conv_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x,
                              float* dw, float* dbias, int64_t rep_stride, int32_t nrep,
                              hipStream_t st) {
     if (vt_channels(dy) != g->Co || vt_channels(x) != g->Ci)
         return isg_set_error(ISG_ERR_INVALID, "conv wgrad: channel mismatch");
     if (!dw) return isg_set_error(ISG_ERR_INVALID, "conv wgrad: dw is NULL");
-    if (!(g->KH == 1 && g->KW == 1)) {  // narrow spatial convs: tap_wgrad.hip
-        const int32_t t = isg_tap_wgrad(g, dy, x, dw, dbias, rep_stride, nrep, st);
+    if (!(g->KH == 1 && g->KW == 1)) {  // thin 3x3 (thin_conv.hip), narrow spatial (tap_wgrad.hip)
+        int32_t t = isg_thin_wgrad(g, dy, x, dw, dbias, rep_stride, nrep, st);
+        if (t != 0) return t < 0 ? t : 0;
+        t = isg_tap_wgrad(g, dy, x, dw, dbias, rep_stride, nrep, st);
         if (t != 0) return t < 0 ? t : 0;
     }
     {

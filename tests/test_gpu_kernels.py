@@ -75,6 +75,9 @@ DENSE = [
     (20, 16, 128, 128, 5, 2, 2, 1),
     (16, 16, 16, 16, 3, 1, 1, 1),
     (48, 16, 16, 16, 2, 2, 0, 1),
+    # thin 3x3 (thin_conv / thin_wgrad, 4 pixels per lane): ragged row count, 1 -> 4
+    (4, 1, 37, 96, 3, 1, 1, 1),
+    (1, 4, 24, 20, 3, 1, 1, 1),
     # k4 s2 p1: the ConvTranspose2d input gradients (odd first tap column, stride-2 pairs)
     (16, 48, 32, 32, 4, 2, 1, 1),
     (16, 4, 64, 48, 4, 2, 1, 1),
