@@ -258,6 +258,9 @@ static bool is_pointwise(const isg_conv_geom* g) {
            g->groups == 1 && g->Ci <= 256 && g->Co <= 256;
 }
 
+int32_t isg_down_conv_fwd(const isg_conv_geom* g, const isg_vtensor* src, const float* w,
+                          const isg_sinks* out, hipStream_t st);
+
 int32_t isg_dense_conv_fwd(const isg_conv_geom* g, const isg_vtensor* x, const float* w,
                            const isg_sinks* out, hipStream_t st) {
     if (vt_channels(x) != g->Ci) return isg_set_error(ISG_ERR_INVALID, "conv fwd: Ci mismatch");
@@ -266,6 +269,10 @@ int32_t isg_dense_conv_fwd(const isg_conv_geom* g, const isg_vtensor* x, const f
     if (!special_off && is_pointwise(g)) return isg_pw_gemm(g, x, w, out, false, st);
     if (!special_off) {  // thin stride-1 convs on the VALU (thin_conv.hip)
         const int32_t t = isg_thin_conv(g, x, w, out, false, st);
+        if (t != 0) return t < 0 ? t : 0;
+    }
+    if (!special_off) {  // k 2S, stride S: the sub-pixel convT's input gradient (down_conv.hip)
+        const int32_t t = isg_down_conv_fwd(g, x, w, out, st);
         if (t != 0) return t < 0 ? t : 0;
     }
     if (!special_off) {  // dense spatial conv, <= 48 output channels (tap_conv.hip)

@@ -1,0 +1,305 @@
+// The backward of the sub-pixel ConvTranspose2d (kernel 2S, stride S, pad S/2;
+// segment.py:305-306 k4 s2 p1 and the mask head's k8 s4 p2, :435-436) on the VALU. Both
+// directions are "down" convolutions with kernel 2S, stride S, pad S/2 over the
+// convT's output gradient dy (C channels, S x the resolution):
+//
+//   input gradient  dx[m][i][j] = sum_{c,kh,kw} W[m][c][kh][kw] * dy[c][S*i - S/2 + kh][S*j - S/2 + kw]
+//   weight gradient dW[m][c][kh][kw] += sum_{n,i,j} x[m][i][j] * dy[c][S*i - S/2 + kh][S*j - S/2 + kw]
+//
+// with W = the convT weight [M = in channels][C = out channels][2S][2S], x its input.
+// The plan issues them as a stride-S conv (OP_CONV_FWD) and its weight gradient
+// (OP_CONV_WGRAD); tap_conv stages at most stride 2 and the generic kernels ran the head's
+// pair at 67 / 90 us (1.07 GFLOP each at bs2 1024^2).
+//
+// down_conv_kernel: one lane per input cell (i, j), all M <= 16 outputs in registers; the
+// cell's C x 2S x 2S patch is read row by row with 16-B loads (the producer's transform
+// applied, zero outside the plane) and multiplied by weights kept in LDS as
+// [c][kh][kw][m] (4 outputs per broadcast ds_read_b128). The epilogue routes every output
+// channel through its sink (stage.h SinkRow) with the BN-backward sums reduced per
+// workgroup.
+// down_wgrad_kernel: persistent workgroups over tiles of TY x TX cells; per tile the x
+// values (with the transform) and the dy patch region go to LDS; lane t owns GEMM column
+// t = (c, kh, kw) and accumulates its M outputs across all of the workgroup's tiles; one
+// atomic per dW element per workgroup into one of nrep replicas.
+#include <algorithm>
+
+#include "stage.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kMaxM = 16;
+constexpr int kMaxC = 4;
+
+struct DownArgs {
+    isg_vtensor dy;    // C channels, Hd x Wd (= S x the cell grid)
+    isg_vtensor x;     // wgrad: M channels, cell grid H x W
+    isg_sinks out;     // input gradient: M channels on the cell grid
+    const float* w;    // [M][C][2S][2S]
+    float* dw;
+    int64_t rep_stride;
+    int nrep;
+    int N, M, C, H, W;  // cell grid
+    int tiles_x, ntiles;
+};
+
+// one 2S-wide patch row of channel table entry t at source row r, columns S*j - S/2 ..
+// S*j + 3S/2 - 1, transformed, zero outside the plane (after the transform)
+template <int S>
+ISG_DEV void patch_row(const ChT& t, int n, int r, int j, int Hd, int Wd, float (&v)[2 * S]) {
+    const bool rok = (unsigned)r < (unsigned)Hd;
+    const int64_t row = (int64_t)(rok ? r : 0) * Wd;
+    const float* xp = t.p + (int64_t)n * t.ns + row;
+    const float* yp = t.y + (int64_t)n * t.yns + row;
+    const bool bwd = t.xf == ISG_XF_BN_BWD;
+    // aligned 16-B / 8-B pieces covering [S*j - S, S*j + 2S): use elements S/2 .. S/2+2S-1
+    const int c0 = S * j - S;
+    float raw[3 * S], ry[3 * S];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        const int c = c0 + q * S;
+        const bool cok = rok && c >= 0 && c < Wd;
+        const int cc = cok ? c : 0;
+        if constexpr (S == 4) {
+            const f32x4 a = gld4(xp, cc);
+            const f32x4 b = bwd ? gld4(yp, cc) : a;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                raw[q * 4 + e] = cok ? a[e] : 0.f;
+                ry[q * 4 + e] = b[e];
+            }
+        } else {
+            const float a0 = gld(xp, cc), a1 = gld(xp, cc + (cok ? 1 : 0));
+            const float b0 = bwd ? gld(yp, cc) : a0, b1 = bwd ? gld(yp, cc + (cok ? 1 : 0)) : a1;
+            raw[q * 2] = cok ? a0 : 0.f;
+            raw[q * 2 + 1] = cok ? a1 : 0.f;
+            ry[q * 2] = b0;
+            ry[q * 2 + 1] = b1;
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < 2 * S; ++e) {
+        const int k = S / 2 + e;
+        const int col = c0 + k;
+        const bool ok = rok && col >= 0 && col < Wd;
+        v[e] = ok ? ch_xform_u(t.xf, t.act, t.k, raw[k], ry[k]) : 0.f;
+    }
+}
+
+template <int S, int M>
+__global__ __launch_bounds__(kThreads) void down_conv_kernel(DownArgs a) {
+    constexpr int K = 2 * S;
+    constexpr int M4 = (M + 3) / 4;
+    __shared__ f32x4 wl[kMaxC * K * K * M4];  // [c][kh][kw][m/4]
+    __shared__ ChT tab[kMaxC];
+    __shared__ SinkRow ri[kMaxM];
+    __shared__ float red[4][3][kMaxM];
+    const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
+    const int Hd = a.H * S, Wd = a.W * S;
+    if (tid < a.C) tab[tid] = ch_table_entry(a.dy, tid, (int64_t)Hd * Wd);
+    if (tid < a.M) ri[tid] = sink_row(a.out, tid, (int64_t)a.H * a.W);
+    float* const wf = reinterpret_cast<float*>(wl);
+    for (int i = tid; i < a.C * K * K * M4 * 4; i += kThreads) {
+        const int m = i % (M4 * 4), r = i / (M4 * 4);  // r = (c*K + kh)*K + kw
+        const int c = r / (K * K), tap = r - c * K * K;
+        wf[i] = m < a.M ? gld(a.w, ((int64_t)m * a.C + c) * K * K + tap) : 0.f;
+    }
+    __syncthreads();
+    const int64_t hw = (int64_t)a.H * a.W;
+    const int64_t cell = (int64_t)blockIdx.x * kThreads + tid;
+    const bool pv = cell < (int64_t)a.N * hw;
+    const int64_t cc = pv ? cell : 0;
+    const int n = (int)(cc / hw);
+    const int64_t pix = cc - (int64_t)n * hw;
+    const int i = (int)(pix / a.W), j = (int)(pix - (int64_t)i * a.W);
+    f32x4 acc[M4];
+#pragma unroll
+    for (int q = 0; q < M4; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int c = 0; c < a.C; ++c) {
+        const ChT t = tab[c];
+#pragma unroll 2
+        for (int kh = 0; kh < K; ++kh) {
+            float v[K];
+            patch_row<S>(t, n, S * i - S / 2 + kh, j, Hd, Wd, v);
+            const f32x4* wr = wl + ((c * K + kh) * K) * M4;
+#pragma unroll
+            for (int kw = 0; kw < K; ++kw)
+#pragma unroll
+                for (int q = 0; q < M4; ++q) acc[q] += wr[kw * M4 + q] * v[kw];
+        }
+    }
+    float s0[M], s1[M], s2[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+        s0[m] = s1[m] = s2[m] = 0.f;
+        if (pv && m < a.M) sink_row_apply(ri[m], n, pix, acc[m >> 2][m & 3], s0[m], s1[m], s2[m]);
+    }
+    if (sinks_need_red(a.out)) {
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+            const float t0 = wave_sum(s0[m]), t1 = wave_sum(s1[m]), t2 = wave_sum(s2[m]);
+            if (lane == 0) {
+                red[wave][0][m] = t0;
+                red[wave][1][m] = t1;
+                red[wave][2][m] = t2;
+            }
+        }
+        __syncthreads();
+        if (tid < a.M) {
+            float r3[3];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) r3[q] = ((red[0][q][tid] + red[1][q][tid]) + red[2][q][tid]) + red[3][q][tid];
+            sink_row_flush(a.out, tid, r3[0], r3[1], r3[2]);
+        }
+    }
+    sinks_finalize(a.out);
+}
+
+// weight gradient: tiles of TY x TX cells; lane t = column (c, kh, kw) < C*K*K <= 256
+template <int S, int M, int TY, int TX>
+__global__ __launch_bounds__(kThreads) void down_wgrad_kernel(DownArgs a) {
+    constexpr int K = 2 * S;
+    constexpr int M4 = (M + 3) / 4;
+    constexpr int NC = TY * TX;                       // cells per tile
+    constexpr int RH = S * TY + S, RW = S * TX + S;   // dy region rows / cols per channel
+    __shared__ f32x4 xl[NC * M4];                     // [cell][m/4]
+    __shared__ float dl[kMaxC * RH * RW];             // [c][row][col]
+    __shared__ ChT tx[kMaxM], ty[kMaxC];
+    const int tid = threadIdx.x;
+    const int Hd = a.H * S, Wd = a.W * S;
+    const int64_t hw = (int64_t)a.H * a.W;
+    if (tid < a.M) tx[tid] = ch_table_entry(a.x, tid, hw);
+    if (tid < a.C) ty[tid] = ch_table_entry(a.dy, tid, (int64_t)Hd * Wd);
+    const int ncol = a.C * K * K;
+    const int col = min(tid, ncol - 1);
+    const int c = col / (K * K), tap = col - c * K * K, kh = tap / K, kw = tap - kh * K;
+    const int coff = (c * RH + kh) * RW + kw;  // + S*(cy*RW + cx) per cell
+    f32x4 acc[M4];
+#pragma unroll
+    for (int q = 0; q < M4; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int tpi = a.tiles_x * ((a.H + TY - 1) / TY);
+    for (int tile = blockIdx.x; tile < a.ntiles; tile += gridDim.x) {
+        const int n = tile / tpi, tr = tile - n * tpi;
+        const int tyi = tr / a.tiles_x;
+        const int i0 = tyi * TY, j0 = (tr - tyi * a.tiles_x) * TX;
+        __syncthreads();  // previous tile consumed (and the channel tables written)
+        // x values of the tile's cells (zero past the grid)
+        float* const xf = reinterpret_cast<float*>(xl);
+        for (int e = tid; e < NC * M4 * 4; e += kThreads) {
+            const int cell = e / (M4 * 4), m = e - cell * (M4 * 4);
+            const int ci = i0 + cell / TX, cj = j0 + cell % TX;
+            float v = 0.f;
+            if (m < a.M && ci < a.H && cj < a.W) {
+                const ChT t = tx[m];
+                const int64_t o = (int64_t)ci * a.W + cj;
+                const float raw = gld(t.p, (int64_t)n * t.ns + o);
+                const float yy = t.xf == ISG_XF_BN_BWD ? gld(t.y, (int64_t)n * t.yns + o) : raw;
+                v = ch_xform(t.xf, t.act, t.k, raw, yy);
+            }
+            xf[e] = v;
+        }
+        // dy region rows S*i0 - S/2 .., cols S*j0 - S/2 .. (zero outside the plane)
+        const int r0 = S * i0 - S / 2, q0 = S * j0 - S / 2;
+        for (int e = tid; e < a.C * RH * RW; e += kThreads) {
+            const int ch = e / (RH * RW), rem = e - ch * RH * RW;
+            const int rr = rem / RW, qq = rem - rr * RW;
+            const int r = r0 + rr, q = q0 + qq;
+            float v = 0.f;
+            if ((unsigned)r < (unsigned)Hd && (unsigned)q < (unsigned)Wd) {
+                const ChT t = ty[ch];
+                const int64_t o = (int64_t)r * Wd + q;
+                const float raw = gld(t.p, (int64_t)n * t.ns + o);
+                const float yy = t.xf == ISG_XF_BN_BWD ? gld(t.y, (int64_t)n * t.yns + o) : raw;
+                v = ch_xform(t.xf, t.act, t.k, raw, yy);
+            }
+            dl[e] = v;
+        }
+        __syncthreads();
+#pragma unroll 4
+        for (int cell = 0; cell < NC; ++cell) {
+            const int cy = cell / TX, cx = cell - cy * TX;
+            const float d = dl[coff + S * (cy * RW + cx)];
+#pragma unroll
+            for (int q = 0; q < M4; ++q) acc[q] += xl[cell * M4 + q] * d;
+        }
+    }
+    if (tid < ncol) {
+        float* const dwr = a.dw + (int64_t)(blockIdx.x % (unsigned)a.nrep) * a.rep_stride;
+#pragma unroll
+        for (int m = 0; m < M; ++m)
+            if (m < a.M) atomicAdd(&dwr[((int64_t)m * a.C + c) * K * K + tap], acc[m >> 2][m & 3]);
+    }
+}
+
+bool down_geom(const isg_conv_geom* g, int& S) {
+    S = g->SH;
+    return g->groups == 1 && (S == 2 || S == 4) && g->SW == S && g->KH == 2 * S && g->KW == 2 * S &&
+           g->PH == S / 2 && g->PW == S / 2 && g->DH == 1 && g->DW == 1 && g->H == S * g->OH &&
+           g->W == S * g->OW && g->W % 4 == 0 && (g->w_ci == 0 || g->w_ci == g->Ci);
+}
+
+bool down_src_ok(const isg_vtensor* v) {
+    for (int i = 0; i < v->nseg; ++i) {
+        const isg_vseg& s = v->s[i];
+        if ((uintptr_t)s.p % 16 || s.n_stride % 4) return false;
+        if (s.xform == ISG_XF_BN_BWD && ((uintptr_t)s.y % 16 || s.y_n_stride % 4)) return false;
+    }
+    return true;
+}
+
+}  // namespace
+
+// Returns 1 if launched, 0 if the shape is not for these kernels, <0 on error.
+int32_t isg_down_conv_fwd(const isg_conv_geom* g, const isg_vtensor* src, const float* w,
+                          const isg_sinks* out, hipStream_t st) {
+    static const bool off = getenv("ISG_NO_DOWN_CONV") != nullptr;
+    int S = 0;
+    if (off || !down_geom(g, S) || g->Ci > kMaxC || g->Co > kMaxM || !down_src_ok(src)) return 0;
+    DownArgs a{};
+    a.dy = *src; a.out = *out; a.w = w;
+    a.N = g->N; a.M = g->Co; a.C = g->Ci; a.H = g->OH; a.W = g->OW;
+    const dim3 grid((unsigned)(((int64_t)a.N * a.H * a.W + kThreads - 1) / kThreads));
+    if (S == 4) {
+        if (a.M <= 4) hipLaunchKernelGGL((down_conv_kernel<4, 4>), grid, dim3(kThreads), 0, st, a);
+        else hipLaunchKernelGGL((down_conv_kernel<4, 16>), grid, dim3(kThreads), 0, st, a);
+    } else {
+        if (a.M <= 4) hipLaunchKernelGGL((down_conv_kernel<2, 4>), grid, dim3(kThreads), 0, st, a);
+        else hipLaunchKernelGGL((down_conv_kernel<2, 16>), grid, dim3(kThreads), 0, st, a);
+    }
+    if (out->fin_counter) isg_fin_note_handled();
+    const int32_t e = isg_check_launch("down_conv_kernel");
+    return e ? e : 1;
+}
+
+// weight gradient of the stride-S down conv: dy = the conv's OUTPUT gradient (M channels
+// on the cell grid), x = its input (C channels, S x the grid) — the plan's roles
+int32_t isg_down_conv_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x,
+                            float* dw, float* dbias, int64_t rep_stride, int32_t nrep,
+                            hipStream_t st) {
+    static const bool off = getenv("ISG_NO_DOWN_CONV") != nullptr;
+    int S = 0;
+    if (off || dbias || !down_geom(g, S) || g->Ci > kMaxC || g->Co > kMaxM) return 0;
+    if (g->Ci * 4 * S * S > kThreads) return 0;
+    DownArgs a{};
+    a.x = *dy;   // M channels on the cell grid
+    a.dy = *x;   // C channels at S x the resolution
+    a.dw = dw;
+    a.rep_stride = nrep > 1 ? rep_stride : 0;
+    a.nrep = nrep < 1 ? 1 : nrep;
+    a.N = g->N; a.M = g->Co; a.C = g->Ci; a.H = g->OH; a.W = g->OW;
+    constexpr int TY = 4, TX = 16;
+    a.tiles_x = (a.W + TX - 1) / TX;
+    a.ntiles = a.N * a.tiles_x * ((a.H + TY - 1) / TY);
+    // persistent: ~4 tiles per workgroup (fewer dW atomics), at least two per CU
+    static const int env_grid = getenv("ISG_DOWN_WG_GRID") ? atoi(getenv("ISG_DOWN_WG_GRID")) : 0;
+    const int grid = std::max(1, std::min(a.ntiles, env_grid ? env_grid : std::max(512, a.ntiles / 4)));
+    if (S == 4) {
+        if (a.M <= 4) hipLaunchKernelGGL((down_wgrad_kernel<4, 4, TY, TX>), dim3(grid), dim3(kThreads), 0, st, a);
+        else hipLaunchKernelGGL((down_wgrad_kernel<4, 16, TY, TX>), dim3(grid), dim3(kThreads), 0, st, a);
+    } else {
+        if (a.M <= 4) hipLaunchKernelGGL((down_wgrad_kernel<2, 4, TY, TX>), dim3(grid), dim3(kThreads), 0, st, a);
+        else hipLaunchKernelGGL((down_wgrad_kernel<2, 16, TY, TX>), dim3(grid), dim3(kThreads), 0, st, a);
+    }
+    const int32_t e = isg_check_launch("down_wgrad_kernel");
+    return e ? e : 1;
+}

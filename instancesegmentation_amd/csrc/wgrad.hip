@@ -587,6 +587,9 @@ int32_t isg_tap_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_v
 
 int32_t isg_thin_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, float* dw,
                        float* dbias, int64_t rep_stride, int32_t nrep, hipStream_t st);
+int32_t isg_down_conv_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x,
+                            float* dw, float* dbias, int64_t rep_stride, int32_t nrep,
+                            hipStream_t st);
 
 int32_t isg_dense_conv_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x,
                              float* dw, float* dbias, int64_t rep_stride, int32_t nrep,
@@ -596,6 +599,8 @@ int32_t isg_dense_conv_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, cons
     if (!dw) return isg_set_error(ISG_ERR_INVALID, "conv wgrad: dw is NULL");
     if (!(g->KH == 1 && g->KW == 1)) {  // thin 3x3 (thin_conv.hip), narrow spatial (tap_wgrad.hip)
         int32_t t = isg_thin_wgrad(g, dy, x, dw, dbias, rep_stride, nrep, st);
+        if (t != 0) return t < 0 ? t : 0;
+        t = isg_down_conv_wgrad(g, dy, x, dw, dbias, rep_stride, nrep, st);  // convT weights
         if (t != 0) return t < 0 ? t : 0;
         t = isg_tap_wgrad(g, dy, x, dw, dbias, rep_stride, nrep, st);
         if (t != 0) return t < 0 ? t : 0;

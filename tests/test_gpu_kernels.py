@@ -75,6 +75,12 @@ DENSE = [
     (20, 16, 128, 128, 5, 2, 2, 1),
     (16, 16, 16, 16, 3, 1, 1, 1),
     (48, 16, 16, 16, 2, 2, 0, 1),
+    # k 2S stride S pad S/2 with <= 4 input channels (down_conv: the sub-pixel convT's
+    # input / weight gradients): ragged cell grids, 3 and 8 output channels
+    (4, 16, 40, 56, 8, 4, 2, 1),
+    (4, 3, 32, 32, 8, 4, 2, 1),
+    (4, 16, 32, 48, 4, 2, 1, 1),
+    (2, 8, 24, 40, 4, 2, 1, 1),
     # thin 3x3 (thin_conv / thin_wgrad, 4 pixels per lane): ragged row count, 1 -> 4
     (4, 1, 37, 96, 3, 1, 1, 1),
     (1, 4, 24, 20, 3, 1, 1, 1),
