@@ -290,9 +290,10 @@ int32_t isg_down_conv_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const
     constexpr int TY = 4, TX = 16;
     a.tiles_x = (a.W + TX - 1) / TX;
     a.ntiles = a.N * a.tiles_x * ((a.H + TY - 1) / TY);
-    // persistent: ~4 tiles per workgroup (fewer dW atomics), at least two per CU
+    // ~2 tiles per workgroup (measured on the head's k8 s4: 4 tiles 74 us, 2 tiles 58 us,
+    // 8 tiles 127 us — parallelism, not the dW atomics, bounds it)
     static const int env_grid = getenv("ISG_DOWN_WG_GRID") ? atoi(getenv("ISG_DOWN_WG_GRID")) : 0;
-    const int grid = std::max(1, std::min(a.ntiles, env_grid ? env_grid : std::max(512, a.ntiles / 4)));
+    const int grid = std::max(1, std::min(a.ntiles, env_grid ? env_grid : std::max(512, a.ntiles / 2)));
     if (S == 4) {
         if (a.M <= 4) hipLaunchKernelGGL((down_wgrad_kernel<4, 4, TY, TX>), dim3(grid), dim3(kThreads), 0, st, a);
         else hipLaunchKernelGGL((down_wgrad_kernel<4, 16, TY, TX>), dim3(grid), dim3(kThreads), 0, st, a);
