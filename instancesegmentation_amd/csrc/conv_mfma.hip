@@ -260,6 +260,8 @@ static bool is_pointwise(const isg_conv_geom* g) {
 
 int32_t isg_down_conv_fwd(const isg_conv_geom* g, const isg_vtensor* src, const float* w,
                           const isg_sinks* out, hipStream_t st);
+int32_t isg_sub2_dgrad(const isg_conv_geom* g, const isg_vtensor* dy, const float* w,
+                       const isg_sinks* dx, hipStream_t st);
 
 int32_t isg_dense_conv_fwd(const isg_conv_geom* g, const isg_vtensor* x, const float* w,
                            const isg_sinks* out, hipStream_t st) {
@@ -308,6 +310,10 @@ int32_t isg_dense_conv_dgrad(const isg_conv_geom* g, const isg_vtensor* dy, cons
     if (!special_off && is_pointwise(g)) return isg_pw_gemm(g, dy, w, dx, true, st);
     if (!special_off) {
         const int32_t t = isg_thin_conv(g, dy, w, dx, true, st);
+        if (t != 0) return t < 0 ? t : 0;
+    }
+    if (!special_off) {  // 5x5 stride 2 as a sub-pixel transposed conv (down_conv.hip)
+        const int32_t t = isg_sub2_dgrad(g, dy, w, dx, st);
         if (t != 0) return t < 0 ? t : 0;
     }
     if (!special_off) {

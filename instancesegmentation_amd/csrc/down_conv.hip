@@ -231,6 +231,128 @@ __global__ __launch_bounds__(kThreads) void down_wgrad_kernel(DownArgs a) {
     }
 }
 
+// ---- input gradient of a stride-2 conv with an odd kernel K, pad K/2 (the stem's second
+// 5x5 s2 conv, segment.py:26) as a sub-pixel transposed conv -----------------------------
+//   dx[m][2i+a][2j+b] = sum_c sum_{kh = a+P mod 2} sum_{kw = b+P mod 2}
+//                       W[c][m][kh][kw] * dy[c][(2i+a+P-kh)/2][(2j+b+P-kw)/2]
+// Every output pixel of the 2x2 block of cell (i, j) reads dy inside the cell's
+// (K/2+1)^2 neighbourhood; a lane owns one cell and all 4 x M outputs of its block
+// (the tap_conv route stages the same dy once per phase, four times over). Weights in LDS
+// as [c][kh][kw][m] (4 outputs per broadcast ds_read_b128).
+template <int K, int M>
+__global__ __launch_bounds__(kThreads) void sub2_dgrad_kernel(DownArgs a) {
+    constexpr int P = K / 2, NB = P + 1;                // neighbourhood rows: i - P/2 .. i + (P+1)/2
+    constexpr int R0 = P / 2;                           // row offset of dy row i in the neighbourhood
+    constexpr int M4 = (M + 3) / 4;
+    __shared__ f32x4 wl[kMaxM * K * K * M4];
+    __shared__ ChT tab[kMaxM];
+    __shared__ SinkRow ri[kMaxM];
+    __shared__ float red[4][3][kMaxM];
+    const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
+    const int Hs = a.H, Ws = a.W;          // dy grid (conv output)
+    const int Hd = 2 * Hs, Wd = 2 * Ws;    // dx grid (conv input)
+    if (tid < a.C) tab[tid] = ch_table_entry(a.dy, tid, (int64_t)Hs * Ws);
+    if (tid < a.M) ri[tid] = sink_row(a.out, tid, (int64_t)Hd * Wd);
+    float* const wf = reinterpret_cast<float*>(wl);
+    for (int e = tid; e < a.C * K * K * M4 * 4; e += kThreads) {
+        const int m = e % (M4 * 4), r = e / (M4 * 4);  // r = c*K*K + tap
+        const int c = r / (K * K), tap = r - c * K * K;
+        wf[e] = m < a.M ? gld(a.w, ((int64_t)c * a.M + m) * K * K + tap) : 0.f;
+    }
+    __syncthreads();
+    const int64_t hw = (int64_t)Hs * Ws;
+    const int64_t cell = (int64_t)blockIdx.x * kThreads + tid;
+    const bool pv = cell < (int64_t)a.N * hw;
+    const int64_t cc = pv ? cell : 0;
+    const int n = (int)(cc / hw);
+    const int64_t pix = cc - (int64_t)n * hw;
+    const int i = (int)(pix / Ws), j = (int)(pix - (int64_t)i * Ws);
+    f32x4 acc[2][2][M4];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int v = 0; v < 2; ++v)
+#pragma unroll
+            for (int q = 0; q < M4; ++q) acc[u][v][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int c = 0; c < a.C; ++c) {
+        const ChT t = tab[c];
+        const bool bwd = t.xf == ISG_XF_BN_BWD;
+        const float* xp = t.p + (int64_t)n * t.ns;
+        const float* yp = t.y + (int64_t)n * t.yns;
+        float nb[NB][NB];
+        {
+            float rx[NB][NB], ry[NB][NB];
+            bool ok[NB][NB];
+#pragma unroll
+            for (int r = 0; r < NB; ++r)
+#pragma unroll
+                for (int q = 0; q < NB; ++q) {
+                    const int yy = i - R0 + r, xx = j - R0 + q;
+                    ok[r][q] = pv && (unsigned)yy < (unsigned)Hs && (unsigned)xx < (unsigned)Ws;
+                    const int64_t o = ok[r][q] ? (int64_t)yy * Ws + xx : 0;
+                    rx[r][q] = gld(xp, o);
+                    ry[r][q] = bwd ? gld(yp, o) : 0.f;
+                }
+#pragma unroll
+            for (int r = 0; r < NB; ++r)
+#pragma unroll
+                for (int q = 0; q < NB; ++q)
+                    nb[r][q] = ok[r][q] ? ch_xform_u(t.xf, t.act, t.k, rx[r][q], ry[r][q]) : 0.f;
+        }
+        const f32x4* wc = wl + c * K * K * M4;
+#pragma unroll
+        for (int kh = 0; kh < K; ++kh) {
+            const int au = (kh + P) & 1;                  // output row phase this tap feeds
+            const int rr = (au + P - kh) / 2 + R0;        // neighbourhood row (exact division)
+#pragma unroll
+            for (int kw = 0; kw < K; ++kw) {
+                const int av = (kw + P) & 1;
+                const int qq = (av + P - kw) / 2 + R0;
+                const float d = nb[rr][qq];
+#pragma unroll
+                for (int q = 0; q < M4; ++q) acc[au][av][q] += wc[(kh * K + kw) * M4 + q] * d;
+            }
+        }
+    }
+    float s0[M], s1[M], s2[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+        s0[m] = s1[m] = s2[m] = 0.f;
+        if (pv && m < a.M) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int v = 0; v < 2; ++v) {
+                    float t0 = 0.f, t1 = 0.f, t2 = 0.f;
+                    sink_row_apply(ri[m], n, (int64_t)(2 * i + u) * Wd + 2 * j + v, acc[u][v][m >> 2][m & 3],
+                                   t0, t1, t2);
+                    s0[m] += t0;
+                    s1[m] += t1;
+                    s2[m] += t2;
+                }
+        }
+    }
+    if (sinks_need_red(a.out)) {
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+            const float t0 = wave_sum(s0[m]), t1 = wave_sum(s1[m]), t2 = wave_sum(s2[m]);
+            if (lane == 0) {
+                red[wave][0][m] = t0;
+                red[wave][1][m] = t1;
+                red[wave][2][m] = t2;
+            }
+        }
+        __syncthreads();
+        if (tid < a.M) {
+            float r3[3];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) r3[q] = ((red[0][q][tid] + red[1][q][tid]) + red[2][q][tid]) + red[3][q][tid];
+            sink_row_flush(a.out, tid, r3[0], r3[1], r3[2]);
+        }
+    }
+    sinks_finalize(a.out);
+}
+
 bool down_geom(const isg_conv_geom* g, int& S) {
     S = g->SH;
     return g->groups == 1 && (S == 2 || S == 4) && g->SW == S && g->KH == 2 * S && g->KW == 2 * S &&
@@ -302,5 +424,23 @@ int32_t isg_down_conv_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const
         else hipLaunchKernelGGL((down_wgrad_kernel<2, 16, TY, TX>), dim3(grid), dim3(kThreads), 0, st, a);
     }
     const int32_t e = isg_check_launch("down_wgrad_kernel");
+    return e ? e : 1;
+}
+
+// Returns 1 if launched, 0 if the shape is not for this kernel, <0 on error.
+int32_t isg_sub2_dgrad(const isg_conv_geom* g, const isg_vtensor* dy, const float* w,
+                       const isg_sinks* dx, hipStream_t st) {
+    static const bool off = getenv("ISG_NO_SUB2_DGRAD") != nullptr;
+    if (off || g->groups != 1 || g->SH != 2 || g->SW != 2 || g->KH != 5 || g->KW != 5 ||
+        g->PH != 2 || g->PW != 2 || g->DH != 1 || g->DW != 1 || g->H != 2 * g->OH ||
+        g->W != 2 * g->OW || g->Co > kMaxM || g->Ci > kMaxM || (g->w_ci && g->w_ci != g->Ci))
+        return 0;
+    DownArgs a{};
+    a.dy = *dy; a.out = *dx; a.w = w;
+    a.N = g->N; a.M = g->Ci; a.C = g->Co; a.H = g->OH; a.W = g->OW;
+    const dim3 grid((unsigned)(((int64_t)a.N * a.H * a.W + kThreads - 1) / kThreads));
+    hipLaunchKernelGGL((sub2_dgrad_kernel<5, 16>), grid, dim3(kThreads), 0, st, a);
+    if (dx->fin_counter) isg_fin_note_handled();
+    const int32_t e = isg_check_launch("sub2_dgrad_kernel");
     return e ? e : 1;
 }
