@@ -377,6 +377,9 @@ int32_t isg_down_conv_fwd(const isg_conv_geom* g, const isg_vtensor* src, const 
     static const bool off = getenv("ISG_NO_DOWN_CONV") != nullptr;
     int S = 0;
     if (off || !down_geom(g, S) || g->Ci > kMaxC || g->Co > kMaxM || !down_src_ok(src)) return 0;
+    // measured: S = 2 (bottle5_1up's k4 s2, 128^2 cells) ran 15.6 -> 18.2 us here against the
+    // halo kernel (too few cells per lane-owned output for the VALU form); S = 4 only
+    if (S != 4) return 0;
     DownArgs a{};
     a.dy = *src; a.out = *out; a.w = w;
     a.N = g->N; a.M = g->Co; a.C = g->Ci; a.H = g->OH; a.W = g->OW;
