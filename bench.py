@@ -166,8 +166,8 @@ def infer_bench(dev, reps=20):
     """BASELINE.json's inference half ("infer masks/sec + NMS p50") on config 4
     (OCHuman-style crowded scene): one 1024x1024 image with K=16 person instances (8 people
     + 8 repeated detections) through the infer.py product path as ONE HIP graph
-    (instancesegmentation_amd/infer.py): per-instance crop to 480x480 + 17 keypoint
-    heatmaps on the GPU, Segment(20) eval with BatchNorm folded, sigmoid, paste-back onto
+    (instancesegmentation_amd/infer.py): per-instance crop to 480x480, Segment(20) eval with
+    BatchNorm folded and the 17 keypoint heatmaps synthesised in its stem, sigmoid, paste-back onto
     the 1024x1024 canvas, greedy mask-NMS at IoU 0.5. masks/s = K / (graph time per
     image, inputs resident); NMS p50 = the NMS launches alone, on the same masks."""
     import numpy as np
@@ -189,7 +189,7 @@ def infer_bench(dev, reps=20):
     for b in bns:
         b.momentum = 1.0
     with torch.no_grad():
-        model(calib.x[:len(boxes)].contiguous(), calib.hm[:len(boxes)].contiguous())
+        model(calib.x[:len(boxes)].contiguous(), calib.keypoints[:len(boxes)].contiguous())
     for b in bns:
         b.momentum = 0.1
     model.eval()
@@ -221,8 +221,9 @@ def infer_bench(dev, reps=20):
         e1.synchronize()
         t_nms.append(e0.elapsed_time(e1))
     ms = float(np.median(t_pipe))
-    return {"metric": "infer masks/sec (crop 480x480 + heatmaps + Segment(20) eval, BN folded "
-                      "+ sigmoid + paste 1024x1024 + mask-NMS IoU 0.5, one HIP graph)",
+    return {"metric": "infer masks/sec (crop 480x480 + Segment(20) eval with the keypoint heatmaps "
+                      "synthesised in its stem, BN folded + sigmoid + paste 1024x1024 + mask-NMS "
+                      "IoU 0.5, one HIP graph)",
             "masks_per_s": round(K / (ms * 1e-3), 1), "ms_per_image": round(ms, 3),
             "nms_p50_ms": round(float(np.median(t_nms)), 4), "instances": K, "kept": len(keep),
             "nonempty_masks": nonempty,

@@ -9,7 +9,8 @@ per-instance input path (train_instance.py:139-202, test branch) and model:
     window   = box +/- 16 px                                  (train_instance.py:166-171)
     valid    = image minus what the centring translation drops (:141-149)
     crop     = window resampled to 480x480, normalised [-1,1] (:175-181, :80-85)
-    heatmaps = keypoint2heatmaps of the projected keypoints   (:33-68, :200-202)
+    heatmaps = keypoint2heatmaps of the projected keypoints   (:33-68, :200-202), made
+               inside the stem kernels from the keypoints (never in HBM)
   logits   = Segment(20) in eval mode with every BatchNorm folded into its conv
              (Conv.fuseforward, segment.py:47-48)
   prob     = sigmoid                                           (segment.py:534)
@@ -47,7 +48,6 @@ from .engine import S_ACT, S_IN, S_OUT, S_STATS, S_TENSOR0, Plan
 CROP = 480   # train_instance.py:77
 PAD = 16     # train_instance.py:167
 N_PARTS = 17
-SIGMA, THRESHOLD = 10.0, 0.01  # train_instance.py:33
 
 
 class InstanceSegmenter:
@@ -71,14 +71,15 @@ class InstanceSegmenter:
         cin = self.model.init_conv.layer1.conv.in_channels
         if cin != 3 + N_PARTS:
             raise ValueError(f"InstanceSegmenter needs Segment(20) (RGB + 17 heatmaps), got {cin}")
-        self.plan = Plan(self.model, [(K, 3, S, S), (K, N_PARTS, S, S)], False, False,
+        # the heatmaps are synthesised inside the stem from the projected keypoints
+        # (engine.Keypoints): they are never written to HBM
+        self.plan = Plan(self.model, [(K, 3, S, S), (K, N_PARTS, 3)], False, False,
                          (False, False))
         self.image = torch.zeros((H, W, 3), dtype=torch.uint8, device=dev)
         self.windows = torch.zeros((K, 4), dtype=torch.int32, device=dev)
         self.valid = torch.zeros((K, 4), dtype=torch.int32, device=dev)
         self.keypoints = torch.zeros((K, N_PARTS, 3), dtype=torch.float64, device=dev)
         self.x = torch.empty((K, 3, S, S), dtype=torch.float32, device=dev)
-        self.hm = torch.empty((K, N_PARTS, S, S), dtype=torch.float32, device=dev)
         self.logits = torch.empty(self.plan.out_shapes[0], dtype=torch.float32, device=dev)
         self.prob = torch.empty_like(self.logits)
         self.masks = torch.empty((K, H, W), dtype=torch.uint8, device=dev)
@@ -94,7 +95,7 @@ class InstanceSegmenter:
         tab[S_ACT] = self.act.data_ptr()
         tab[S_STATS] = self.stats.data_ptr()
         tab[S_IN[0]] = self.x.data_ptr()
-        tab[S_IN[1]] = self.hm.data_ptr()
+        tab[S_IN[1]] = self.keypoints.data_ptr()
         tab[S_OUT[0]] = self.logits.data_ptr()
         tensors = [p for _, p in self.model.named_parameters()] + \
                   [b for _, b in self.model.named_buffers()]
@@ -116,8 +117,6 @@ class InstanceSegmenter:
         L.check(lib.isg_instance_crop(self.image.data_ptr(), self.H, self.W,
                                       self.windows.data_ptr(), self.valid.data_ptr(), K, S,
                                       self.x.data_ptr(), st), "instance_crop")
-        L.check(lib.isg_keypoint_heatmaps(self.keypoints.data_ptr(), K, N_PARTS, S, S, SIGMA,
-                                          THRESHOLD, self.hm.data_ptr(), st), "heatmaps")
         self.plan.fwd.run(self.table, st)
         L.check(lib.isg_sigmoid_fwd(self.logits.data_ptr(), self.prob.data_ptr(),
                                     self.prob.numel(), st), "sigmoid")

@@ -168,9 +168,11 @@ def test_instance_segmenter_pipeline_matches_oracle():
     win = IO.instance_windows(boxes)
     valid = IO.valid_rects(boxes, H, W)
     x_ref = IO.crop_instances(img, win, valid)
-    hm_ref = IO.instance_heatmaps(IO.crop_keypoints(kps, win))
+    kp_ref = IO.crop_keypoints(kps, win)
+    hm_ref = IO.instance_heatmaps(kp_ref)
     assert np.array_equal(eng.x[:n].cpu().numpy(), x_ref)
-    assert np.array_equal(eng.hm[:n].cpu().numpy(), hm_ref)
+    # the heatmaps are synthesised inside the stem from these keypoints (kp_stem.hip)
+    assert np.array_equal(eng.keypoints[:n].cpu().numpy(), kp_ref)
     assert np.all(eng.x[n:].cpu().numpy() == -1.0)  # padded slots: empty windows
     # stage 2: logits of the fused network against the fp64 oracle (eval, running stats)
     xin = np.concatenate([x_ref, hm_ref], 1)

@@ -153,6 +153,8 @@ def test_bench_traffic_record_matches_dominant_op():
     assert got == by_label["dw_init_conv.layer1"]["hbm_bytes_per_launch"]
     # another configuration is not covered by the committed pass
     assert bench.pmc_traffic("dw_init_conv.layer1", types.SimpleNamespace(batch=1, cin=20, size=1024)) is None
+    # the keypoint-path dominant op (tools/pmc_bench.sh) is covered too
+    assert bench.pmc_traffic("dx_init_conv.layer2", args) == by_label["dx_init_conv.layer2"]["hbm_bytes_per_launch"]
 
 
 def test_plan_rejects_32bit_offset_overflow():

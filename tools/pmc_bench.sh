@@ -26,9 +26,11 @@ for c in vals:
                 vals[c].append(float(r["Counter_Value"]))
 fs = sum(vals["FETCH_SIZE"]) / max(1, len(vals["FETCH_SIZE"]))
 ws = sum(vals["WRITE_SIZE"]) / max(1, len(vals["WRITE_SIZE"]))
-res = {"op": "bench", "label": label, "kernel": kernel, "config": [2, 20, 1024],
-       "dispatches": len(vals["FETCH_SIZE"]), "FETCH_SIZE_kb_per_dispatch": fs,
-       "WRITE_SIZE_kb_per_dispatch": ws, "hbm_bytes_per_launch": (2.0 * fs + ws) * 1024.0,
+res = {"op": "bench", "label": label, "config": [2, 20, 1024],
+       "shape": "bench.py --steps 3 --warmup 1 (bs2 1024^2, keypoint input)",
+       "kernels": {kernel: {"dispatches": len(vals["FETCH_SIZE"]), "FETCH_SIZE_kb_per_dispatch": fs,
+                            "WRITE_SIZE_kb_per_dispatch": ws}},
+       "hbm_bytes_per_launch": (2.0 * fs + ws) * 1024.0,
        "correction": "2*FETCH_SIZE + WRITE_SIZE per dispatch (KB->B); gfx950 FETCH_SIZE halves 16-B/lane reads"}
 json.dump(res, open(f"{out}/../traffic_{tag}.json", "w"), indent=1)
 print(json.dumps(res))
