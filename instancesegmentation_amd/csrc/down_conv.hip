@@ -236,46 +236,99 @@ __global__ __launch_bounds__(kThreads) void down_wgrad_kernel(DownArgs a) {
 //   dx[m][2i+a][2j+b] = sum_c sum_{kh = a+P mod 2} sum_{kw = b+P mod 2}
 //                       W[c][m][kh][kw] * dy[c][(2i+a+P-kh)/2][(2j+b+P-kw)/2]
 // Every output pixel of the 2x2 block of cell (i, j) reads dy inside the cell's
-// (K/2+1)^2 neighbourhood; a lane owns one cell and all 4 x M outputs of its block
-// (the tap_conv route stages the same dy once per phase, four times over). Weights in LDS
-// as [c][kh][kw][m] (4 outputs per broadcast ds_read_b128).
-template <int K, int M>
-__global__ __launch_bounds__(kThreads) void sub2_dgrad_kernel(DownArgs a) {
-    constexpr int P = K / 2, NB = P + 1;                // neighbourhood rows: i - P/2 .. i + (P+1)/2
-    constexpr int R0 = P / 2;                           // row offset of dy row i in the neighbourhood
-    constexpr int M4 = (M + 3) / 4;
-    __shared__ f32x4 wl[kMaxM * K * K * M4];
+// (P+1)^2 neighbourhood, so one staging of dy serves all four phases (the tap_conv route
+// stages the same dy once per phase, four times over: 99 us; a VALU form with a lane per
+// cell and the weights broadcast from LDS: 85 us; this MFMA form: 67 us).
+
+// sink_row_apply on two horizontally adjacent outputs (pix even, 8-B aligned): one 8-B
+// load of the sink operand and one 8-B store instead of two stride-2 accesses
+typedef float v2f_t __attribute__((ext_vector_type(2)));
+typedef const v2f_t __attribute__((address_space(1)))* gcv2_p;
+typedef v2f_t __attribute__((address_space(1)))* gv2_p;
+ISG_DEV void sink_row_apply2(const SinkRow& q, int n, int64_t pix, float v0, float v1, float& s0,
+                             float& s1, float& s2) {
+    const int64_t off = (int64_t)n * q.ns + pix;
+    if (q.mode == ISG_SINK_STORE) {
+        v0 += q.bias;
+        v1 += q.bias;
+        *(gv2_p)((gfloat_p)q.p + off) = v2f_t{v0, v1};
+        s0 = v0 + v1;
+        s1 = v0 * v0 + v1 * v1;
+    } else if (q.mode == ISG_SINK_ACCUM) {
+        const v2f_t o = *(gcv2_p)((gcfloat_p)q.p + off);
+        *(gv2_p)((gfloat_p)q.p + off) = v2f_t{o[0] + v0, o[1] + v1};
+        s0 = v0 + v1;
+        s1 = v0 * v0 + v1 * v1;
+    } else if (q.mode == ISG_SINK_ACTBWD) {
+        const v2f_t y = *(gcv2_p)((gcfloat_p)q.y + (int64_t)n * q.yns + pix);
+        float g[2];
+        const float v[2] = {v0, v1};
+        s0 = s1 = s2 = 0.f;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const float z = (y[e] - q.f.mean) * q.f.scale + q.f.beta;
+            float gv = v[e];
+            if (q.act == ISG_ACT_RELU) {
+                gv = z > 0.f ? v[e] : 0.f;
+            } else if (q.act == ISG_ACT_PRELU) {
+                gv = z > 0.f ? v[e] : v[e] * q.f.slope;
+                s2 += z > 0.f ? 0.f : z * v[e];
+            }
+            g[e] = gv;
+            s0 += gv;
+            s1 += gv * (y[e] - q.f.mean);
+        }
+        *(gv2_p)((gfloat_p)q.p + off) = v2f_t{g[0], g[1]};
+    }
+}
+
+// MFMA form of the same input gradient (v_mfma_f32_16x16x4_f32): a wave owns 16
+// consecutive cells of one dy row and all 4 phases x 16 outputs of their 2x2 blocks.
+// K runs over (channel group of 4, tap): A[m][k] = W[4g + k][m][kh][kw] (lane: m = l&15,
+// k = l>>4), B[k][cell] = the transformed dy value of channel 4g + k at the tap's
+// neighbour of the cell (lane: k = l>>4, cell = l&15), one MFMA per (group, tap) into the
+// tap's phase accumulator: 4 x 25 MFMAs per 16 cells for Co = 16. D lane: m = 4(l>>4)+r.
+constexpr int kRowsPB = 4;  // dy rows per workgroup (measured: 1 row 81 us, 2 76, 4 67, 8 102)
+
+template <int K>
+__global__ __launch_bounds__(kThreads) void sub2_dgrad_mfma_kernel(DownArgs a) {
+    constexpr int P = K / 2, R0 = P / 2, NB = P + 1;
+    __shared__ float wl[kMaxM * kMaxM * K * K];  // [c][m][kh][kw] (the weight's own layout)
     __shared__ ChT tab[kMaxM];
     __shared__ SinkRow ri[kMaxM];
     __shared__ float red[4][3][kMaxM];
     const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
-    const int Hs = a.H, Ws = a.W;          // dy grid (conv output)
-    const int Hd = 2 * Hs, Wd = 2 * Ws;    // dx grid (conv input)
+    const int kq = lane >> 4, pl = lane & 15;
+    const int Hs = a.H, Ws = a.W, Wd = 2 * Ws;
     if (tid < a.C) tab[tid] = ch_table_entry(a.dy, tid, (int64_t)Hs * Ws);
-    if (tid < a.M) ri[tid] = sink_row(a.out, tid, (int64_t)Hd * Wd);
-    float* const wf = reinterpret_cast<float*>(wl);
-    for (int e = tid; e < a.C * K * K * M4 * 4; e += kThreads) {
-        const int m = e % (M4 * 4), r = e / (M4 * 4);  // r = c*K*K + tap
-        const int c = r / (K * K), tap = r - c * K * K;
-        wf[e] = m < a.M ? gld(a.w, ((int64_t)c * a.M + m) * K * K + tap) : 0.f;
+    if (tid < a.M) ri[tid] = sink_row(a.out, tid, (int64_t)2 * Hs * Wd);
+    for (int e = tid; e < kMaxM * kMaxM * K * K; e += kThreads) {
+        const int c = e / (kMaxM * K * K), r = e - c * kMaxM * K * K;
+        const int m = r / (K * K), tap = r - m * K * K;
+        wl[e] = (c < a.C && m < a.M) ? gld(a.w, ((int64_t)c * a.M + m) * K * K + tap) : 0.f;
     }
     __syncthreads();
-    const int64_t hw = (int64_t)Hs * Ws;
-    const int64_t cell = (int64_t)blockIdx.x * kThreads + tid;
-    const bool pv = cell < (int64_t)a.N * hw;
-    const int64_t cc = pv ? cell : 0;
-    const int n = (int)(cc / hw);
-    const int64_t pix = cc - (int64_t)n * hw;
-    const int i = (int)(pix / Ws), j = (int)(pix - (int64_t)i * Ws);
-    f32x4 acc[2][2][M4];
+    // block: 64 cells (4 waves x 16) of kRowsPB consecutive rows, one row at a time (the
+    // weight staging above is amortised over the rows); grid x = row segments, y = row
+    // groups, z = images
+    const int n = blockIdx.z;
+    const int jw = blockIdx.x * 64 + wave * 16;  // this wave's first cell
+    const int j = jw + pl;                       // this lane's B cell
+    float bs0[4] = {0.f, 0.f, 0.f, 0.f}, bs1[4] = {0.f, 0.f, 0.f, 0.f}, bs2[4] = {0.f, 0.f, 0.f, 0.f};
+    const int i_end = min(Hs, (int)(blockIdx.y + 1) * kRowsPB);
+    for (int i = blockIdx.y * kRowsPB; i < i_end; ++i) {
+    f32x4 acc[2][2];
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
-        for (int v = 0; v < 2; ++v)
+        for (int v = 0; v < 2; ++v) acc[u][v] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // all channel groups unrolled (channels past C masked): the compiler can issue every
+    // group's neighbourhood loads ahead of the MFMAs
 #pragma unroll
-            for (int q = 0; q < M4; ++q) acc[u][v][q] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int c = 0; c < a.C; ++c) {
-        const ChT t = tab[c];
+    for (int g = 0; g < kMaxM / 4; ++g) {
+        const int c = 4 * g + kq;
+        const bool cv = c < a.C;
+        const ChT t = tab[cv ? c : 0];
         const bool bwd = t.xf == ISG_XF_BN_BWD;
         const float* xp = t.p + (int64_t)n * t.ns;
         const float* yp = t.y + (int64_t)n * t.yns;
@@ -288,7 +341,7 @@ __global__ __launch_bounds__(kThreads) void sub2_dgrad_kernel(DownArgs a) {
 #pragma unroll
                 for (int q = 0; q < NB; ++q) {
                     const int yy = i - R0 + r, xx = j - R0 + q;
-                    ok[r][q] = pv && (unsigned)yy < (unsigned)Hs && (unsigned)xx < (unsigned)Ws;
+                    ok[r][q] = cv && (unsigned)yy < (unsigned)Hs && (unsigned)xx < (unsigned)Ws;
                     const int64_t o = ok[r][q] ? (int64_t)yy * Ws + xx : 0;
                     rx[r][q] = gld(xp, o);
                     ry[r][q] = bwd ? gld(yp, o) : 0.f;
@@ -297,56 +350,56 @@ __global__ __launch_bounds__(kThreads) void sub2_dgrad_kernel(DownArgs a) {
             for (int r = 0; r < NB; ++r)
 #pragma unroll
                 for (int q = 0; q < NB; ++q)
-                    nb[r][q] = ok[r][q] ? ch_xform_u(t.xf, t.act, t.k, rx[r][q], ry[r][q]) : 0.f;
+                    nb[r][q] = ok[r][q] ? ch_xform(t.xf, t.act, t.k, rx[r][q], ry[r][q]) : 0.f;
         }
-        const f32x4* wc = wl + c * K * K * M4;
+        const float* wa = wl + ((4 * g + kq) * kMaxM + pl) * K * K;  // A: c = 4g + kq, m = pl
 #pragma unroll
         for (int kh = 0; kh < K; ++kh) {
-            const int au = (kh + P) & 1;                  // output row phase this tap feeds
-            const int rr = (au + P - kh) / 2 + R0;        // neighbourhood row (exact division)
+            const int au = (kh + P) & 1, rr = (au + P - kh) / 2 + R0;
 #pragma unroll
             for (int kw = 0; kw < K; ++kw) {
-                const int av = (kw + P) & 1;
-                const int qq = (av + P - kw) / 2 + R0;
-                const float d = nb[rr][qq];
-#pragma unroll
-                for (int q = 0; q < M4; ++q) acc[au][av][q] += wc[(kh * K + kw) * M4 + q] * d;
+                const int av = (kw + P) & 1, qq = (av + P - kw) / 2 + R0;
+                acc[au][av] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[kh * K + kw], nb[rr][qq], acc[au][av], 0, 0, 0);
             }
         }
     }
-    float s0[M], s1[M], s2[M];
+    // epilogue: lane holds D[m = 4kq + r][cell = pl] of every phase
+    const int jo = jw + pl;
+    const bool cok = jo < Ws;
+    float* const s0 = bs0;
+    float* const s1 = bs1;
+    float* const s2 = bs2;
 #pragma unroll
-    for (int m = 0; m < M; ++m) {
-        s0[m] = s1[m] = s2[m] = 0.f;
-        if (pv && m < a.M) {
+    for (int r = 0; r < 4; ++r) {
+        const int m = 4 * kq + r;
+        if (cok && m < a.M) {
+            const SinkRow q = ri[m];
 #pragma unroll
-            for (int u = 0; u < 2; ++u)
-#pragma unroll
-                for (int v = 0; v < 2; ++v) {
-                    float t0 = 0.f, t1 = 0.f, t2 = 0.f;
-                    sink_row_apply(ri[m], n, (int64_t)(2 * i + u) * Wd + 2 * j + v, acc[u][v][m >> 2][m & 3],
-                                   t0, t1, t2);
-                    s0[m] += t0;
-                    s1[m] += t1;
-                    s2[m] += t2;
-                }
+            for (int u = 0; u < 2; ++u) {
+                float t0 = 0.f, t1 = 0.f, t2 = 0.f;
+                sink_row_apply2(q, n, (int64_t)(2 * i + u) * Wd + 2 * jo, acc[u][0][r], acc[u][1][r], t0, t1, t2);
+                s0[r] += t0;
+                s1[r] += t1;
+                s2[r] += t2;
+            }
         }
     }
+    }  // rows
     if (sinks_need_red(a.out)) {
 #pragma unroll
-        for (int m = 0; m < M; ++m) {
-            const float t0 = wave_sum(s0[m]), t1 = wave_sum(s1[m]), t2 = wave_sum(s2[m]);
-            if (lane == 0) {
-                red[wave][0][m] = t0;
-                red[wave][1][m] = t1;
-                red[wave][2][m] = t2;
+        for (int r = 0; r < 4; ++r) {
+            const float t0 = dpp_row16_sum(bs0[r]), t1 = dpp_row16_sum(bs1[r]), t2 = dpp_row16_sum(bs2[r]);
+            if (pl == 0) {
+                red[wave][0][4 * kq + r] = t0;
+                red[wave][1][4 * kq + r] = t1;
+                red[wave][2][4 * kq + r] = t2;
             }
         }
         __syncthreads();
         if (tid < a.M) {
             float r3[3];
 #pragma unroll
-            for (int q = 0; q < 3; ++q) r3[q] = ((red[0][q][tid] + red[1][q][tid]) + red[2][q][tid]) + red[3][q][tid];
+            for (int q3 = 0; q3 < 3; ++q3) r3[q3] = ((red[0][q3][tid] + red[1][q3][tid]) + red[2][q3][tid]) + red[3][q3][tid];
             sink_row_flush(a.out, tid, r3[0], r3[1], r3[2]);
         }
     }
@@ -441,8 +494,8 @@ int32_t isg_sub2_dgrad(const isg_conv_geom* g, const isg_vtensor* dy, const floa
     DownArgs a{};
     a.dy = *dy; a.out = *dx; a.w = w;
     a.N = g->N; a.M = g->Ci; a.C = g->Co; a.H = g->OH; a.W = g->OW;
-    const dim3 grid((unsigned)(((int64_t)a.N * a.H * a.W + kThreads - 1) / kThreads));
-    hipLaunchKernelGGL((sub2_dgrad_kernel<5, 16>), grid, dim3(kThreads), 0, st, a);
+    const dim3 grid((unsigned)((a.W + 63) / 64), (unsigned)((a.H + kRowsPB - 1) / kRowsPB), (unsigned)a.N);
+    hipLaunchKernelGGL((sub2_dgrad_mfma_kernel<5>), grid, dim3(kThreads), 0, st, a);
     if (dx->fin_counter) isg_fin_note_handled();
     const int32_t e = isg_check_launch("sub2_dgrad_kernel");
     return e ? e : 1;
