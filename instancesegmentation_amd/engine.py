@@ -451,14 +451,15 @@ _BN_FUSE = _BN_FINAL and os.environ.get("ISG_BN_FUSE", "0") == "1"
 
 
 def _fork_pools(ol):
-    """Max-pool forwards depend only on their input and nothing writes what they read or
-    produce until their first consumer: fork each onto the executor's side stream and
-    join right before the first later op that reads any byte of its output."""
+    """Max-pool forwards (and the keypoint heatmaps' pool) depend only on their input and
+    nothing writes what they read or produce until their first consumer: fork each onto
+    the executor's side stream and join right before the first later op that reads any
+    byte of its output."""
     if os.environ.get("ISG_NO_SIDE_POOL", "0") == "1":
         return
     recs = ol.recs
     for i, r in enumerate(recs):
-        if r.kind != L.OP_MAXPOOL_FWD or getattr(r, "out_range", None) is None:
+        if r.kind not in (L.OP_MAXPOOL_FWD, L.OP_KP_POOL) or getattr(r, "out_range", None) is None:
             continue
         slot, lo, hi = r.out_range
         for j in range(i + 1, len(recs)):
@@ -723,11 +724,15 @@ class KpPoolOp:
 
     def fwd(self, ops):
         g = self.g
-        ops.add(Record(L.OP_KP_POOL, L.KpStem,
-                       dict(self.kp.spec(), g={"N": g.N, "H": self.H, "W": self.W}, k=self.k,
-                            out=self.out.ptr(self.c0), out_n_stride=self.out.n_stride),
-                       label="kp_pool_" + self.out.name,
-                       nbytes=4 * g.N * self.kp.nparts * self.out.H * self.out.W))
+        r = Record(L.OP_KP_POOL, L.KpStem,
+                   dict(self.kp.spec(), g={"N": g.N, "H": self.H, "W": self.W}, k=self.k,
+                        out=self.out.ptr(self.c0), out_n_stride=self.out.n_stride),
+                   label="kp_pool_" + self.out.name,
+                   nbytes=4 * g.N * self.kp.nparts * self.out.H * self.out.W)
+        o = self.out.ptr(self.c0)  # bytes written (for _fork_pools)
+        r.out_range = (o.slot, o.off, o.off + ((g.N - 1) * self.out.n_stride +
+                                               self.kp.nparts * self.out.H * self.out.W) * 4)
+        ops.add(r)
 
     def bwd(self, ops, gs):
         return  # keypoints carry no gradient
