@@ -1,0 +1,98 @@
+"""The data-parallel Trainer step on the MI355X: two ranks, one process
+each, both on the box's one GPU, exchanging over gloo (CUDA tensors) — the same
+`Trainer` code path `bench.py --gpus N` runs over RCCL: HIP-graph captured forward +
+backward part 1, the asynchronous bucket-1 all-reduce between the graphs while backward
+part 2 (the stem) runs, bucket 2, then Adam.
+
+Checked per rank after one captured step on its own sub-batch (keypoint input):
+  * the exchanged gradient equals the mean of the two ranks' local gradients (each from
+    a world-1 Trainer on the same sub-batch in the same process);
+  * parameters after Adam are identical on both ranks;
+  * BN running statistics are rank 0's on both ranks (DDP broadcast_buffers), up to the
+    fp64 statistics' atomic summation order between two runs.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    from instancesegmentation_amd.data import device_batch
+    from instancesegmentation_amd.model.segment import Segment
+    from instancesegmentation_amd.train import Trainer
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n, h, w = 2, 128, 128
+        torch.manual_seed(77)
+        init = Segment(20).state_dict()
+        xs, mask = device_batch(n, h, w, dev, seed=300 + rank, keypoints=True)
+        shapes = [tuple(t.shape) for t in xs]
+        # local reference: world-1 step on this rank's sub-batch
+        m1 = Segment(20)
+        m1.load_state_dict(init)
+        singles = [dist.new_group([r]) for r in range(world)]  # every rank creates every group
+        local = Trainer(m1, n, shapes, device=dev, process_group=singles[rank])
+        assert local.world == 1
+        local.step(xs, mask)
+        torch.cuda.synchronize()
+        g_local = (local.grad_flat.clone() * 1.0).cpu()  # grad_scale 1/(pixels*1)
+        bufs_local = local.flatb.clone().cpu()
+        # the data-parallel step
+        m2 = Segment(20)
+        m2.load_state_dict(init)
+        tr = Trainer(m2, n, shapes, device=dev).capture()
+        assert tr.world == world and len(tr.graphs) >= 3
+        tr.step(xs, mask)
+        torch.cuda.synchronize()
+        g_dp = tr.grad_flat.clone().cpu()
+        # every rank's local gradient, to form the mean
+        gl = [torch.zeros_like(g_local) for _ in range(world)]
+        dist.all_gather(gl, g_local)
+        bl = [torch.zeros_like(bufs_local) for _ in range(world)]
+        dist.all_gather(bl, bufs_local)
+        ref = sum(gl) / world
+        sc = ref.abs().max().item()
+        gerr = (g_dp.double() - ref.double()).abs().max().item() / sc
+        flat = tr.flat.clone().cpu()
+        fl = [torch.zeros_like(flat) for _ in range(world)]
+        dist.all_gather(fl, flat)
+        nbuf = bufs_local.numel()
+        berr = ((tr.flatb.cpu()[:nbuf] - bl[0]).abs() / (bl[0].abs() + 1e-3)).max().item()
+        out[rank] = (gerr, (fl[0] - fl[1]).abs().max().item(), berr, float(tr.loss()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_trainer_two_ranks_on_gpu():
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    for r in range(world):
+        gerr, perr, berr, loss = out[r]
+        print(f"rank {r}: exchanged-gradient rel err {gerr:.2e}, param diff across ranks "
+              f"{perr:.2e}, running stats vs rank 0 {berr:.2e}, loss {loss:.6f}")
+        assert np.isfinite(loss)
+        # the same gradients up to the fp32 atomics' summation order on each side
+        assert gerr < 1e-4, gerr
+        assert perr == 0.0, perr
+        assert berr < 1e-5, berr  # rank 0's statistics (fp64-atomic order noise only)
