@@ -21,6 +21,7 @@ Backward is derived op by op in reverse order:
     double-precision statistics in one pass at the end.
 """
 import ctypes
+import contextlib
 import os
 import struct
 
@@ -418,6 +419,18 @@ class Graph:
         self.ops.append(op)
         return Value([Val(out, c0, x.C, grad=x.grad)])
 
+    @contextlib.contextmanager
+    def side_branch(self):
+        """Convolutions (and max-pools) emitted inside run on the executor's side stream in the forward
+        pass (an independent residual branch: it reads only values produced before it
+        and nothing reads its output until the block's tail), see _fork_branches."""
+        n0 = len(self.ops)
+        yield
+        for op in self.ops[n0:]:
+            if not isinstance(op, (ConvOp, PoolOp)):
+                raise NotImplementedError("side branch: convolutions and max-pools only")
+            op.side = True
+
     def tail(self, terms, act="none", slope=None, out=None, c0=0, name=""):
         """out = act(sum(terms)); terms = [(Value single-seg, up)]; BN'd terms must have
         act none (the activation of a Conv(act=None), segment.py:42)."""
@@ -467,6 +480,30 @@ def _fork_pools(ol):
                 if j > i + 1:  # something to overlap with
                     r.flags |= Record.OPF_SIDE | Record.OPF_FORK_NOW
                     recs[j].flags |= Record.OPF_JOIN
+                break
+
+
+def _fork_branches(ol, side_recs):
+    """Forward records of side-branch convolutions (Graph.side_branch) run on the
+    executor's side stream, each forked at its place in the list (OPF_FORK_NOW: the side
+    stream waits for everything issued on the main stream so far, i.e. the branch
+    input). The first later main-stream record that reads any byte the branch writes —
+    its output or its BN statistics/coefficients — joins the side stream. Forward only:
+    backward sinks accumulate into shared gradient buffers."""
+    if os.environ.get("ISG_NO_SIDE_BRANCH", "0") == "1" or not side_recs:
+        return
+    recs = ol.recs
+    pos = {id(r): i for i, r in enumerate(recs)}
+    for r, ranges in side_recs:
+        r.flags |= Record.OPF_SIDE | Record.OPF_FORK_NOW
+    side_ids = {id(r) for r, _ in side_recs}
+    for r, ranges in side_recs:
+        for j in range(pos[id(r)] + 1, len(recs)):
+            if id(recs[j]) in side_ids:
+                continue
+            if any(fs == slot and lo <= off < hi for _, fs, off in recs[j].fix
+                   for slot, lo, hi in ranges):
+                recs[j].flags |= Record.OPF_JOIN
                 break
 
 
@@ -855,11 +892,20 @@ class Plan:
         fw = OpList()
         if g.stats_size:
             fw.add(Record(L.OP_MEMSET, L.MemsetRec, {"p": Ptr(S_STATS), "bytes": g.stats_size * 8}))
+        side_recs = []
         for op in g.ops:
+            i0 = len(fw.recs)
             op.fwd(fw)
             bnr = getattr(op, "bnr", None)
             if train and bnr is not None and _BN_FINAL and not getattr(op, "fused_final", False):
                 fw.add(bn_final_record([bnr], False))
+            if getattr(op, "side", False):
+                o = op.out.ptr()
+                rng = [(o.slot, o.off, o.off + ((N - 1) * op.out.n_stride +
+                                                op.out.C * op.out.H * op.out.W) * 4)]
+                if bnr is not None:
+                    rng.append((S_STATS, bnr.stats_off * 8, (bnr.ctr_fwd + 48) * 8))
+                side_recs += [(r, rng) for r in fw.recs[i0:]]
         if train and g.bns:
             items = []
             for b in g.bns:
@@ -871,6 +917,7 @@ class Plan:
                 chunk = items[i:i + L.LIST_CHUNK]
                 fw.add(Record(L.OP_BN_UPDATE, L.ListRec, {"n": len(chunk)}, L.BnUpdate, chunk))
         _fork_pools(fw)
+        _fork_branches(fw, side_recs)
         self.fwd = fw.compile()
         self.act_size = g.act_size
         self.stats_size = max(g.stats_size, 8)

@@ -180,9 +180,10 @@ class BottleneckDown2(EngineModule):
 
     def emit(self, g, x):
         name = g.mod_names[id(self)]
+        with g.side_branch():  # forward: overlaps the convs chain (engine._fork_branches)
+            r1 = g.maxpool(x, 2, name=name + ".pool")
+            r = self.convm[0].emit(g, r1)
         y = _chain(g, self.convs, x)
-        r1 = g.maxpool(x, 2, name=name + ".pool")
-        r = self.convm[0].emit(g, r1)
         kind, slope = g.act_of(self.prelu)
         return g.tail([(y, False), (r, False)], kind, slope, name=name), r1
 
@@ -204,8 +205,9 @@ class BottleneckDim_Res(EngineModule):
         self.relu = nn.ReLU(inplace=True)
 
     def emit(self, g, x):
+        with g.side_branch():  # forward: overlaps the convs chain (engine._fork_branches)
+            r = self.resconv[0].emit(g, x)
         y = _chain(g, self.convs, x)
-        r = self.resconv[0].emit(g, x)
         kind, slope = g.act_of(self.prelu if self.usePrelu else self.relu)
         return g.tail([(y, False), (r, False)], kind, slope, name=g.mod_names[id(self)])
 
@@ -284,14 +286,15 @@ class BottleneckUp_Res(EngineModule):
         if not (isinstance(up, nn.UpsamplingNearest2d) and up.scale_factor in (2, 2.0, (2, 2))
                 and c1.kernel_size == (1, 1)):
             raise NotImplementedError("uppool must be nearest x2 followed by a 1x1 conv")
+        with g.side_branch():  # forward: overlaps the convs chain (engine._fork_branches)
+            r = self.conv2[0].emit(g, x)
+            u = g.conv(c1, cat(r, mp_indices), name=name + ".uppool")
         y = self.convs[0].emit(g, x)
         kind, slope = g.act_of(self.convs[3])
         bn = self.convs[2] if isinstance(self.convs[2], nn.BatchNorm2d) else None
         y = g.conv_transpose(self.convs[1], y, bn=bn, act=kind, slope=slope,
                              name=name + ".convT")
         y = self.convs[4].emit(g, y)
-        r = self.conv2[0].emit(g, x)
-        u = g.conv(c1, cat(r, mp_indices), name=name + ".uppool")
         return g.tail([(y, False), (u, True)], "relu", None, name=name)
 
 
