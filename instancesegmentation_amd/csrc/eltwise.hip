@@ -363,6 +363,22 @@ __global__ void bn_finalize_kernel(BnFinalList items, int nitems, int bwd) {
     }
 }
 
+// one layer (the executor's per-BN-point launches): a 64-B kernel argument instead of the
+// ISG_LIST_CHUNK-item list
+__global__ void bn_finalize1_kernel(isg_bn bn, int bwd) {
+    float* out = bn.coef;
+    bn.coef = nullptr;
+    for (int c = threadIdx.x; c < bn.C; c += blockDim.x) {
+        if (!bwd) {
+            const ChanCoef k = fwd_coef(bn, nullptr, c);
+            reinterpret_cast<f32x4*>(out)[c] = f32x4{k.c0, k.c1, k.c2, 0.f};
+        } else {
+            const ChanCoef k = bwd_coef(bn, c);
+            reinterpret_cast<f32x4*>(out)[bn.C + c] = f32x4{k.c0, k.c1, k.c2, k.c3};
+        }
+    }
+}
+
 __global__ void grad_final_kernel(GradFinalList items, int nitems) {
     const int it = blockIdx.x;
     if (it >= nitems) return;
@@ -605,6 +621,12 @@ int32_t isg_bn_finalize(const isg_bn* items, int32_t nitems, int32_t bwd, isg_st
     for (int i = 0; i < nitems; ++i)
         if (!items[i].coef || !items[i].stats || (((uintptr_t)items[i].coef) & 15))
             return isg_set_error(ISG_ERR_INVALID, "bn_finalize: item %d needs stats and a 16-B aligned coef", i);
+    static const bool list_only = getenv("ISG_BNF_LIST") != nullptr;
+    if (nitems == 1 && !list_only) {
+        hipLaunchKernelGGL(bn_finalize1_kernel, dim3(1), dim3(items[0].C > 64 ? 128 : 64), 0, st,
+                           items[0], bwd ? 1 : 0);
+        return isg_check_launch("bn_finalize1_kernel");
+    }
     for (int b = 0; b < nitems; b += ISG_LIST_CHUNK) {
         const int n = nitems - b < ISG_LIST_CHUNK ? nitems - b : ISG_LIST_CHUNK;
         BnFinalList l;

@@ -629,6 +629,152 @@ bool pwx_src_ok(const isg_vtensor& v, int HW) {
     return true;
 }
 
+
+// ---- thin pointwise (K, M <= 16) on the VALU ---------------------------------------------
+// The 4 <-> 16 channel 1x1 layers of the stride-4 decoder (bottle5_*, 2 x 256^2 pixels)
+// move 10-19 MB each but ran at 0.4-0.5 TB/s on the MFMA kernels: a 16-row tile pads K = 4
+// to 16 and every workgroup runs the whole LDS phase chain for 64 pixels. Here one lane
+// owns 4 consecutive pixels: its K channel quads are loaded with 16-B loads all at once
+// (the producer's transform applied per element), the M x K weights are broadcast from LDS
+// as f32x4 along m, and every output row goes through its sink with one 16-B access per
+// operand. One-wave workgroups: the BN partials are a wave reduction.
+struct ThinPwArgs {
+    isg_vtensor src;
+    isg_sinks out;
+    const float* w;
+    int rs, cs;
+    int HW;
+    int64_t Q;  // pixel quads
+};
+
+typedef f32x4 __attribute__((address_space(1)))* gf32x4_p;
+
+ISG_DEV void sink_row_apply4(const SinkRow& q, int n, int64_t pix, f32x4 v, float& s0, float& s1,
+                             float& s2) {
+    const int64_t off = (int64_t)n * q.ns + pix;
+    s0 = s1 = s2 = 0.f;
+    if (q.mode == ISG_SINK_STORE) {
+        v += q.bias;
+        *(gf32x4_p)((gfloat_p)q.p + off) = v;
+        s0 = (v[0] + v[1]) + (v[2] + v[3]);
+        s1 = (v[0] * v[0] + v[1] * v[1]) + (v[2] * v[2] + v[3] * v[3]);
+    } else if (q.mode == ISG_SINK_ACCUM) {
+        const f32x4 o = gld4(q.p, off);
+        *(gf32x4_p)((gfloat_p)q.p + off) = o + v;
+        s0 = (v[0] + v[1]) + (v[2] + v[3]);
+        s1 = (v[0] * v[0] + v[1] * v[1]) + (v[2] * v[2] + v[3] * v[3]);
+    } else if (q.mode == ISG_SINK_ACTBWD) {
+        const f32x4 y = gld4(q.y, (int64_t)n * q.yns + pix);
+        f32x4 g;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float z = (y[e] - q.f.mean) * q.f.scale + q.f.beta;
+            float gv = v[e];
+            if (q.act == ISG_ACT_RELU) {
+                gv = z > 0.f ? v[e] : 0.f;
+            } else if (q.act == ISG_ACT_PRELU) {
+                gv = z > 0.f ? v[e] : v[e] * q.f.slope;
+                s2 += z > 0.f ? 0.f : z * v[e];
+            }
+            g[e] = gv;
+            s0 += gv;
+            s1 += gv * (y[e] - q.f.mean);
+        }
+        *(gf32x4_p)((gfloat_p)q.p + off) = g;
+    }
+}
+
+template <int K, int M>
+__global__ __launch_bounds__(64) void thin_pw_kernel(ThinPwArgs a) {
+    constexpr int M4 = M / 4;
+    __shared__ f32x4 wl[K * M4];  // [k][m/4]
+    __shared__ ChT tab[K];
+    __shared__ SinkRow ri[M];
+    const int lane = threadIdx.x;
+    if (lane < K) tab[lane] = ch_table_entry(a.src, lane, a.HW);
+    if (lane < M) ri[lane] = sink_row(a.out, lane, a.HW);
+    float* const wf = reinterpret_cast<float*>(wl);
+    for (int i = lane; i < K * M; i += 64) {
+        const int k = i / M, m = i - k * M;
+        wf[i] = gld(a.w, (int64_t)m * a.rs + (int64_t)k * a.cs);
+    }
+    __syncthreads();
+    const int64_t qd = (int64_t)blockIdx.x * 64 + lane;
+    const bool pv = qd < a.Q;
+    const int64_t p = (pv ? qd : 0) * 4;
+    const int n = (int)(p / a.HW);
+    const int pix = (int)(p - (int64_t)n * a.HW);
+    f32x4 raw[K], ry[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {  // every load in flight together (y == p unless BN-backward)
+        const ChT t = tab[k];
+        const int yns = t.y == t.p ? t.ns : t.yns;
+        raw[k] = gld4(t.p, (int64_t)n * t.ns + pix);
+        ry[k] = gld4(t.y, (int64_t)n * yns + pix);
+    }
+    f32x4 acc[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const ChT t = tab[k];
+        f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = ch_xform_u(t.xf, t.act, t.k, raw[k][e], ry[k][e]);
+#pragma unroll
+        for (int q = 0; q < M4; ++q) {
+            const f32x4 w4 = wl[k * M4 + q];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[q * 4 + j] += w4[j] * v;
+        }
+    }
+    const bool red = sinks_need_red(a.out);
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+        float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+        if (pv) sink_row_apply4(ri[m], n, pix, acc[m], s0, s1, s2);
+        if (red) {
+            s0 = wave_sum(s0);
+            s1 = wave_sum(s1);
+            s2 = wave_sum(s2);
+            if (lane == m) sink_row_flush(a.out, m, s0, s1, s2);
+        }
+    }
+}
+
+bool sinks_aligned16(const isg_sinks& sk) {
+    for (int s = 0; s < sk.nsink; ++s) {
+        const isg_sink& k = sk.s[s];
+        if (k.mode == ISG_SINK_NONE) continue;
+        if (!aligned16(k.p) || k.n_stride % 4) return false;
+        if (k.mode == ISG_SINK_ACTBWD && (!aligned16(k.y) || k.y_n_stride % 4)) return false;
+    }
+    return true;
+}
+
+// 1: launched, 0: not applicable, < 0: error
+int32_t thin_pw(const PwArgs& a, hipStream_t st) {
+    static const bool off = getenv("ISG_NO_THIN_PW") != nullptr;
+    if (off || a.HW % 4 || a.out.fin_counter || !pwx_src_ok(a.src, a.HW) || !sinks_aligned16(a.out))
+        return 0;
+    ThinPwArgs b{};
+    b.src = a.src; b.out = a.out; b.w = a.w; b.rs = a.rs; b.cs = a.cs; b.HW = a.HW;
+    b.Q = a.P / 4;
+    const dim3 grid((unsigned)((b.Q + 63) / 64));
+#define ISG_THIN_PW(KK, MM)                                                          \
+    if (a.K == KK && a.M == MM) {                                                    \
+        hipLaunchKernelGGL((thin_pw_kernel<KK, MM>), grid, dim3(64), 0, st, b);     \
+        const int32_t e = isg_check_launch("thin_pw_kernel");                        \
+        return e ? e : 1;                                                            \
+    }
+    ISG_THIN_PW(4, 16)
+    ISG_THIN_PW(16, 4)
+    ISG_THIN_PW(4, 4)
+    ISG_THIN_PW(8, 8)
+    ISG_THIN_PW(16, 16)
+#undef ISG_THIN_PW
+    return 0;
+}
 }  // namespace
 
 ISG_STAMP_ACCESSOR(isg_dbg_stamps_pw)
@@ -651,6 +797,10 @@ int32_t isg_pw_gemm(const isg_conv_geom* g, const isg_vtensor* src, const float*
         return isg_set_error(ISG_ERR_UNSUPPORTED, "pw gemm: K = %d channels > %d", a.K, kMaxK);
     if (a.M > 2 * kMaxBM)
         return isg_set_error(ISG_ERR_UNSUPPORTED, "pw gemm: M = %d rows", a.M);
+    {  // thin layers (K, M <= 16) on the VALU
+        const int32_t t = thin_pw(a, st);
+        if (t != 0) return t < 0 ? t : 0;
+    }
     static const bool slab_off = getenv("ISG_PW_CHUNKED") != nullptr;
     int wmode = 0;
     if (aligned16(w)) {

@@ -61,6 +61,12 @@ DENSE = [
     (96, 48, 16, 16, 1, 1, 0, 1),
     (48, 128, 16, 16, 1, 1, 0, 1),
     (16, 16, 20, 20, 3, 1, 2, 2),
+    # thin pointwise (pw_gemm.hip thin_pw_kernel: K, M <= 16, HW % 4 == 0; 5x7 falls back)
+    (4, 16, 64, 64, 1, 1, 0, 1),
+    (16, 4, 36, 20, 1, 1, 0, 1),
+    (8, 8, 10, 6, 1, 1, 0, 1),
+    (16, 16, 24, 24, 1, 1, 0, 1),
+    (4, 4, 5, 7, 1, 1, 0, 1),
     # tap_conv coverage: Ci % 4 != 0, 3 row tiles, ragged edges, multi-tile grids
     (3, 16, 64, 48, 5, 2, 2, 1),
     (16, 36, 33, 45, 3, 1, 1, 1),
