@@ -813,7 +813,10 @@ int32_t isg_pw_gemm(const isg_conv_geom* g, const isg_vtensor* src, const float*
     // per-workgroup phase chain loses to the chunked kernel (the 128 -> 48 dgrads
     // 12.2 -> 17.0 us, the 256 -> 128 resconv forward 27.6 -> 49.5 us)
     static const bool slab_all = getenv("ISG_PW_SLAB_ALL") != nullptr;
-    const bool slab_pays = slab_all || (!dgrad && a.P >= 65536) || (dgrad && a.M <= 64 && a.K <= 128);
+    // (r02g per-op tables: the 64^2 128 -> 48 forwards 13.8 -> 12.5 us on the slab)
+    static const bool fwd_small = getenv("ISG_NO_PW_FWD_SLAB_SMALL") == nullptr;
+    const bool slab_pays = slab_all || (!dgrad && a.P >= 65536) || (dgrad && a.M <= 64 && a.K <= 128) ||
+                           (fwd_small && !dgrad && a.M <= 64 && a.K <= 128);
     if (!slab_off && slab_pays && wmode && pwx_src_ok(*src, a.HW)) {
         PwxArgs b{};
         b.src = a.src; b.out = a.out; b.w = w; b.rs = a.rs; b.cs = a.cs;
