@@ -691,12 +691,13 @@ __global__ __launch_bounds__(64) void thin_pw_kernel(ThinPwArgs a) {
     __shared__ ChT tab[K];
     __shared__ SinkRow ri[M];
     const int lane = threadIdx.x;
+    const int m0 = blockIdx.y * M;  // this workgroup's M output rows
     if (lane < K) tab[lane] = ch_table_entry(a.src, lane, a.HW);
-    if (lane < M) ri[lane] = sink_row(a.out, lane, a.HW);
+    if (lane < M) ri[lane] = sink_row(a.out, m0 + lane, a.HW);
     float* const wf = reinterpret_cast<float*>(wl);
     for (int i = lane; i < K * M; i += 64) {
         const int k = i / M, m = i - k * M;
-        wf[i] = gld(a.w, (int64_t)m * a.rs + (int64_t)k * a.cs);
+        wf[i] = gld(a.w, (int64_t)(m0 + m) * a.rs + (int64_t)k * a.cs);
     }
     __syncthreads();
     const int64_t qd = (int64_t)blockIdx.x * 64 + lane;
@@ -737,7 +738,7 @@ __global__ __launch_bounds__(64) void thin_pw_kernel(ThinPwArgs a) {
             s0 = wave_sum(s0);
             s1 = wave_sum(s1);
             s2 = wave_sum(s2);
-            if (lane == m) sink_row_flush(a.out, m, s0, s1, s2);
+            if (lane == m) sink_row_flush(a.out, m0 + m, s0, s1, s2);
         }
     }
 }
@@ -760,9 +761,14 @@ int32_t thin_pw(const PwArgs& a, hipStream_t st) {
     ThinPwArgs b{};
     b.src = a.src; b.out = a.out; b.w = a.w; b.rs = a.rs; b.cs = a.cs; b.HW = a.HW;
     b.Q = a.P / 4;
-    const dim3 grid((unsigned)((b.Q + 63) / 64));
+    // opt-in: M = 32, 48, 64 as 16-row tiles on grid.y (the input quads re-read from L2).
+    // Measured slower in the step (r02h: 374 -> 362 images/s; the 128^2 16 -> 48 layers
+    // stay on the MFMA kernels)
+    static const bool tile_on = getenv("ISG_THIN_PW_TILE") != nullptr;
+    const int mt = tile_on && a.M > 16 && a.M % 16 == 0 && a.M <= 64 ? 16 : a.M;
+    const dim3 grid((unsigned)((b.Q + 63) / 64), (unsigned)(a.M / mt));
 #define ISG_THIN_PW(KK, MM)                                                          \
-    if (a.K == KK && a.M == MM) {                                                    \
+    if (a.K == KK && mt == MM) {                                                     \
         hipLaunchKernelGGL((thin_pw_kernel<KK, MM>), grid, dim3(64), 0, st, b);     \
         const int32_t e = isg_check_launch("thin_pw_kernel");                        \
         return e ? e : 1;                                                            \

@@ -67,6 +67,8 @@ DENSE = [
     (8, 8, 10, 6, 1, 1, 0, 1),
     (16, 16, 24, 24, 1, 1, 0, 1),
     (4, 4, 5, 7, 1, 1, 0, 1),
+    (16, 48, 24, 20, 1, 1, 0, 1),
+    (4, 32, 16, 12, 1, 1, 0, 1),
     # tap_conv coverage: Ci % 4 != 0, 3 row tiles, ragged edges, multi-tile grids
     (3, 16, 64, 48, 5, 2, 2, 1),
     (16, 36, 33, 45, 3, 1, 1, 1),
