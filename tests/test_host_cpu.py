@@ -222,6 +222,7 @@ def test_forward_side_branches_fork_and_join():
         if readers:  # a join between the fork and the first main-stream reader
             assert any(recs[j].flags & Record.OPF_JOIN for j in range(i + 1, readers[0] + 1)), \
                 op.out.name
-    # backward records never use the side stream for branch work (shared dx sinks)
+    # backward: no branch work on the side stream (shared dx sinks); only bucket 1's
+    # replica fold and gradient finalisation fork there (after every statistic is done)
     assert not any(r.flags & Record.OPF_FORK_NOW for r in p.bwd.recs
-                   if r.kind not in (L.OP_MAXPOOL_FWD, L.OP_KP_POOL))
+                   if r.kind not in (L.OP_SUM_REP, L.OP_GRAD_FINAL))
