@@ -138,9 +138,9 @@ def pmc_traffic(label, args):
 def infer_scene(H, W, persons, dups, seed=11):
     """A crowded synthetic image (BASELINE config 4, OCHuman-style): `persons` overlapping
     person boxes with 17 keypoints each, plus `dups` repeated detections of the same people
-    that mask-NMS must suppress. (Repeats are exact: the random-init network's masks are
-    high-frequency textures, so a few-pixel jitter already decorrelates them below IoU
-    0.5; a trained network's blob-shaped masks would not need that.)"""
+    with a few-pixel jitter of box (+/-3 px) and keypoints (+/-2 px) — an over-complete
+    detector's output, so mask-NMS ranks and compares genuinely different masks (exact
+    repeats would make every duplicate's IoU exactly 1)."""
     import numpy as np
     rng = np.random.Generator(np.random.PCG64(seed))
     img = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
@@ -155,10 +155,10 @@ def infer_scene(H, W, persons, dups, seed=11):
         kp[:, 2] = rng.uniform(size=17) < 0.8
         boxes.append(b)
         kps.append(kp)
-    for i in range(dups):  # repeated detections of the same people (identical prompts)
+    for i in range(dups):  # repeated, jittered detections of the same people
         j = i % persons
-        boxes.append(list(boxes[j]))
-        kps.append(kps[j].copy())
+        boxes.append([v + int(rng.integers(-3, 4)) for v in boxes[j]])
+        kps.append(kps[j] + np.array([rng.uniform(-2, 2), rng.uniform(-2, 2), 0.0]))
     return img, np.asarray(boxes), np.asarray(kps)
 
 
@@ -227,7 +227,7 @@ def infer_bench(dev, reps=20):
             "masks_per_s": round(K / (ms * 1e-3), 1), "ms_per_image": round(ms, 3),
             "nms_p50_ms": round(float(np.median(t_nms)), 4), "instances": K, "kept": len(keep),
             "nonempty_masks": nonempty,
-            "config": "OCHuman-crowded synthetic: 8 people + 8 repeated detections; "
+            "config": "OCHuman-crowded synthetic: 8 people + 8 jittered repeat detections; "
                       "random-init Segment(20), BN statistics calibrated on the scene",
             "dtype": "f32", "data": "synthetic"}
 

@@ -44,19 +44,27 @@ ISG_DEV int rep_of_block() {
 }
 // pointer to this workgroup's replica of an accumulator of n values
 ISG_DEV double* rep_ptr(double* base, int n) { return base + (int64_t)rep_of_block() * n; }
-// sum over replicas of element i of an accumulator of n values
-ISG_DEV double rep_sum(const double* base, int n, int i) {
+// sum over replicas of element i of an accumulator of n values. fresh: read inside the
+// launch whose workgroups are still adding to it (the fused finalisation's last
+// workgroup): agent-scope loads (global_load sc1, past this CU's L1) of values that only
+// agent-scope atomics wrote (performed past every XCD's L2), so no release/acquire fence
+// pair is needed (MI355X_MICROARCH.md, inter-workgroup visibility, hand-off row 1).
+ISG_DEV double rep_sum(const double* base, int n, int i, bool fresh = false) {
     double s = 0.0;
 #pragma unroll
-    for (int r = 0; r < ISG_STAT_REP; ++r) s += base[(int64_t)r * n + i];
+    for (int r = 0; r < ISG_STAT_REP; ++r) {
+        const double* p = base + (int64_t)r * n + i;
+        s += fresh ? __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                   : *p;
+    }
     return s;
 }
 
-ISG_DEV void bn_mean_rstd(const isg_bn& bn, int c, double& mean, double& rstd) {
+ISG_DEV void bn_mean_rstd(const isg_bn& bn, int c, double& mean, double& rstd, bool fresh = false) {
     if (bn.train) {
         double inv = 1.0 / (double)bn.count;
-        mean = rep_sum(bn.stats, 4 * bn.C, c) * inv;
-        double var = rep_sum(bn.stats, 4 * bn.C, bn.C + c) * inv - mean * mean;
+        mean = rep_sum(bn.stats, 4 * bn.C, c, fresh) * inv;
+        double var = rep_sum(bn.stats, 4 * bn.C, bn.C + c, fresh) * inv - mean * mean;
         if (var < 0.0) var = 0.0;
         rstd = 1.0 / sqrt(var + (double)bn.eps);
     } else {
@@ -66,13 +74,13 @@ ISG_DEV void bn_mean_rstd(const isg_bn& bn, int c, double& mean, double& rstd) {
 }
 
 // forward coefficients of a BN_FWD segment channel
-ISG_DEV ChanCoef fwd_coef(const isg_bn& bn, const float* slope, int c) {
+ISG_DEV ChanCoef fwd_coef(const isg_bn& bn, const float* slope, int c, bool fresh = false) {
     if (bn.coef) {  // finalised once per layer (isg_bn_finalize)
         const f32x4 f = reinterpret_cast<const f32x4*>(bn.coef)[c];
         return ChanCoef{f[0], f[1], f[2], slope ? slope[c] : 0.f};
     }
     double mean, rstd;
-    bn_mean_rstd(bn, c, mean, rstd);
+    bn_mean_rstd(bn, c, mean, rstd, fresh);
     ChanCoef k;
     k.c0 = (float)mean;
     k.c1 = (float)((double)bn.gamma[c] * rstd);
@@ -82,19 +90,19 @@ ISG_DEV ChanCoef fwd_coef(const isg_bn& bn, const float* slope, int c) {
 }
 
 // backward coefficients: dy = A*g + B*(y-mean) + C
-ISG_DEV ChanCoef bwd_coef(const isg_bn& bn, int c) {
+ISG_DEV ChanCoef bwd_coef(const isg_bn& bn, int c, bool fresh = false) {
     if (bn.coef) {
         const f32x4 f = reinterpret_cast<const f32x4*>(bn.coef)[bn.C + c];
         return ChanCoef{f[0], f[1], f[2], f[3]};
     }
     double mean, rstd;
-    bn_mean_rstd(bn, c, mean, rstd);
+    bn_mean_rstd(bn, c, mean, rstd, fresh);
     double gam = (double)bn.gamma[c];
     ChanCoef k;
     if (bn.train) {
         double inv = 1.0 / (double)bn.count;
-        double gs = rep_sum(bn.stats, 4 * bn.C, 2 * bn.C + c);
-        double gxs = rep_sum(bn.stats, 4 * bn.C, 3 * bn.C + c);  // sum g*(y - mean), centred
+        double gs = rep_sum(bn.stats, 4 * bn.C, 2 * bn.C + c, fresh);
+        double gxs = rep_sum(bn.stats, 4 * bn.C, 3 * bn.C + c, fresh);  // sum g*(y - mean), centred
         double mg = gs * inv;
         double mgx = rstd * gxs * inv;         // mean(g * xhat)
         k.c0 = (float)(gam * rstd);
@@ -108,6 +116,18 @@ ISG_DEV ChanCoef bwd_coef(const isg_bn& bn, int c) {
         k.c3 = 0.f;
     }
     return k;
+}
+
+// A keypoint coordinate made safe for the reference's int() window bounds
+// (train_instance.py:52-58): false for NaN / infinity (the reference's int() raises; the
+// part is treated as not visible), else v clamped to [-(r + 2), extent + r + 2], which
+// leaves the window [max(0,int(v-r)), min(extent-1,int(v+r+1))) unchanged — empty
+// beyond those bounds either way — while keeping the int conversions defined.
+ISG_DEV bool kp_coord(double& v, double r, int extent) {
+    if (!(v == v) || v - v != 0.0) return false;
+    const double lo = -(r + 2.0), hi = (double)extent + r + 2.0;
+    v = v < lo ? lo : (v > hi ? hi : v);
+    return true;
 }
 
 ISG_DEV float apply_act(float v, int act, float slope) {
@@ -289,21 +309,23 @@ ISG_DEV bool sinks_need_red(const isg_sinks& sk) {
 
 // ---- fused BatchNorm finalisation ---------------------------------------------------
 // Every thread of every workgroup of a launch whose sinks carry fin_mode calls this LAST
-// (no early return before it). After the workgroup barrier, an agent-scope release fence
-// orders the workgroup's statistics atomics before its ticket; the last arriver acquires. Tickets are two
+// (no early return before it). The handed-off bytes are the statistics, which every
+// workgroup writes ONLY with agent-scope atomic adds (performed past the XCD L2s): each
+// wave waits for its own atomics (vmcnt(0)), the workgroup barrier orders all waves
+// before lane 0's ticket add, and the last arriver reads the statistics with agent-scope
+// (sc1) loads (rep_sum fresh) — hand-off row 1 of MI355X_MICROARCH.md's inter-workgroup
+// table, with no release fence (an L2 write-back per workgroup, which had made this
+// fusion slower than the separate finalisation launch it replaces). Tickets are two
 // level — 32 sub-counters, the last arriver of each bumps the top counter — so at most
 // ~nb/32 workgroups contend on one address. The workgroup that completes the top counter
-// acquires and evaluates the coefficients (fp64, isg_bn_finalize's math), then re-zeroes
-// the counters. Counter block: ISG_FIN_CTR uint32 (top, then 32 subs), zeroed.
+// evaluates the coefficients (fp64, isg_bn_finalize's math), then re-zeroes the
+// counters. Counter block: ISG_FIN_CTR uint32 (top, then 32 subs), zeroed.
 #define ISG_FIN_SUBS 32
 ISG_DEV bool fin_last_block(uint32_t* ctr) {
     __shared__ int s_last;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0 && threadIdx.y == 0) {
-        // release: every statistics write of this workgroup is ordered before its ticket
-        // (the HIP memory model's guarantee, not an assumption about where atomics land)
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         const unsigned nb = gridDim.x * gridDim.y * gridDim.z;
         const unsigned b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
         bool last;
@@ -314,10 +336,6 @@ ISG_DEV bool fin_last_block(uint32_t* ctr) {
             const unsigned ns = nb / ISG_FIN_SUBS + (sub < nb % ISG_FIN_SUBS ? 1u : 0u);
             last = __hip_atomic_fetch_add(ctr + 1 + sub, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ns - 1 &&
                    __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ISG_FIN_SUBS - 1;
-        }
-        if (last) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         s_last = last ? 1 : 0;
     }
@@ -334,10 +352,10 @@ ISG_DEV void fin_sink(const isg_sink& k) {
     bn.coef = nullptr;  // evaluate from the statistics
     for (int c = tid; c < bn.C; c += nt) {
         if (k.fin_mode == 1) {
-            const ChanCoef f = fwd_coef(bn, nullptr, c);
+            const ChanCoef f = fwd_coef(bn, nullptr, c, true);
             reinterpret_cast<f32x4*>(out)[c] = f32x4{f.c0, f.c1, f.c2, 0.f};
         } else {
-            const ChanCoef f = bwd_coef(bn, c);
+            const ChanCoef f = bwd_coef(bn, c, true);
             reinterpret_cast<f32x4*>(out)[bn.C + c] = f32x4{f.c0, f.c1, f.c2, f.c3};
         }
     }

@@ -79,7 +79,8 @@ __global__ __launch_bounds__(kThreads) void heatmap_kernel(const double* __restr
     const int kpart = blockIdx.x;  // instance * nparts + part
     const double* q = kp + (int64_t)kpart * 3;
     if (!(q[2] > 0.0)) return;  // not 'vis'
-    const double x = q[0], y = q[1];
+    double x = q[0], y = q[1];
+    if (!kp_coord(x, r, W) || !kp_coord(y, r, H)) return;  // non-finite: not visible
     // python int() truncates toward zero
     const int xmin = max(0, (int)(x - r)), xmax = min(W - 1, (int)(x + r + 1.0));
     const int ymin = max(0, (int)(y - r)), ymax = min(H - 1, (int)(y + r + 1.0));

@@ -64,7 +64,7 @@ ISG_DEV Win part_window(const KpArgs& a, int n, int j) {
     Win w;
     w.kx = q[0];
     w.ky = q[1];
-    if (!(q[2] > 0.0)) {
+    if (!(q[2] > 0.0) || !kp_coord(w.kx, a.r, a.W) || !kp_coord(w.ky, a.r, a.H)) {
         w.x0 = w.y0 = 0;
         w.x1 = w.y1 = 0;
         return w;

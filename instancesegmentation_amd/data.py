@@ -15,10 +15,14 @@ N_PARTS = 17
 
 def keypoint_heatmaps(points, h, w, sigma=10.0, threshold=0.01):
     """train_instance.py:33-68 semantics (see oracle/heatmaps_oracle.py for the pinned
-    restatement): visible parts only; window [max(0,int(x-r)), min(w-1,int(x+r+1)))."""
+    restatement): visible parts only; window [max(0,int(x-r)), min(w-1,int(x+r+1))).
+    A non-finite coordinate (where the reference's int() raises) marks the part as not
+    visible — the same rule as the GPU kernels (common.h kp_coord)."""
     r = math.sqrt(math.log(threshold) * (-sigma ** 2))
     maps = np.zeros((N_PARTS, h, w), np.float32)
     for part, (x, y) in points.items():
+        if not (math.isfinite(x) and math.isfinite(y)):
+            continue
         x0, x1 = max(0, int(x - r)), min(w - 1, int(x + r + 1))
         y0, y1 = max(0, int(y - r)), min(h - 1, int(y + r + 1))
         if x1 <= x0 or y1 <= y0:
@@ -212,19 +216,24 @@ class InstanceCommonDataset(torch.utils.data.Dataset):
     """train_instance.py:71-216 on the common-dataset layout, without imgaug/ymlib.
 
     __getitem__ returns (image_tensor [3,480,480] in [-1,1], mask_tensor [1,480,480] in
-    [0,1], out) like the reference; out also carries 'heatmaps' [17,480,480] (the
-    reference computes them, :202, and drops them — Segment(20) needs them). The
+    [0,1], out) like the reference; out also carries 'keypoints' [17,3] float64 in crop
+    coordinates and, with_heatmaps, 'heatmaps' [17,480,480] (the reference computes them
+    from the keypoints, :200-202, and drops them — Segment(20) needs them). The
     augmentation is the reference's active one (both branches, :148-196; the random ones
     are commented out there): translate the box centre to the image centre, crop/pad to
     the instance mask's box +/- 16 px, resize to 480x480 — one resampling, the same
     contract as the GPU crop kernel."""
 
-    def __init__(self, dataset_dir, test: bool = False) -> None:
+    def __init__(self, dataset_dir, test: bool = False, with_heatmaps: bool = True) -> None:
         super().__init__()
         import glob
         import json
         import os
         self.test = test
+        # False: out carries only the crop-space keypoints [17,3] (x, y, visible), from
+        # which the GPU stem synthesises the same heatmaps (kp_stem.hip) — the dense
+        # 17 x 480 x 480 maps are then neither computed on the host nor copied to HBM
+        self.with_heatmaps = with_heatmaps
         self.out_size = (480, 480)
         self.root = dataset_dir
         self.results = []
@@ -265,13 +274,15 @@ class InstanceCommonDataset(torch.utils.data.Dataset):
         kp = _keypoint_table(ckey(r, "body_keypoint", {}) or {})
         kp[:, 0] = (kp[:, 0] - win[0]) * S / (win[2] - win[0])
         kp[:, 1] = (kp[:, 1] - win[1]) * S / (win[3] - win[1])
-        pts = {j: (kp[j, 0], kp[j, 1]) for j in range(N_PARTS) if kp[j, 2] > 0}
-        heatmaps = keypoint_heatmaps(pts, S, S)
+        kp[:, 2] = (kp[:, 2] > 0).astype(np.float64)
         image_tensor = torch.from_numpy(
             ((img_c.astype(np.float32) / np.float32(255.0) - np.float32(0.5)) / np.float32(0.5))
             .transpose(2, 0, 1).copy())
         mask_tensor = torch.from_numpy((mask_c.astype(np.float32) / np.float32(255.0))[None])
-        out = {"image": img_c, "mask": mask_c, "heatmaps": torch.from_numpy(heatmaps)}
+        out = {"image": img_c, "mask": mask_c, "keypoints": torch.from_numpy(kp)}
+        if self.with_heatmaps:
+            pts = {j: (kp[j, 0], kp[j, 1]) for j in range(N_PARTS) if kp[j, 2] > 0}
+            out["heatmaps"] = torch.from_numpy(keypoint_heatmaps(pts, S, S))
         return image_tensor, mask_tensor, out
 
 

@@ -463,11 +463,21 @@ _BN_FINAL = os.environ.get("ISG_NO_BN_FINAL", "0") != "1"  # debugging switch
 _BN_FUSE = _BN_FINAL and os.environ.get("ISG_BN_FUSE", "0") == "1"
 
 
+def _buf_range(buf):
+    """(slot, lo, hi): the byte range of a whole arena buffer. A pool writes a channel slice
+    of its output buffer, but a later record's pointer into that buffer names only where
+    its own access STARTS (e.g. channel 0 of a concat it reads whole): any pointer into the
+    buffer counts as touching the slice, so the join can never be placed after a reader
+    whose start lies below the slice."""
+    o = buf.ptr(0)
+    return (o.slot, o.off, o.off + buf.numel * 4)
+
+
 def _fork_pools(ol):
     """Max-pool forwards (and the keypoint heatmaps' pool) depend only on their input and
     nothing writes what they read or produce until their first consumer: fork each onto
-    the executor's side stream and join right before the first later op that reads any
-    byte of its output."""
+    the executor's side stream and join right before the first later op that touches its
+    output buffer (out_range = the whole buffer, _buf_range)."""
     if os.environ.get("ISG_NO_SIDE_POOL", "0") == "1":
         return
     recs = ol.recs
@@ -766,9 +776,7 @@ class KpPoolOp:
                         out=self.out.ptr(self.c0), out_n_stride=self.out.n_stride),
                    label="kp_pool_" + self.out.name,
                    nbytes=4 * g.N * self.kp.nparts * self.out.H * self.out.W)
-        o = self.out.ptr(self.c0)  # bytes written (for _fork_pools)
-        r.out_range = (o.slot, o.off, o.off + ((g.N - 1) * self.out.n_stride +
-                                               self.kp.nparts * self.out.H * self.out.W) * 4)
+        r.out_range = _buf_range(self.out)  # for _fork_pools
         ops.add(r)
 
     def bwd(self, ops, gs):
@@ -787,10 +795,7 @@ class PoolOp:
                     "out": self.out.ptr(self.c0), "out_ns": self.out.n_stride},
                    label=self.out.name,
                    nbytes=4 * g.N * self.x.C * (self.x.H * self.x.W + self.out.H * self.out.W))
-        # bytes this op writes (for _fork_pools): its channels of every image
-        o = self.out.ptr(self.c0)
-        hw = self.out.H * self.out.W
-        r.out_range = (o.slot, o.off, o.off + ((g.N - 1) * self.out.n_stride + self.x.C * hw) * 4)
+        r.out_range = _buf_range(self.out)  # for _fork_pools
         ops.add(r)
 
     def bwd(self, ops, gs):
@@ -900,9 +905,7 @@ class Plan:
             if train and bnr is not None and _BN_FINAL and not getattr(op, "fused_final", False):
                 fw.add(bn_final_record([bnr], False))
             if getattr(op, "side", False):
-                o = op.out.ptr()
-                rng = [(o.slot, o.off, o.off + ((N - 1) * op.out.n_stride +
-                                                op.out.C * op.out.H * op.out.W) * 4)]
+                rng = [_buf_range(op.out)]
                 if bnr is not None:
                     rng.append((S_STATS, bnr.stats_off * 8, (bnr.ctr_fwd + 48) * 8))
                 side_recs += [(r, rng) for r in fw.recs[i0:]]

@@ -48,6 +48,7 @@ from .engine import S_ACT, S_IN, S_OUT, S_STATS, S_TENSOR0, Plan
 CROP = 480   # train_instance.py:77
 PAD = 16     # train_instance.py:167
 N_PARTS = 17
+NMS_MAX = 256  # masks one isg_mask_nms launch can rank (include/isg.h)
 
 
 class InstanceSegmenter:
@@ -258,12 +259,24 @@ def main(argv=None):
         img = np.asarray(Image.open(filepath).convert("RGB"))
         boxes, kps = read_instances(os.path.join(dirname, basename + ".json"))
         H, W = img.shape[:2]
-        eng = engines.get((H, W))
+        # one greedy NMS over ALL instances of the image: the capacity grows (doubling
+        # from --max-instances, one captured engine per capacity) up to the NMS kernel's
+        # limit of NMS_MAX masks; only beyond that is the image split into chunks, each
+        # with its own NMS (duplicates in different chunks are then not suppressed; the
+        # output JSON says so)
+        cap = max(1, args.max_instances)
+        while cap < min(len(boxes), NMS_MAX):
+            cap *= 2
+        cap = min(cap, NMS_MAX) if len(boxes) > args.max_instances else cap
+        eng = engines.get((H, W, cap))
         if eng is None:
-            eng = engines[(H, W)] = InstanceSegmenter(model, (H, W), args.max_instances,
-                                                      args.iou)
+            eng = engines[(H, W, cap)] = InstanceSegmenter(model, (H, W), cap, args.iou)
         res = {"image": os.path.basename(filepath), "instances": len(boxes), "keep": [],
                "scores": []}
+        if len(boxes) > eng.K:
+            print(f"warning: {basename}: {len(boxes)} instances > {eng.K}: mask-NMS runs per "
+                  f"chunk of {eng.K}")
+            res["nms"] = f"per chunk of {eng.K}"
         if len(boxes):
             for b0 in range(0, len(boxes), eng.K):
                 masks, keep, scores = eng(img, boxes[b0:b0 + eng.K], kps[b0:b0 + eng.K])

@@ -162,6 +162,7 @@ class Trainer:
         self.target = torch.empty(self.plan.out_shapes[0], dtype=torch.float32, device=dev)
         self.table = self._make_table()
         self.graphs = None
+        self._captured = (None, None)
         self.events = []
         self.split = None
 
@@ -184,6 +185,10 @@ class Trainer:
         return tab
 
     # ---- the step body -------------------------------------------------------------
+    def _hyper(self):
+        return (float(self.lr), tuple(float(b) for b in self.betas), float(self.eps),
+                float(self.wd))
+
     def _adam(self):
         L.check(L.lib().isg_adam_dev(self.flat.data_ptr(), self.grad_flat.data_ptr(),
                                      self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(),
@@ -273,6 +278,7 @@ class Trainer:
         if warm:
             self.warm()
         torch.cuda.synchronize(self.device)
+        self._captured = (split, self._hyper())
         plan = []
         cur = []
         for u in self._schedule(split) + ["end"]:
@@ -380,6 +386,10 @@ class Trainer:
                 assert st["exp_avg"].shape == params[i].shape
         self.step_dev.fill_(max(steps) if steps else 0)
         self.step_count = max(steps) if steps else 0
+        # isg_adam_dev takes lr/betas/eps/wd by value, so a captured graph holds the old
+        # ones: re-record the step when the loaded hyperparameters differ
+        if self.graphs and self._captured[1] != self._hyper():
+            self.capture(split=self._captured[0])
 
     def load_state_dict(self, sd):
         """Model weights and buffers, copied into the flat buffers in place (the captured

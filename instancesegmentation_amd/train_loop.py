@@ -6,6 +6,7 @@ visualisation (cv.imshow, :429-469, :511-517) left out.
 Differences from the reference, all deliberate:
   * the model is Segment(20) fed RGB + 17 heatmaps (the self-consistent configuration,
     SURVEY.md §0.4: the reference's `Segment(3)` + one-argument `train_batch` crashes);
+    the loader hands over the keypoints and the stem synthesises the heatmaps on the GPU;
   * one optimisation step is `Trainer.step` (one HIP graph: forward, BCE, backward,
     Adam), one process per GPU with the two-bucket RCCL exchange when launched with
     torchrun; rank 0 alone validates and writes checkpoints;
@@ -109,9 +110,13 @@ def parse_args(argv=None):
 
 
 def _batches(loader, device):
+    """(inputs, mask, results) per batch. The second input is the keypoints [B,17,3]
+    (float64, 408 B per image): the Trainer's stem synthesises the 17 heatmaps from them
+    on the GPU (kp_stem.hip) instead of the loader building and uploading 17 x 480 x 480
+    fp32 maps per image (train_instance.py:200-213)."""
     for image_ts, mask_ts, results in loader:
-        hm = torch.stack([r["heatmaps"] for r in results])
-        yield ([image_ts.to(device, non_blocking=True), hm.to(device, non_blocking=True)],
+        kp = torch.stack([r["keypoints"] for r in results])
+        yield ([image_ts.to(device, non_blocking=True), kp.to(device, non_blocking=True)],
                mask_ts.to(device, non_blocking=True), results)
 
 
@@ -124,8 +129,8 @@ def fit(args, device=None, process_group=None):
     device = torch.device(device or "cuda")
     world = dist.get_world_size() if dist.is_initialized() else 1
     rank = dist.get_rank() if dist.is_initialized() else 0
-    trainset = InstanceCommonDataset(args.train_dataset_dir)
-    valset = InstanceCommonDataset(args.val_dataset_dir, test=True)
+    trainset = InstanceCommonDataset(args.train_dataset_dir, with_heatmaps=False)
+    valset = InstanceCommonDataset(args.val_dataset_dir, test=True, with_heatmaps=False)
     sampler = (torch.utils.data.distributed.DistributedSampler(trainset) if world > 1 else None)
     trainloader = torch.utils.data.DataLoader(
         trainset, batch_size=args.batch_size, shuffle=sampler is None, sampler=sampler,
@@ -135,7 +140,7 @@ def fit(args, device=None, process_group=None):
     S = trainset.out_size[0]
     model = Segment(20)
     trainer = Trainer(model, args.batch_size, [(args.batch_size, 3, S, S),
-                                               (args.batch_size, 17, S, S)], device=device,
+                                               (args.batch_size, 17, 3)], device=device,
                       process_group=process_group)
     branch_name = git_branch_name()
     best_path = args.checkpoint_save_path or os.path.join(args.checkpoint_dir,

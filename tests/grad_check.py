@@ -26,15 +26,26 @@ def _t(x):
         torch.from_numpy(np.asarray(x)).double()
 
 
+# north_star: "fp32 mask logits within 1e-4" of the reference CPU path. Where the CPU-fp32
+# reference is itself within WELL_CONDITIONED of fp64, the GPU must be within 1e-4 of the
+# CPU-fp32 output directly; elsewhere that distance is reported (it is then dominated by
+# the CPU path's own rounding error).
+WELL_CONDITIONED = 5e-5
+
+
 def check_logits(got, ref64, ref32, tag=""):
     got, ref64, ref32 = _t(got), _t(ref64), _t(ref32)
     err = (got - ref64).abs().max().item()
+    d32 = (got - ref32).abs().max().item()
     floor = (ref32 - ref64).abs().max().item()
     scale = max(1.0, ref64.abs().max().item())
-    print(f"{tag}: logits max abs err {err:.3e} (bar 1e-4; CPU-fp32 reference's own err "
-          f"{floor:.3e}; |logit|max {ref64.abs().max().item():.2f})")
+    print(f"{tag}: logits max abs err vs fp64 {err:.3e}, vs the CPU-fp32 reference "
+          f"{d32:.3e} (bar 1e-4; CPU-fp32 reference's own err {floor:.3e}; |logit|max "
+          f"{ref64.abs().max().item():.2f})")
     assert err <= max(1e-4, 2.0 * floor), (err, floor)
     assert err <= 1e-4 * scale, (err, scale)
+    if floor <= WELL_CONDITIONED:
+        assert d32 <= 1e-4, (d32, floor)
     return err
 
 

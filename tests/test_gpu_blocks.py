@@ -28,12 +28,19 @@ BLOCKS = {
                  lambda c, x: O.bottleneck_dim_relu(c, "blk", x), 48),
     "conv_prelu": (lambda: S.Conv(16, 16, k=5, s=2, p=2, act=torch.nn.PReLU(16)),
                    lambda c, x: O.conv(c, "blk", x, k=5, s=2, p=2, act="prelu"), 16),
+    # A8 (segment.py:296-344): two inputs, x and the pooled skip features of the same
+    # resolution; output at twice the resolution
+    "up_res": (lambda: S.BottleneckUp_Res(128, 16, 48),
+               lambda c, x, s: O.bottleneck_up_res(c, "blk", x, s), 128, 48),
+    "up_res_other": (lambda: S.BottleneckUp_Res_Other(48, 4, 16, 36),
+                     lambda c, x, s: O.bottleneck_up_res(c, "blk", x, s), 48, 36),
 }
 SIZES = [(16, 24), (32, 32), (12, 20)]
 
 
 def run_block(name, hw, seed=0):
-    make, ofn, cin = BLOCKS[name]
+    make, ofn, cin = BLOCKS[name][:3]
+    cskip = BLOCKS[name][3] if len(BLOCKS[name]) > 3 else 0
     torch.manual_seed(seed)
     blk = make()
     shapes = [(k, tuple(v.shape)) for k, v in blk.state_dict().items()]
@@ -45,7 +52,11 @@ def run_block(name, hw, seed=0):
     rng = np.random.Generator(np.random.PCG64(seed))
     x = rng.normal(0, 1, (2, cin, H, W)).astype(np.float32)
     xt = torch.from_numpy(x).to(DEV).requires_grad_(True)
-    out = blk(xt)
+    ins = [xt]
+    if cskip:
+        sk = rng.normal(0, 1, (2, cskip, H, W)).astype(np.float32)
+        ins.append(torch.from_numpy(sk).to(DEV).requires_grad_(True))
+    out = blk(*ins)
     outs = out if isinstance(out, tuple) else (out,)
     douts = [torch.from_numpy(rng.normal(0, 1, tuple(o.shape)).astype(np.float32)).to(DEV)
              for o in outs]
@@ -57,10 +68,13 @@ def run_block(name, hw, seed=0):
         if v.is_floating_point() and not k.endswith(("running_mean", "running_var")):
             v.requires_grad_(True)
     xr = torch.from_numpy(x).double().requires_grad_(True)
-    ro = ofn(O.Ctx(P, True), xr)
+    rins = [xr]
+    if cskip:
+        rins.append(torch.from_numpy(sk).double().requires_grad_(True))
+    ro = ofn(O.Ctx(P, True), *rins)
     ros = ro if isinstance(ro, tuple) else (ro,)
     torch.autograd.backward(ros, [d.double().cpu() for d in douts])
-    return blk, outs, xt, ros, xr, P
+    return blk, outs, ins, ros, rins, P
 
 
 def err(a, b):
@@ -72,10 +86,11 @@ def err(a, b):
 @pytest.mark.parametrize("hw", SIZES)
 @pytest.mark.parametrize("name", list(BLOCKS))
 def test_block_parity(name, hw):
-    blk, outs, xt, ros, xr, P = run_block(name, hw)
+    blk, outs, ins, ros, rins, P = run_block(name, hw)
     for o, r in zip(outs, ros):
         assert err(o, r) < 1e-5, f"output {err(o, r):.2e}"
-    assert err(xt.grad, xr.grad) < 1e-4, f"input grad {err(xt.grad, xr.grad):.2e}"
+    for i, (xt, xr) in enumerate(zip(ins, rins)):  # input (and skip) gradients
+        assert err(xt.grad, xr.grad) < 1e-4, f"input {i} grad {err(xt.grad, xr.grad):.2e}"
     bad = []
     for k, p in blk.named_parameters():
         ref = P["blk." + k].grad

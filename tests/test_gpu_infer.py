@@ -98,6 +98,16 @@ def test_heatmaps_random_keypoints_match_oracle():
     ref = IO.instance_heatmaps(kp, S)
     got = _heatmaps_gpu(kp, S, S)
     assert np.array_equal(got, ref)
+    # user-supplied coordinates: huge values give empty windows as in the
+    # reference (python int() is exact); NaN / inf, where the reference's int() raises,
+    # make the part not visible instead of an undefined int conversion on the GPU
+    bad = kp.copy()
+    bad[0, :4, 2] = 1.0
+    bad[0, 0, 0], bad[0, 1, 1], bad[0, 2, 0], bad[0, 3, 1] = np.nan, np.inf, -np.inf, 1e300
+    bad[1, 5, 0], bad[1, 5, 2] = -1e300, 1.0
+    clean = bad.copy()
+    clean[0, :3, 2] = 0.0
+    assert np.array_equal(_heatmaps_gpu(bad, S, S), IO.instance_heatmaps(clean, S))
 
 
 def _calibrated(model_cin=20, seed=41):
@@ -128,7 +138,9 @@ def test_fused_eval_matches_unfused_and_oracle():
     ea, eb = (a - ref).abs().max().item(), (b - ref).abs().max().item()
     print(f"eval logits |max| {scale:.1f}: unfused err {ea:.2e}, fused err {eb:.2e}, "
           f"CPU-fp32 err {floor:.2e}")
-    assert eb <= max(1e-4 * max(1.0, scale), 2.0 * floor)
+    # absolute bar (north_star: logits within 1e-4), relaxed only to 2x the CPU-fp32
+    # reference's own error where that is larger (BN folding reorders the arithmetic)
+    assert eb <= max(1e-4, 2.0 * floor), (eb, floor)
     with pytest.raises(RuntimeError):
         f.train()
 
@@ -181,8 +193,10 @@ def test_instance_segmenter_pipeline_matches_oracle():
     got = eng.logits[:n].double().cpu()
     err = (got - ref).abs().max().item()
     floor = (ref32.double() - ref).abs().max().item()
-    print(f"pipeline logits err {err:.2e} (CPU-fp32 {floor:.2e}, |max| {ref.abs().max():.1f})")
-    assert err <= max(1e-4 * max(1.0, ref.abs().max().item()), 2.0 * floor)
+    d32 = (got - ref32.double()).abs().max().item()
+    print(f"pipeline logits err vs fp64 {err:.2e}, vs CPU-fp32 {d32:.2e} (CPU-fp32's own "
+          f"{floor:.2e}, |max| {ref.abs().max():.1f})")
+    assert err <= max(1e-4, 2.0 * floor), (err, floor)
     # stage 3: paste + NMS bit-exact to the oracle on the GPU's own probabilities
     prob = eng.prob[:n, 0].cpu().numpy()
     m_ref = MO.paste_masks(prob, win, H, W)
@@ -197,3 +211,45 @@ def test_instance_segmenter_pipeline_matches_oracle():
     eager = InstanceSegmenter(m, (H, W), max_instances=8, iou_thr=0.5, capture=False)
     masks3, keep3, _ = eager(img2, boxes2, kps2)
     assert keep2 == keep3 and torch.equal(masks2, masks3)
+
+
+def test_infer_main_runs_one_nms_over_all_instances(tmp_path):
+    """infer.main on an image with more instances than --max-instances: the
+    capacity grows so ONE mask-NMS ranks every instance — the kept set equals an
+    InstanceSegmenter run over all of them, and exact repeats of the same detection in
+    what used to be different chunks suppress each other."""
+    from PIL import Image
+
+    from instancesegmentation_amd import infer as I
+    from instancesegmentation_amd.data import ORDER_PART_NAMES
+    from instancesegmentation_amd.infer import InstanceSegmenter
+    rng = np.random.Generator(np.random.PCG64(31))
+    H, W = 192, 256
+    m, _ = _calibrated()
+    img, boxes, kps = _scene(rng, H, W, 3, 0)
+    boxes = np.concatenate([boxes] * 4)  # 12 instances: every person detected 4 times
+    kps = np.concatenate([kps] * 4)
+    d = tmp_path / "images"
+    d.mkdir()
+    Image.fromarray(img).save(d / "a.png")
+    objs = [{"box": [int(v) for v in b],
+             "body_keypoint": {ORDER_PART_NAMES[j]: {"status": "vis" if k[j, 2] > 0 else "missing",
+                                                     "point": [float(k[j, 0]), float(k[j, 1])]}
+                               for j in range(17)}} for b, k in zip(boxes, kps)]
+    with open(d / "a.json", "w") as f:
+        json.dump({"object": objs}, f)
+    ck = tmp_path / "m.pth"
+    torch.save({"state_dict": {k: v.cpu() for k, v in m.state_dict().items()}}, ck)
+    out = tmp_path / "out"
+    assert I.main(["-i", str(d), "-o", str(out), "--checkpoint", str(ck),
+                   "--max-instances", "4"]) == 0
+    res = json.load(open(out / "a.json"))
+    assert res["instances"] == 12 and "nms" not in res
+    eng = InstanceSegmenter(m, (H, W), max_instances=16, iou_thr=0.5, capture=False)
+    _, keep, scores = eng(img, boxes, kps)
+    assert res["keep"] == keep, (res["keep"], keep)
+    # repeats of one person are identical masks: at most one non-empty copy survives
+    kept = [i for i in res["keep"] if scores[i] > 0]
+    assert kept and len({i % 3 for i in kept}) == len(kept), (kept, scores)
+    for i in res["keep"]:
+        assert (out / "a" / f"{i}.png").exists()

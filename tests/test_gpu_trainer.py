@@ -165,3 +165,26 @@ def test_train_loop_runs_and_checkpoints(tmp_path):
     assert TL.load_checkpoint(path, tr2) == 1
     assert torch.equal(tr2.flat, tr.flat) and torch.equal(tr2.flatb, tr.flatb)
     assert torch.equal(tr2.exp_avg, tr.exp_avg) and int(tr2.step_dev.item()) == 2
+
+
+def test_loaded_adam_hyperparameters_reach_the_captured_step():
+    """Trainer.load_optimizer_state_dict after capture(): the Adam launch holds
+    lr/betas/eps/wd by value, so the step is re-recorded when they change — here lr 0 from
+    a loaded optimizer state must leave every parameter unchanged by the next step."""
+    fx = SegmentFixture("segment20_n2_128.npz")
+    tr = Trainer(_model(fx), fx.n, [(fx.n, 3, fx.h, fx.w), (fx.n, 17, fx.h, fx.w)], device=DEV)
+    tr.capture()
+    xs, y = _inputs(fx.x), torch.from_numpy(fx.mask).to(DEV)
+    tr.step(xs, y)
+    sd = tr.optimizer_state_dict()
+    sd["param_groups"][0]["lr"] = 0.0
+    tr.load_optimizer_state_dict(sd)
+    before = tr.flat.clone()
+    tr.step(xs, y)
+    torch.cuda.synchronize()
+    assert torch.equal(tr.flat, before)
+    sd["param_groups"][0]["lr"] = 1e-3
+    tr.load_optimizer_state_dict(sd)
+    tr.step(xs, y)
+    torch.cuda.synchronize()
+    assert not torch.equal(tr.flat, before)

@@ -226,3 +226,27 @@ def test_forward_side_branches_fork_and_join():
     # replica fold and gradient finalisation fork there (after every statistic is done)
     assert not any(r.flags & Record.OPF_FORK_NOW for r in p.bwd.recs
                    if r.kind not in (L.OP_SUM_REP, L.OP_GRAD_FINAL))
+
+
+@pytest.mark.parametrize("n", [1, 2])
+def test_forked_pools_join_before_any_reader_of_their_buffer(n):
+    """engine._fork_pools at batch 1 and 2: the keypoint heatmaps' pool
+    writes channels [3, 20) of init_down, but bottle1_1's convs read init_down from channel
+    0. Every main-stream record whose pointer falls anywhere in a forked pool's output
+    buffer must come after a join (at N == 1 the old start-pointer rule placed none)."""
+    from instancesegmentation_amd.engine import Record
+    m = Segment(20)
+    p = Plan(m, [(n, 3, 64, 64), (n, 17, 3)], True, True, (False, False))
+    recs = p.fwd.recs
+    pools = [i for i, r in enumerate(recs) if r.kind in (L.OP_MAXPOOL_FWD, L.OP_KP_POOL)
+             and r.flags & Record.OPF_SIDE]
+    assert any(recs[i].kind == L.OP_KP_POOL for i in pools)
+    for i in pools:
+        slot, lo, hi = recs[i].out_range
+        readers = [j for j in range(i + 1, len(recs)) if not recs[j].flags & Record.OPF_SIDE
+                   and any(fs == slot and lo <= off < hi for _, fs, off in recs[j].fix)]
+        if recs[i].kind == L.OP_KP_POOL:
+            assert readers
+        if readers:  # (bottle1_1.pool is read by side-stream branches only)
+            assert any(recs[j].flags & Record.OPF_JOIN for j in range(i + 1, readers[0] + 1)), \
+                (n, recs[i].label, recs[readers[0]].label)

@@ -103,6 +103,14 @@ def test_common_dataset_reader(tmp_path):
                (kp[j, 1] - win[1]) * 480 / (win[3] - win[1])) for j in range(17) if kp[j, 2] > 0}
     ref = np.stack(keypoint2heatmaps(pts, (480, 480)))
     assert np.array_equal(out["heatmaps"].numpy(), ref)
+    # the keypoints handed to the GPU stem (train_loop) redraw exactly these heatmaps
+    k = out["keypoints"].numpy()
+    assert k.dtype == np.float64 and k.shape == (17, 3)
+    kpts = {j: (k[j, 0], k[j, 1]) for j in range(17) if k[j, 2] > 0}
+    assert np.array_equal(np.stack(keypoint2heatmaps(kpts, (480, 480))), ref)
+    ds2 = D.InstanceCommonDataset(str(tmp_path), test=True, with_heatmaps=False)
+    _, _, out2 = ds2[0]
+    assert "heatmaps" not in out2 and np.array_equal(out2["keypoints"].numpy(), k)
     b = D.collate_fn([ds[0], ds[0]])
     assert b[0].shape == (2, 3, 480, 480) and isinstance(b[2], list)
 
