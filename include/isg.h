@@ -363,6 +363,40 @@ int32_t isg_kp_stem_fwd(const isg_kp_stem* a, isg_stream_t stream);
 int32_t isg_kp_stem_wgrad(const isg_kp_stem* a, isg_stream_t stream);
 int32_t isg_kp_pool(const isg_kp_stem* a, isg_stream_t stream);
 
+/* ---- fused mask head (segment.py:435-438, 504-505) ------------------------ */
+
+/* bottle6_1 = ConvTranspose2d(16 -> 4, k8, s4, p2) followed by bottle6_2 = Conv2d(4 -> 1,
+ * 3x3, p1) (no nonlinearity between them), with the 4-channel full-resolution
+ * intermediate kept on chip (recomputed in the backward).
+ *   fwd: out = logits [N,1,4Hi,4Wi]
+ *   bwd: dx (sinks: STORE / ACCUM without statistics) = dL/dx; dw1/db1/dw2/db2 += the
+ *        parameter gradients, added into replica (workgroup % nrep) of each (replica r at
+ *        + r*rep_stride floats; NULL skips one). Replaces the unfused isg_convT_fwd +
+ *        isg_conv_fwd (+ their dgrad / wgrad) pair, which round-trips the intermediate
+ *        through HBM. */
+typedef struct {
+    isg_vtensor x;               /* [N,16,Hi,Wi] */
+    const float* w1;             /* ConvTranspose2d weight [16][4][8][8] */
+    const float* b1;             /* [4] or NULL */
+    const float* w2;             /* Conv2d weight [1][4][3][3] */
+    const float* b2;             /* [1] or NULL */
+    float* out;                  /* fwd */
+    int64_t out_n_stride;
+    const float* dout;           /* bwd: dL/dlogits */
+    int64_t dout_n_stride;
+    isg_sinks dx;                /* bwd */
+    float* dw1;
+    float* db1;
+    float* dw2;
+    float* db2;
+    int64_t rep_stride;
+    int32_t nrep;
+    int32_t N, Hi, Wi;
+} isg_mask_head;
+
+int32_t isg_mask_head_fwd(const isg_mask_head* a, isg_stream_t stream);
+int32_t isg_mask_head_bwd(const isg_mask_head* a, isg_stream_t stream);
+
 /* ---- plan executor ------------------------------------------------------ */
 
 /* A recorded op list (built once per input shape by the Python planner) replayed
@@ -386,7 +420,8 @@ int32_t isg_exec_ms(const void* ops, int32_t nops, void* const* table, isg_strea
 
 /* sizeof() of the ABI structs and executor records (0 vtensor, 1 sinks, 2 conv record,
  * 3 wgrad record, 4 pool record, 5 tail, 6 tail_grad, 7 bn_update, 8 grad_final,
- * 9 bce record, 10 conv_geom, 11 bn, 12 vseg, 13 sink, 14 sum_rep record, 15 kp_stem) so
+ * 9 bce record, 10 conv_geom, 11 bn, 12 vseg, 13 sink, 14 sum_rep record, 15 kp_stem,
+ * 16 mask_head) so
  * bindings can verify layouts. */
 int32_t isg_record_size(int32_t which);
 

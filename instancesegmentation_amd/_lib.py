@@ -19,7 +19,7 @@ SINK_STORE, SINK_ACCUM, SINK_ACTBWD, SINK_NONE = 0, 1, 2, 3
 MAX_SEGS = 3
 LIST_CHUNK = 32
 STAT_REP = 16     # ISG_STAT_REP: accumulator replicas (isg.h)
-ABI_VERSION = 6
+ABI_VERSION = 7
 WREP = 16         # ISG_WREP: weight-gradient replicas (isg.h)
 
 
@@ -93,6 +93,14 @@ class KpStem(Structure):
                 ("out_n_stride", c_int64)]
 
 
+class MaskHead(Structure):
+    _fields_ = [("x", VTensor), ("w1", c_void_p), ("b1", c_void_p), ("w2", c_void_p),
+                ("b2", c_void_p), ("out", c_void_p), ("out_n_stride", c_int64), ("dout", c_void_p),
+                ("dout_n_stride", c_int64), ("dx", Sinks), ("dw1", c_void_p), ("db1", c_void_p),
+                ("dw2", c_void_p), ("db2", c_void_p), ("rep_stride", c_int64), ("nrep", c_int32),
+                ("N", c_int32), ("Hi", c_int32), ("Wi", c_int32)]
+
+
 # executor records (api.cpp)
 class ConvRec(Structure):
     _fields_ = [("g", Geom), ("a", VTensor), ("w", c_void_p), ("out", Sinks)]
@@ -131,10 +139,11 @@ OP_MAXPOOL_FWD, OP_MAXPOOL_BWD, OP_TAIL_FWD, OP_TAIL_BWD = 5, 6, 7, 8
 OP_BN_UPDATE, OP_GRAD_FINAL, OP_BCE, OP_MEMSET = 9, 10, 11, 12
 OP_SUM_REP, OP_BN_FINAL = 13, 14
 OP_KP_STEM_FWD, OP_KP_STEM_WGRAD, OP_KP_POOL = 15, 16, 17
+OP_HEAD_FWD, OP_HEAD_BWD = 18, 19
 
 _RECORD_CHECK = [(0, VTensor), (1, Sinks), (2, ConvRec), (3, WgradRec), (4, PoolRec), (5, Tail),
                  (6, TailGrad), (7, BnUpdate), (8, GradFinal), (9, BceRec), (10, Geom), (11, Bn),
-                 (12, VSeg), (13, Sink), (14, SumRepRec), (15, KpStem)]
+                 (12, VSeg), (13, Sink), (14, SumRepRec), (15, KpStem), (16, MaskHead)]
 
 # exported symbol -> (restype, argtypes)
 SIGNATURES = {
@@ -174,6 +183,8 @@ SIGNATURES = {
     "isg_kp_stem_fwd": (c_int32, [POINTER(KpStem), c_void_p]),
     "isg_kp_stem_wgrad": (c_int32, [POINTER(KpStem), c_void_p]),
     "isg_kp_pool": (c_int32, [POINTER(KpStem), c_void_p]),
+    "isg_mask_head_fwd": (c_int32, [POINTER(MaskHead), c_void_p]),
+    "isg_mask_head_bwd": (c_int32, [POINTER(MaskHead), c_void_p]),
     "isg_exec": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p]),
     "isg_exec_ms": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p]),
     "isg_last_error": (c_char_p, []),

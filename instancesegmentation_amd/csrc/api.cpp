@@ -79,7 +79,7 @@ static bool partial_w(const isg_conv_geom* g) { return g->w_ci > 0 && g->w_ci !=
 extern "C" {
 
 const char* isg_last_error(void) { return g_last_error.c_str(); }
-int32_t isg_abi_version(void) { return 6; }
+int32_t isg_abi_version(void) { return 7; }
 int32_t isg_stat_replicas(void) { return ISG_STAT_REP; }
 
 int32_t isg_conv_fwd(const isg_conv_geom* g, const isg_vtensor* x, const float* w,
@@ -146,6 +146,8 @@ enum {
     OP_KP_STEM_FWD = 15,
     OP_KP_STEM_WGRAD = 16,
     OP_KP_POOL = 17,
+    OP_HEAD_FWD = 18,
+    OP_HEAD_BWD = 19,
 };
 
 struct ConvRec {
@@ -324,6 +326,12 @@ static int32_t run_op_raw(int32_t kind, char* buf, isg_stream_t st) {
         case OP_KP_POOL:
             rc = isg_kp_pool((const isg_kp_stem*)buf, st);
             break;
+        case OP_HEAD_FWD:
+            rc = isg_mask_head_fwd((const isg_mask_head*)buf, st);
+            break;
+        case OP_HEAD_BWD:
+            rc = isg_mask_head_bwd((const isg_mask_head*)buf, st);
+            break;
         case OP_MEMSET: {
             auto* r = (MemsetRec*)buf;
             if (hipMemsetAsync(r->p, 0, (size_t)r->bytes, st) != hipSuccess)
@@ -436,6 +444,7 @@ int32_t isg_record_size(int32_t which) {
         case 13: return (int32_t)sizeof(isg_sink);
         case 14: return (int32_t)sizeof(SumRepRec);
         case 15: return (int32_t)sizeof(isg_kp_stem);
+        case 16: return (int32_t)sizeof(isg_mask_head);
         default: return -1;
     }
 }

@@ -406,6 +406,153 @@ __global__ __launch_bounds__(kThreads) void sub2_dgrad_mfma_kernel(DownArgs a) {
     sinks_finalize(a.out);
 }
 
+// LDS-staged form (the path taken): the workgroup's dy band — kRowsPB + 2 rows x (64 + 2)
+// columns x 16 channels — is loaded ONCE with 16-B loads, transformed once per element
+// (BatchNorm backward rebuilt from g and the saved y) and zero-padded into LDS; the MFMA
+// B operands are then conflict-free ds_read_b32 (channel planes 16 mod 32 banks apart).
+// The direct form above re-read every dy element from L2 in up to 9 lanes (4-B loads)
+// and re-transformed it each time: ~11 VALU instructions per MFMA, 61 % of wave cycles
+// waiting (profiles/r02f_pmc_sq_summary.txt).
+constexpr int kSubRS = 66;                 // staged row: columns j0 - 1 .. j0 + 64
+constexpr int kSubPL = 400;                // channel plane (>= (kRowsPB + 2) * 66, 16 mod 32)
+static_assert(kSubPL >= (kRowsPB + 2) * kSubRS && kSubPL % 32 == 16, "staging plane");
+
+__global__ __launch_bounds__(kThreads) void sub2_dgrad_lds_kernel(DownArgs a) {
+    constexpr int K = 5, P = 2, R0 = 1;
+    __shared__ float wl[kMaxM * kMaxM * K * K];  // [c][m][kh][kw] (the weight's own layout)
+    __shared__ float Ls[kMaxM * kSubPL];         // [c][row][col] transformed dy band
+    __shared__ ChT tab[kMaxM];
+    __shared__ SinkRow ri[kMaxM];
+    __shared__ float red[4][3][kMaxM];
+    const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
+    const int kq = lane >> 4, pl = lane & 15;
+    const int Hs = a.H, Ws = a.W, Wd = 2 * Ws;
+    const int n = blockIdx.z, j0 = blockIdx.x * 64, i0 = blockIdx.y * kRowsPB;
+    if (tid < a.C) tab[tid] = ch_table_entry(a.dy, tid, (int64_t)Hs * Ws);
+    if (tid < a.M) ri[tid] = sink_row(a.out, tid, (int64_t)2 * Hs * Wd);
+    for (int e = tid; e < kMaxM * kMaxM * K * K; e += kThreads) {
+        const int c = e / (kMaxM * K * K), r = e - c * kMaxM * K * K;
+        const int m = r / (K * K), tap = r - m * K * K;
+        wl[e] = (c < a.C && m < a.M) ? gld(a.w, ((int64_t)c * a.M + m) * K * K + tap) : 0.f;
+    }
+    __syncthreads();
+    // ---- stage the band: interior quads (16-B loads), then the two halo columns
+    {
+        constexpr int NQ = kMaxM * (kRowsPB + 2) * 16;  // (c, row, quad)
+        constexpr int U = NQ / kThreads;
+        static_assert(NQ % kThreads == 0, "staging split");
+        f32x4 xv[U], yv[U];
+        int meta[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int e = tid + u * kThreads;
+            const int c = e / ((kRowsPB + 2) * 16), rq = e - c * (kRowsPB + 2) * 16;
+            const int rr = rq >> 4, q = rq & 15;
+            const int yy = i0 - 1 + rr, xx = j0 + 4 * q;
+            const bool ok = c < a.C && (unsigned)yy < (unsigned)Hs && xx < Ws;
+            meta[u] = ok ? e : -1 - e;
+            const ChT t = tab[c < a.C ? c : 0];
+            const int64_t o = ok ? (int64_t)yy * Ws + xx : 0;
+            xv[u] = gld4(t.p + (int64_t)n * t.ns, o);
+            yv[u] = t.xf == ISG_XF_BN_BWD ? gld4(t.y + (int64_t)n * t.yns, o) : xv[u];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool ok = meta[u] >= 0;
+            const int e = ok ? meta[u] : -1 - meta[u];
+            const int c = e / ((kRowsPB + 2) * 16), rq = e - c * (kRowsPB + 2) * 16;
+            const int rr = rq >> 4, q = rq & 15;
+            float* d = Ls + c * kSubPL + rr * kSubRS + 1 + 4 * q;
+            if (ok) {
+                const ChT t = tab[c];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) d[k] = ch_xform(t.xf, t.act, t.k, xv[u][k], yv[u][k]);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) d[k] = 0.f;
+            }
+        }
+        for (int e = tid; e < kMaxM * (kRowsPB + 2) * 2; e += kThreads) {
+            const int c = e / ((kRowsPB + 2) * 2), rs = e - c * (kRowsPB + 2) * 2;
+            const int rr = rs >> 1, side = rs & 1;
+            const int yy = i0 - 1 + rr, xx = side ? j0 + 64 : j0 - 1;
+            float v = 0.f;
+            if (c < a.C && (unsigned)yy < (unsigned)Hs && (unsigned)xx < (unsigned)Ws) {
+                const ChT t = tab[c];
+                const int64_t o = (int64_t)yy * Ws + xx;
+                const float x = gld(t.p + (int64_t)n * t.ns, o);
+                const float y = t.xf == ISG_XF_BN_BWD ? gld(t.y + (int64_t)n * t.yns, o) : x;
+                v = ch_xform(t.xf, t.act, t.k, x, y);
+            }
+            Ls[c * kSubPL + rr * kSubRS + (side ? 65 : 0)] = v;
+        }
+    }
+    __syncthreads();
+    const int jw = j0 + wave * 16;  // this wave's first cell
+    float bs0[4] = {0.f, 0.f, 0.f, 0.f}, bs1[4] = {0.f, 0.f, 0.f, 0.f}, bs2[4] = {0.f, 0.f, 0.f, 0.f};
+    const int i_end = min(Hs, i0 + kRowsPB);
+    for (int i = i0; i < i_end; ++i) {
+        f32x4 acc[2][2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int v = 0; v < 2; ++v) acc[u][v] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const float* lb = Ls + kq * kSubPL + (i - i0) * kSubRS + wave * 16 + pl;
+#pragma unroll
+        for (int g = 0; g < kMaxM / 4; ++g) {
+            const float* wa = wl + ((4 * g + kq) * kMaxM + pl) * K * K;  // A: c = 4g + kq, m = pl
+            const float* lg = lb + 4 * g * kSubPL;
+#pragma unroll
+            for (int kh = 0; kh < K; ++kh) {
+                const int au = (kh + P) & 1, rr = (au + P - kh) / 2 + R0;
+#pragma unroll
+                for (int kw = 0; kw < K; ++kw) {
+                    const int av = (kw + P) & 1, qq = (av + P - kw) / 2 + R0;
+                    acc[au][av] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[kh * K + kw], lg[rr * kSubRS + qq],
+                                                                       acc[au][av], 0, 0, 0);
+                }
+            }
+        }
+        // epilogue: lane holds D[m = 4kq + r][cell = pl] of every phase
+        const int jo = jw + pl;
+        const bool cok = jo < Ws;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int m = 4 * kq + r;
+            if (cok && m < a.M) {
+                const SinkRow q = ri[m];
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    float t0 = 0.f, t1 = 0.f, t2 = 0.f;
+                    sink_row_apply2(q, n, (int64_t)(2 * i + u) * Wd + 2 * jo, acc[u][0][r], acc[u][1][r], t0, t1, t2);
+                    bs0[r] += t0;
+                    bs1[r] += t1;
+                    bs2[r] += t2;
+                }
+            }
+        }
+    }
+    if (sinks_need_red(a.out)) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float t0 = dpp_row16_sum(bs0[r]), t1 = dpp_row16_sum(bs1[r]), t2 = dpp_row16_sum(bs2[r]);
+            if (pl == 0) {
+                red[wave][0][4 * kq + r] = t0;
+                red[wave][1][4 * kq + r] = t1;
+                red[wave][2][4 * kq + r] = t2;
+            }
+        }
+        __syncthreads();
+        if (tid < a.M) {
+            float r3[3];
+#pragma unroll
+            for (int q3 = 0; q3 < 3; ++q3) r3[q3] = ((red[0][q3][tid] + red[1][q3][tid]) + red[2][q3][tid]) + red[3][q3][tid];
+            sink_row_flush(a.out, tid, r3[0], r3[1], r3[2]);
+        }
+    }
+    sinks_finalize(a.out);
+}
+
 bool down_geom(const isg_conv_geom* g, int& S) {
     S = g->SH;
     return g->groups == 1 && (S == 2 || S == 4) && g->SW == S && g->KH == 2 * S && g->KW == 2 * S &&
@@ -495,7 +642,11 @@ int32_t isg_sub2_dgrad(const isg_conv_geom* g, const isg_vtensor* dy, const floa
     a.dy = *dy; a.out = *dx; a.w = w;
     a.N = g->N; a.M = g->Ci; a.C = g->Co; a.H = g->OH; a.W = g->OW;
     const dim3 grid((unsigned)((a.W + 63) / 64), (unsigned)((a.H + kRowsPB - 1) / kRowsPB), (unsigned)a.N);
-    hipLaunchKernelGGL((sub2_dgrad_mfma_kernel<5>), grid, dim3(kThreads), 0, st, a);
+    static const bool direct = getenv("ISG_SUB2_DIRECT") != nullptr;  // the unstaged form (A/B)
+    if (!direct && a.W % 4 == 0 && down_src_ok(dy))
+        hipLaunchKernelGGL(sub2_dgrad_lds_kernel, grid, dim3(kThreads), 0, st, a);
+    else
+        hipLaunchKernelGGL((sub2_dgrad_mfma_kernel<5>), grid, dim3(kThreads), 0, st, a);
     if (dx->fin_counter) isg_fin_note_handled();
     const int32_t e = isg_check_launch("sub2_dgrad_kernel");
     return e ? e : 1;

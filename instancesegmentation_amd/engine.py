@@ -409,6 +409,26 @@ class Graph:
         self.ops.append(op)
         return Value([Val(out, 0, ct.out_channels, bnr, act, slope, grad=self.need_grad)])
 
+    def head(self, ct, conv, x, name=""):
+        """The mask head (segment.py:435-438, 504-505): ConvTranspose2d(16 -> 4, k8, s4, p2)
+        then Conv2d(4 -> 1, 3x3, p1) as ONE fused op (isg_mask_head_*: the 4-channel
+        intermediate never reaches HBM), or None when the modules / input do not have
+        that exact shape (the caller then emits the two convolutions) or ISG_NO_HEAD=1."""
+        if os.environ.get("ISG_NO_HEAD", "0") == "1":
+            return None
+        if not (ct.in_channels == 16 and ct.out_channels == 4 and ct.kernel_size == (8, 8)
+                and ct.stride == (4, 4) and ct.padding == (2, 2) and ct.groups == 1
+                and ct.dilation == (1, 1) and not any(ct.output_padding)
+                and conv.in_channels == 4 and conv.out_channels == 1
+                and conv.kernel_size == (3, 3) and conv.stride == (1, 1)
+                and conv.padding == (1, 1) and conv.dilation == (1, 1) and conv.groups == 1
+                and x.C == 16 and all(not s.virtual for s in x.segs)):
+            return None
+        out = self.act_buf(1, 4 * x.H, 4 * x.W, name)
+        op = HeadOp(self, ct, conv, x, out)
+        self.ops.append(op)
+        return Value([Val(out, 0, 1, grad=self.need_grad)])
+
     def maxpool(self, x, k, out=None, c0=0, name=""):
         if x.H % k or x.W % k:
             raise RuntimeError(f"max_pool{k}: {x.H}x{x.W} not divisible (reference needs "
@@ -763,6 +783,63 @@ class ConvOp:
             gs.bias_from_bn.append((self.mod, self.bnr))
 
 
+class HeadOp:
+    """Fused mask head (Graph.head): one forward and one backward record."""
+
+    def __init__(self, g, ct, conv, x, out):
+        self.g, self.ct, self.conv, self.x, self.out = g, ct, conv, x, out
+
+    def _spec(self):
+        g = self.g
+        segs = [fwd_seg(v, g.train) for v in self.x.segs]
+        s = {"x": vtensor(segs, g.N, self.x.H, self.x.W), "w1": g.tptr(self.ct, "weight"),
+             "w2": g.tptr(self.conv, "weight"), "N": g.N, "Hi": self.x.H, "Wi": self.x.W}
+        if self.ct.bias is not None:
+            s["b1"] = g.tptr(self.ct, "bias")
+        if self.conv.bias is not None:
+            s["b2"] = g.tptr(self.conv, "bias")
+        return s
+
+    def _cost(self):
+        """(flops, bytes) of the forward: convT 2*16*4*64 MAC per input pixel, the 3x3
+        2*36 per output pixel; input read once, logits written once."""
+        g = self.g
+        q = g.N * self.x.H * self.x.W
+        p = 16 * q
+        return 2 * (16 * 4 * 64 * q + 36 * p), 4 * (16 * q + p)
+
+    def fwd(self, ops):
+        s = dict(self._spec(), out=self.out.ptr(), out_n_stride=self.out.n_stride)
+        fl, nb = self._cost()
+        ops.add(Record(L.OP_HEAD_FWD, L.MaskHead, s, label=self.out.name, flops=fl, nbytes=nb))
+
+    def bwd(self, ops, gs):
+        g = self.g
+        dy = gs.dy_seg(self.out, None, g.train)
+        if dy is None:
+            return
+        s = dict(self._spec(), dout=dy["p"], dout_n_stride=dy["n_stride"],
+                 rep_stride=g.pgrad_size, nrep=L.WREP)
+        if self.x.grad:
+            sinks, c = [], 0
+            for v in self.x.segs:
+                sinks.append(gs.sink_for(v, c, g.train))
+                c += v.C
+            s["dx"] = sinks_spec(sinks)
+        else:
+            s["dx"] = {"nsink": 0}
+        s["dw1"] = g.wrep_ptr(self.ct, "weight")
+        s["dw2"] = g.wrep_ptr(self.conv, "weight")
+        if self.ct.bias is not None:
+            s["db1"] = g.wrep_ptr(self.ct, "bias")
+        if self.conv.bias is not None:
+            s["db2"] = g.wrep_ptr(self.conv, "bias")
+        fl, nb = self._cost()
+        # input gradient + both weight gradients (+ the intermediate recomputed)
+        ops.add(Record(L.OP_HEAD_BWD, L.MaskHead, s, label="d_" + self.out.name,
+                       flops=3 * fl, nbytes=nb + 4 * 16 * g.N * self.x.H * self.x.W))
+
+
 class KpPoolOp:
     """max_pool(k) of the keypoint heatmaps (segment.py:31 on the heatmap channels)."""
 
@@ -890,7 +967,12 @@ class Plan:
         self.out_bufs = []
         for i, o in enumerate(outs):
             ob = Buf(S_OUT[i], N, o.C, o.H, o.W, f"out{i}")
-            self._emit_output(g, o, ob)
+            head = next((op for op in g.ops if isinstance(op, HeadOp) and len(o.segs) == 1
+                         and op.out is o.segs[0].buf and not o.segs[0].virtual), None)
+            if head is not None:
+                head.out = ob  # the fused head writes the output slot itself (no copy)
+            else:
+                self._emit_output(g, o, ob)
             self.out_bufs.append(ob)
         self.out_shapes = [(N, b.C, b.H, b.W) for b in self.out_bufs]
         # ---- forward list

@@ -400,6 +400,9 @@ class Segment(EngineModule):
         y = self.bottle4_3.emit(g, y)                                  # :497
         y = self.bottle5_1up.emit(g, y, b1_idx)                        # :500
         y = self.bottle5_2.emit(g, y)                                  # :501
+        head = g.head(self.bottle6_1, self.bottle6_2, y, name="logits")  # :504-505 fused
+        if head is not None:
+            return head
         y = g.conv_transpose(self.bottle6_1, y, name="bottle6_1")      # :504
         return g.conv(self.bottle6_2, y, name="logits")                # :505
 

@@ -92,6 +92,8 @@ DENSE = [
     # 5x5 s2 p2 input gradient as a sub-pixel transposed conv (sub2_dgrad): ragged, odd grid
     (16, 16, 62, 90, 5, 2, 2, 1),
     (8, 12, 40, 24, 5, 2, 2, 1),
+    # ... on the LDS-staged form (cell columns % 4 == 0): two column blocks, ragged rows
+    (16, 16, 74, 136, 5, 2, 2, 1),
     # thin 3x3 (thin_conv / thin_wgrad, 4 pixels per lane): ragged row count, 1 -> 4
     (4, 1, 37, 96, 3, 1, 1, 1),
     (1, 4, 24, 20, 3, 1, 1, 1),

@@ -1,0 +1,78 @@
+"""Fused mask head (isg_mask_head_fwd / _bwd, csrc/mask_head.hip) against an fp64 torch
+restatement of the reference's two layers (segment.py:435-438, 504-505:
+ConvTranspose2d(16 -> 4, k8, s4, p2) then Conv2d(4 -> 1, 3x3, p1)), forward and backward
+(input gradient through a STORE and an ACCUM sink, all four parameter gradients summed
+over the weight-gradient replicas), on whole and partial tiles."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from instancesegmentation_amd import _lib as L
+from tests.isg_helpers import call, sinks, struct, vt
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _case(N, Hi, Wi, seed):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(N, 16, Hi, Wi, generator=g)
+    w1 = torch.randn(16, 4, 8, 8, generator=g) * 0.05
+    b1 = torch.randn(4, generator=g) * 0.1
+    w2 = torch.randn(1, 4, 3, 3, generator=g) * 0.3
+    b2 = torch.randn(1, generator=g) * 0.1
+    dl = torch.randn(N, 1, 4 * Hi, 4 * Wi, generator=g)
+    return x, w1, b1, w2, b2, dl
+
+
+def _ref(x, w1, b1, w2, b2, dl):
+    P = [t.double().requires_grad_(True) for t in (x, w1, b1, w2, b2)]
+    y = F.conv2d(F.conv_transpose2d(P[0], P[1], P[2], stride=4, padding=2), P[3], P[4], padding=1)
+    y.backward(dl.double())
+    return y.detach(), [p.grad for p in P]
+
+
+def _rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return (a - b).abs().max().item() / max(b.abs().max().item(), 1e-12)
+
+
+@pytest.mark.parametrize("N,Hi,Wi", [(2, 8, 16), (1, 5, 7), (2, 17, 33), (1, 64, 64)])
+def test_mask_head_fwd_bwd(N, Hi, Wi):
+    x, w1, b1, w2, b2, dl = _case(N, Hi, Wi, Hi * 100 + Wi)
+    ref_y, ref_g = _ref(x, w1, b1, w2, b2, dl)
+    d = {k: v.to(DEV).contiguous() for k, v in dict(x=x, w1=w1, b1=b1, w2=w2, b2=b2, dl=dl).items()}
+    OH, OW = 4 * Hi, 4 * Wi
+    out = torch.full((N, 1, OH, OW), 7.0, device=DEV)
+    # two input segments (channels 0-9, 10-15) exercise the vtensor segment split
+    xa, xb = d["x"][:, :10].contiguous(), d["x"][:, 10:].contiguous()
+    seg = lambda t, C: {"p": t.data_ptr(), "n_stride": C * Hi * Wi, "C": C, "xform": L.XF_PLAIN}
+    base = {"x": {"s": [seg(xa, 10), seg(xb, 6)], "nseg": 2, "N": N, "H": Hi, "W": Wi},
+            "w1": d["w1"].data_ptr(), "b1": d["b1"].data_ptr(), "w2": d["w2"].data_ptr(),
+            "b2": d["b2"].data_ptr(), "N": N, "Hi": Hi, "Wi": Wi}
+    a = struct(L.MaskHead, dict(base, out=out.data_ptr(), out_n_stride=OH * OW))
+    call("isg_mask_head_fwd", a, L.stream_ptr())
+    e = _rel(out, ref_y)
+    print(f"{N}x16x{Hi}x{Wi}: logits rel err {e:.2e}")
+    assert e < 2e-6
+    # backward: dx of channels 0-9 STOREd, 10-15 ACCUMulated onto a preset value
+    dxa = torch.full((N, 10, Hi, Wi), 5.0, device=DEV)
+    pre = torch.randn(N, 6, Hi, Wi, device=DEV)
+    dxb = pre.clone()
+    R, nrep = 4096 + 4 + 36 + 1, L.WREP
+    rep = torch.zeros(nrep * R, device=DEV)
+    rp = rep.data_ptr()
+    sk = [{"p": dxa.data_ptr(), "n_stride": 10 * Hi * Wi, "c0": 0, "C": 10, "mode": L.SINK_STORE},
+          {"p": dxb.data_ptr(), "n_stride": 6 * Hi * Wi, "c0": 10, "C": 6, "mode": L.SINK_ACCUM}]
+    b = struct(L.MaskHead, dict(base, dout=d["dl"].data_ptr(), dout_n_stride=OH * OW,
+                                dx={"s": sk, "nsink": 2}, dw1=rp, db1=rp + 4 * 4096,
+                                dw2=rp + 4 * 4100, db2=rp + 4 * 4136, rep_stride=R, nrep=nrep))
+    call("isg_mask_head_bwd", b, L.stream_ptr())
+    tot = rep.view(nrep, R).sum(0).cpu()
+    dx = torch.cat([dxa.cpu(), (dxb - pre).cpu()], 1)
+    errs = {"dx": _rel(dx, ref_g[0]), "dw1": _rel(tot[:4096].view(16, 4, 8, 8), ref_g[1]),
+            "db1": _rel(tot[4096:4100], ref_g[2]), "dw2": _rel(tot[4100:4136].view(1, 4, 3, 3), ref_g[3]),
+            "db2": _rel(tot[4136:4137], ref_g[4])}
+    print({k: f"{v:.1e}" for k, v in errs.items()})
+    assert all(v < 2e-5 for v in errs.values()), errs

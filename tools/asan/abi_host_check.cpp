@@ -40,7 +40,7 @@ static void put_op(std::vector<char>& b, int kind, const void* desc, int bytes,
 int main() {
     EXPECT(isg_abi_version() > 0);
     EXPECT(isg_stat_replicas() == ISG_STAT_REP);
-    for (int i = 0; i <= 15; ++i) EXPECT(isg_record_size(i) > 0);
+    for (int i = 0; i <= 16; ++i) EXPECT(isg_record_size(i) > 0);
     EXPECT(isg_record_size(-1) == -1 && isg_record_size(99) == -1);
 
     // argument validation and the thread-local message
