@@ -260,6 +260,8 @@ static bool is_pointwise(const isg_conv_geom* g) {
 
 int32_t isg_down_conv_fwd(const isg_conv_geom* g, const isg_vtensor* src, const float* w,
                           const isg_sinks* out, hipStream_t st);
+int32_t isg_s2k5_fwd(const isg_conv_geom* g, const isg_vtensor* x, const float* w,
+                     const isg_sinks* out, hipStream_t st);
 int32_t isg_sub2_dgrad(const isg_conv_geom* g, const isg_vtensor* dy, const float* w,
                        const isg_sinks* dx, hipStream_t st);
 
@@ -275,6 +277,10 @@ int32_t isg_dense_conv_fwd(const isg_conv_geom* g, const isg_vtensor* x, const f
     }
     if (!special_off) {  // k 2S, stride S: the sub-pixel convT's input gradient (down_conv.hip)
         const int32_t t = isg_down_conv_fwd(g, x, w, out, st);
+        if (t != 0) return t < 0 ? t : 0;
+    }
+    if (!special_off) {  // 5x5 stride 2, <= 16 channels: the stem's second conv (down_conv.hip)
+        const int32_t t = isg_s2k5_fwd(g, x, w, out, st);
         if (t != 0) return t < 0 ? t : 0;
     }
     if (!special_off) {  // dense spatial conv, <= 48 output channels (tap_conv.hip)

@@ -553,6 +553,151 @@ __global__ __launch_bounds__(kThreads) void sub2_dgrad_lds_kernel(DownArgs a) {
     sinks_finalize(a.out);
 }
 
+// ---- 5x5 stride-2 pad-2 forward, LDS-staged (the stem's second conv, segment.py:23-26:
+// 16 -> 16 channels, 512^2 -> 256^2 at 1024^2 input) ---------------------------------------
+// A workgroup owns 64 output columns x kS2Rows output rows of one image and all (<= 16)
+// output channels. Its input band — 2 * kS2Rows + 3 rows x 132 columns x 16 channels — is
+// loaded ONCE with 16-B loads, the producer's BatchNorm + activation applied once per
+// element, and stored split into even / odd column planes, so every tap of a 16-pixel
+// MFMA group reads 16 consecutive LDS words. The weights are the A operands, held in
+// registers for the whole workgroup (100 per lane); one MFMA per (channel group, tap):
+// A[m][k] = W[m][4g + k][tap] (lane: m = l&15, k = l>>4), B[k][px] = band value of
+// channel 4g + k under the tap for pixel px (lane: k = l>>4, px = l&15).
+constexpr int kS2Rows = 2;                    // output rows per workgroup
+constexpr int kS2NR = 2 * kS2Rows + 3;        // staged input rows
+constexpr int kS2EW = 66;                     // columns per parity plane
+constexpr int kS2RS = 2 * kS2EW;              // staged row: [even 66 | odd 66]
+constexpr int kS2PL = 944;                    // channel plane (>= 7 * 132, 16 mod 32)
+static_assert(kS2PL >= kS2NR * kS2RS && kS2PL % 32 == 16, "stem2 plane");
+
+__global__ __launch_bounds__(kThreads) void s2k5_fwd_kernel(DownArgs a) {
+    constexpr int K = 5;
+    __shared__ float Ls[kMaxM * kS2PL];
+    __shared__ ChT tab[kMaxM];
+    __shared__ SinkRow ri[kMaxM];
+    __shared__ float red[4][3][kMaxM];
+    const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
+    const int kq = lane >> 4, pl = lane & 15;
+    const int Ho = a.H, Wo = a.W, Hi = 2 * Ho, Wi = 2 * Wo;  // a.H/W: output grid
+    const int n = blockIdx.z, ox0 = blockIdx.x * 64, oy0 = blockIdx.y * kS2Rows;
+    if (tid < a.C) tab[tid] = ch_table_entry(a.dy, tid, (int64_t)Hi * Wi);
+    if (tid < a.M) ri[tid] = sink_row(a.out, tid, (int64_t)Ho * Wo);
+    // A fragments: W[m = pl][c = 4g + kq][tap], w = [M][C][5][5]
+    float wa[kMaxM / 4][K * K];
+    {
+        const int m = pl < a.M ? pl : 0;
+#pragma unroll
+        for (int g = 0; g < kMaxM / 4; ++g) {
+            const int c = 4 * g + kq;
+            const bool ok = pl < a.M && c < a.C;
+            const float* wp = a.w + ((int64_t)m * a.C + (c < a.C ? c : 0)) * K * K;
+#pragma unroll
+            for (int t = 0; t < K * K; ++t) wa[g][t] = ok ? gld(wp, t) : 0.f;
+        }
+    }
+    __syncthreads();
+    // ---- stage the band: quads from the aligned column 2*ox0 - 4
+    {
+        constexpr int NQ = 34;  // quads per staged row
+        constexpr int NE = kMaxM * kS2NR * NQ;
+        constexpr int U = (NE + kThreads - 1) / kThreads;
+        const int c0 = 2 * ox0 - 4;
+        // every load first (clamped addresses, no branch around a load), then transform
+        f32x4 xv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int e = min(tid + u * kThreads, NE - 1);
+            const int c = e / (kS2NR * NQ), rq = e - c * (kS2NR * NQ);
+            const int rr = rq / NQ, q = rq - rr * NQ;
+            const int iy = 2 * oy0 - 2 + rr, ix = c0 + 4 * q;
+            const bool ok = c < a.C && (unsigned)iy < (unsigned)Hi && ix >= 0 && ix < Wi;
+            const ChT t = tab[c < a.C ? c : 0];
+            xv[u] = gld4(t.p + (int64_t)n * t.ns, ok ? (int64_t)iy * Wi + ix : 0);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int e = tid + u * kThreads;
+            if (e >= NE) continue;
+            const int c = e / (kS2NR * NQ), rq = e - c * (kS2NR * NQ);
+            const int rr = rq / NQ, q = rq - rr * NQ;
+            const int iy = 2 * oy0 - 2 + rr, ix = c0 + 4 * q;
+            const bool ok = c < a.C && (unsigned)iy < (unsigned)Hi && ix >= 0 && ix < Wi;
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if (ok) {
+                const ChT t = tab[c];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) v[k] = ch_xform(t.xf, t.act, t.k, xv[u][k], xv[u][k]);
+            }
+            float* row = Ls + c * kS2PL + rr * kS2RS;
+            // element k of quad q is input column c0 + 4q + k = 2*ox0 - 2 + r, r = 4q + k - 2:
+            // even r -> even plane [r / 2], odd r -> odd plane [(r - 1) / 2]
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int r = 4 * q + k - 2;
+                if (r < 0 || r >= 2 * kS2EW) continue;
+                row[(r & 1) * kS2EW + (r >> 1)] = v[k];
+            }
+        }
+    }
+    __syncthreads();
+    // ---- MFMA: wave w owns output columns 16w .. 16w + 15 of every tile row
+    f32x4 acc[kS2Rows];
+#pragma unroll
+    for (int r = 0; r < kS2Rows; ++r) acc[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const float* lb = Ls + kq * kS2PL + wave * 16 + pl;
+#pragma unroll
+    for (int g = 0; g < kMaxM / 4; ++g) {
+        const float* lg = lb + 4 * g * kS2PL;
+#pragma unroll
+        for (int kh = 0; kh < K; ++kh)
+#pragma unroll
+            for (int kw = 0; kw < K; ++kw) {
+                const int col = (kw & 1) * kS2EW + (kw >> 1);
+#pragma unroll
+                for (int r = 0; r < kS2Rows; ++r)
+                    acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[g][kh * K + kw],
+                                                                  lg[(2 * r + kh) * kS2RS + col], acc[r], 0, 0, 0);
+            }
+    }
+    // ---- epilogue: lane holds D[m = 4kq + i][px = pl] of each tile row
+    float bs0[4] = {0.f, 0.f, 0.f, 0.f}, bs1[4] = {0.f, 0.f, 0.f, 0.f}, bs2[4] = {0.f, 0.f, 0.f, 0.f};
+    const int ox = ox0 + wave * 16 + pl;
+#pragma unroll
+    for (int r = 0; r < kS2Rows; ++r) {
+        const int oy = oy0 + r;
+        if (oy >= Ho || ox >= Wo) continue;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int m = 4 * kq + i;
+            if (m >= a.M) continue;
+            float t0 = 0.f, t1 = 0.f, t2 = 0.f;
+            sink_row_apply(ri[m], n, (int64_t)oy * Wo + ox, acc[r][i], t0, t1, t2);
+            bs0[i] += t0;
+            bs1[i] += t1;
+            bs2[i] += t2;
+        }
+    }
+    if (sinks_need_red(a.out)) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float t0 = dpp_row16_sum(bs0[i]), t1 = dpp_row16_sum(bs1[i]), t2 = dpp_row16_sum(bs2[i]);
+            if (pl == 0) {
+                red[wave][0][4 * kq + i] = t0;
+                red[wave][1][4 * kq + i] = t1;
+                red[wave][2][4 * kq + i] = t2;
+            }
+        }
+        __syncthreads();
+        if (tid < a.M) {
+            float r3[3];
+#pragma unroll
+            for (int q3 = 0; q3 < 3; ++q3) r3[q3] = ((red[0][q3][tid] + red[1][q3][tid]) + red[2][q3][tid]) + red[3][q3][tid];
+            sink_row_flush(a.out, tid, r3[0], r3[1], r3[2]);
+        }
+    }
+    sinks_finalize(a.out);
+}
+
 bool down_geom(const isg_conv_geom* g, int& S) {
     S = g->SH;
     return g->groups == 1 && (S == 2 || S == 4) && g->SW == S && g->KH == 2 * S && g->KW == 2 * S &&
@@ -649,5 +794,25 @@ int32_t isg_sub2_dgrad(const isg_conv_geom* g, const isg_vtensor* dy, const floa
         hipLaunchKernelGGL((sub2_dgrad_mfma_kernel<5>), grid, dim3(kThreads), 0, st, a);
     if (dx->fin_counter) isg_fin_note_handled();
     const int32_t e = isg_check_launch("sub2_dgrad_kernel");
+    return e ? e : 1;
+}
+
+// 5x5 stride 2 pad 2 forward with <= 16 input / output channels (s2k5_fwd_kernel).
+// Returns 1 if launched, 0 if the shape is not for this kernel, <0 on error.
+int32_t isg_s2k5_fwd(const isg_conv_geom* g, const isg_vtensor* x, const float* w,
+                     const isg_sinks* out, hipStream_t st) {
+    static const bool off = getenv("ISG_NO_S2K5") != nullptr;
+    if (off || g->groups != 1 || g->SH != 2 || g->SW != 2 || g->KH != 5 || g->KW != 5 ||
+        g->PH != 2 || g->PW != 2 || g->DH != 1 || g->DW != 1 || g->H != 2 * g->OH ||
+        g->W != 2 * g->OW || g->W % 4 || g->Co > kMaxM || g->Ci > kMaxM ||
+        (g->w_ci && g->w_ci != g->Ci) || !down_src_ok(x))
+        return 0;
+    DownArgs a{};
+    a.dy = *x; a.out = *out; a.w = w;
+    a.N = g->N; a.M = g->Co; a.C = g->Ci; a.H = g->OH; a.W = g->OW;
+    const dim3 grid((unsigned)((a.W + 63) / 64), (unsigned)((a.H + kS2Rows - 1) / kS2Rows), (unsigned)a.N);
+    hipLaunchKernelGGL(s2k5_fwd_kernel, grid, dim3(kThreads), 0, st, a);
+    if (out->fin_counter) isg_fin_note_handled();
+    const int32_t e = isg_check_launch("s2k5_fwd_kernel");
     return e ? e : 1;
 }

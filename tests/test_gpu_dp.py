@@ -96,3 +96,48 @@ def test_dp_trainer_two_ranks_on_gpu():
         assert gerr < 1e-4, gerr
         assert perr == 0.0, perr
         assert berr < 1e-5, berr  # rank 0's statistics (fp64-atomic order noise only)
+
+
+def _fit_worker(rank, world, port, root, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    from instancesegmentation_amd import train_loop as TL
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.manual_seed(5)  # the same initial weights on every rank
+        args = TL.parse_args(["--train-dataset-dir", os.path.join(root, "ds"),
+                              "--val-dataset-dir", os.path.join(root, "ds"),
+                              "--checkpoint-dir", os.path.join(root, "ck"),
+                              "--batch-size", "1", "--epoch", "3", "--val-iter", "1",
+                              "--show-iter", "1", "--cpu-num", "0", "--max-steps", "3"])
+        tr, history = TL.fit(args, device=dev)
+        torch.cuda.synchronize()
+        flat = tr.flat.clone().cpu()
+        fl = [torch.zeros_like(flat) for _ in range(world)]
+        dist.all_gather(fl, flat)
+        out[rank] = (history, int(tr.step_dev.item()), (fl[0] - fl[1]).abs().max().item(),
+                     tr.world)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_train_loop_fit_two_ranks(tmp_path):
+    """train_loop.fit (the train_instance.py driver) data-parallel over two ranks sharing
+    the GPU (gloo): DistributedSampler batches, the two-bucket exchange every step, the
+    validation / checkpoint decisions broadcast from rank 0 — both ranks take the same
+    decisions (identical history), step the same number of times and end with identical
+    parameters."""
+    from tests.test_infer_cpu import _write_dataset
+    _write_dataset(tmp_path / "ds", np.random.default_rng(12))
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_fit_worker, args=(world, _free_port(), str(tmp_path), out), nprocs=world, join=True)
+    (h0, s0, d0, w0), (h1, s1, d1, w1) = out[0], out[1]
+    print(f"history rank0 {h0}\nhistory rank1 {h1}")
+    assert w0 == w1 == world
+    assert h0 == h1 and len(h0) >= 1
+    assert s0 == s1 == 3
+    assert d0 == 0.0 and d1 == 0.0

@@ -94,6 +94,10 @@ DENSE = [
     (8, 12, 40, 24, 5, 2, 2, 1),
     # ... on the LDS-staged form (cell columns % 4 == 0): two column blocks, ragged rows
     (16, 16, 74, 136, 5, 2, 2, 1),
+    # the LDS-staged 5x5 s2 forward (s2k5_fwd: <= 16 channels, W % 4 == 0): partial
+    # column block, odd output rows, fewer channels than the 16-lane fragments
+    (16, 16, 134, 200, 5, 2, 2, 1),
+    (12, 8, 40, 36, 5, 2, 2, 1),
     # thin 3x3 (thin_conv / thin_wgrad, 4 pixels per lane): ragged row count, 1 -> 4
     (4, 1, 37, 96, 3, 1, 1, 1),
     (1, 4, 24, 20, 3, 1, 1, 1),
