@@ -413,14 +413,17 @@ __global__ __launch_bounds__(kThreads) void sub2_dgrad_mfma_kernel(DownArgs a) {
 // The direct form above re-read every dy element from L2 in up to 9 lanes (4-B loads)
 // and re-transformed it each time: ~11 VALU instructions per MFMA, 61 % of wave cycles
 // waiting (profiles/r02f_pmc_sq_summary.txt).
-constexpr int kSubRS = 66;                 // staged row: columns j0 - 1 .. j0 + 64
-constexpr int kSubPL = 400;                // channel plane (>= (kRowsPB + 2) * 66, 16 mod 32)
+constexpr int kSubRS = 72;                 // staged row: column x at x - (j0 - 4), 0..68
+constexpr int kSubPL = 432;                // channel plane (>= (kRowsPB + 2) * 72, 16 mod 32)
 static_assert(kSubPL >= (kRowsPB + 2) * kSubRS && kSubPL % 32 == 16, "staging plane");
+
+// the producer transform of one staged value: kind and activation wave-uniform (SGPRs)
+ISG_DEV float xf_u(const ChT& t, float x, float y) { return ch_xform_u(t.xf, t.act, t.k, x, y); }
 
 __global__ __launch_bounds__(kThreads) void sub2_dgrad_lds_kernel(DownArgs a) {
     constexpr int K = 5, P = 2, R0 = 1;
     __shared__ float wl[kMaxM * kMaxM * K * K];  // [c][m][kh][kw] (the weight's own layout)
-    __shared__ float Ls[kMaxM * kSubPL];         // [c][row][col] transformed dy band
+    __shared__ __attribute__((aligned(16))) float Ls[kMaxM * kSubPL];  // [c][row][col] dy band
     __shared__ ChT tab[kMaxM];
     __shared__ SinkRow ri[kMaxM];
     __shared__ float red[4][3][kMaxM];
@@ -462,7 +465,7 @@ __global__ __launch_bounds__(kThreads) void sub2_dgrad_lds_kernel(DownArgs a) {
             const int e = ok ? meta[u] : -1 - meta[u];
             const int c = e / ((kRowsPB + 2) * 16), rq = e - c * (kRowsPB + 2) * 16;
             const int rr = rq >> 4, q = rq & 15;
-            float* d = Ls + c * kSubPL + rr * kSubRS + 1 + 4 * q;
+            float* d = Ls + c * kSubPL + rr * kSubRS + 4 + 4 * q;
             if (ok) {
                 const ChT t = tab[c];
 #pragma unroll
@@ -484,7 +487,7 @@ __global__ __launch_bounds__(kThreads) void sub2_dgrad_lds_kernel(DownArgs a) {
                 const float y = t.xf == ISG_XF_BN_BWD ? gld(t.y + (int64_t)n * t.yns, o) : x;
                 v = ch_xform(t.xf, t.act, t.k, x, y);
             }
-            Ls[c * kSubPL + rr * kSubRS + (side ? 65 : 0)] = v;
+            Ls[c * kSubPL + rr * kSubRS + (side ? 68 : 3)] = v;
         }
     }
     __syncthreads();
@@ -497,7 +500,7 @@ __global__ __launch_bounds__(kThreads) void sub2_dgrad_lds_kernel(DownArgs a) {
         for (int u = 0; u < 2; ++u)
 #pragma unroll
             for (int v = 0; v < 2; ++v) acc[u][v] = f32x4{0.f, 0.f, 0.f, 0.f};
-        const float* lb = Ls + kq * kSubPL + (i - i0) * kSubRS + wave * 16 + pl;
+        const float* lb = Ls + kq * kSubPL + (i - i0) * kSubRS + wave * 16 + pl + 3;
 #pragma unroll
         for (int g = 0; g < kMaxM / 4; ++g) {
             const float* wa = wl + ((4 * g + kq) * kMaxM + pl) * K * K;  // A: c = 4g + kq, m = pl
@@ -565,14 +568,15 @@ __global__ __launch_bounds__(kThreads) void sub2_dgrad_lds_kernel(DownArgs a) {
 // channel 4g + k under the tap for pixel px (lane: k = l>>4, px = l&15).
 constexpr int kS2Rows = 2;                    // output rows per workgroup
 constexpr int kS2NR = 2 * kS2Rows + 3;        // staged input rows
-constexpr int kS2EW = 66;                     // columns per parity plane
-constexpr int kS2RS = 2 * kS2EW;              // staged row: [even 66 | odd 66]
-constexpr int kS2PL = 944;                    // channel plane (>= 7 * 132, 16 mod 32)
+constexpr int kS2Q = 34;                      // 16-B quads per staged row (from column 2*ox0 - 4)
+constexpr int kS2EW = 2 * kS2Q;               // columns per parity plane (index = column pair + 1)
+constexpr int kS2RS = 2 * kS2EW;              // staged row: [even 68 | odd 68]
+constexpr int kS2PL = 976;                    // channel plane (>= 7 * 136, 16 mod 32)
 static_assert(kS2PL >= kS2NR * kS2RS && kS2PL % 32 == 16, "stem2 plane");
 
 __global__ __launch_bounds__(kThreads) void s2k5_fwd_kernel(DownArgs a) {
     constexpr int K = 5;
-    __shared__ float Ls[kMaxM * kS2PL];
+    __shared__ __attribute__((aligned(16))) float Ls[kMaxM * kS2PL];
     __shared__ ChT tab[kMaxM];
     __shared__ SinkRow ri[kMaxM];
     __shared__ float red[4][3][kMaxM];
@@ -582,34 +586,40 @@ __global__ __launch_bounds__(kThreads) void s2k5_fwd_kernel(DownArgs a) {
     const int n = blockIdx.z, ox0 = blockIdx.x * 64, oy0 = blockIdx.y * kS2Rows;
     if (tid < a.C) tab[tid] = ch_table_entry(a.dy, tid, (int64_t)Hi * Wi);
     if (tid < a.M) ri[tid] = sink_row(a.out, tid, (int64_t)Ho * Wo);
-    // A fragments: W[m = pl][c = 4g + kq][tap], w = [M][C][5][5]
+    // A fragments: W[m = pl][c = 4g + kq][tap], w = [M][C][5][5]: the weight is copied
+    // into the (not yet used) band buffer with coalesced loads first — a direct per-lane
+    // gather is 100 scattered loads per lane, which made this kernel TA-bound
     float wa[kMaxM / 4][K * K];
     {
+        const int nw = a.M * a.C * K * K;
+        for (int e = tid; e < nw; e += kThreads) Ls[e] = gld(a.w, e);
+        __syncthreads();
         const int m = pl < a.M ? pl : 0;
 #pragma unroll
         for (int g = 0; g < kMaxM / 4; ++g) {
             const int c = 4 * g + kq;
             const bool ok = pl < a.M && c < a.C;
-            const float* wp = a.w + ((int64_t)m * a.C + (c < a.C ? c : 0)) * K * K;
+            const float* wp = Ls + (m * a.C + (c < a.C ? c : 0)) * K * K;
 #pragma unroll
-            for (int t = 0; t < K * K; ++t) wa[g][t] = ok ? gld(wp, t) : 0.f;
+            for (int t = 0; t < K * K; ++t) wa[g][t] = ok ? wp[t] : 0.f;
         }
     }
     __syncthreads();
-    // ---- stage the band: quads from the aligned column 2*ox0 - 4
+    // ---- stage the band: every (channel, row, quad) 16-B load in flight at once (15 per
+    //      lane), then the producer transform and the split of quad q (input columns
+    //      2*ox0 - 4 + 4q .. +3) into the even / odd planes with two 8-B stores: even
+    //      [2q, 2q + 1] = columns (+0, +2), odd [2q, 2q + 1] = (+1, +3)
     {
-        constexpr int NQ = 34;  // quads per staged row
-        constexpr int NE = kMaxM * kS2NR * NQ;
+        constexpr int NE = kMaxM * kS2NR * kS2Q;
         constexpr int U = (NE + kThreads - 1) / kThreads;
-        const int c0 = 2 * ox0 - 4;
-        // every load first (clamped addresses, no branch around a load), then transform
+        typedef float f32x2 __attribute__((ext_vector_type(2)));
         f32x4 xv[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int e = min(tid + u * kThreads, NE - 1);
-            const int c = e / (kS2NR * NQ), rq = e - c * (kS2NR * NQ);
-            const int rr = rq / NQ, q = rq - rr * NQ;
-            const int iy = 2 * oy0 - 2 + rr, ix = c0 + 4 * q;
+            const int c = e / (kS2NR * kS2Q), rq = e - c * (kS2NR * kS2Q);
+            const int rr = rq / kS2Q, q = rq - rr * kS2Q;
+            const int iy = 2 * oy0 - 2 + rr, ix = 2 * ox0 - 4 + 4 * q;
             const bool ok = c < a.C && (unsigned)iy < (unsigned)Hi && ix >= 0 && ix < Wi;
             const ChT t = tab[c < a.C ? c : 0];
             xv[u] = gld4(t.p + (int64_t)n * t.ns, ok ? (int64_t)iy * Wi + ix : 0);
@@ -618,25 +628,17 @@ __global__ __launch_bounds__(kThreads) void s2k5_fwd_kernel(DownArgs a) {
         for (int u = 0; u < U; ++u) {
             const int e = tid + u * kThreads;
             if (e >= NE) continue;
-            const int c = e / (kS2NR * NQ), rq = e - c * (kS2NR * NQ);
-            const int rr = rq / NQ, q = rq - rr * NQ;
-            const int iy = 2 * oy0 - 2 + rr, ix = c0 + 4 * q;
+            const int c = e / (kS2NR * kS2Q), rq = e - c * (kS2NR * kS2Q);
+            const int rr = rq / kS2Q, q = rq - rr * kS2Q;
+            const int iy = 2 * oy0 - 2 + rr, ix = 2 * ox0 - 4 + 4 * q;
             const bool ok = c < a.C && (unsigned)iy < (unsigned)Hi && ix >= 0 && ix < Wi;
-            f32x4 v = {0.f, 0.f, 0.f, 0.f};
-            if (ok) {
-                const ChT t = tab[c];
+            const ChT t = tab[c < a.C ? c : 0];
+            f32x4 v;
 #pragma unroll
-                for (int k = 0; k < 4; ++k) v[k] = ch_xform(t.xf, t.act, t.k, xv[u][k], xv[u][k]);
-            }
-            float* row = Ls + c * kS2PL + rr * kS2RS;
-            // element k of quad q is input column c0 + 4q + k = 2*ox0 - 2 + r, r = 4q + k - 2:
-            // even r -> even plane [r / 2], odd r -> odd plane [(r - 1) / 2]
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int r = 4 * q + k - 2;
-                if (r < 0 || r >= 2 * kS2EW) continue;
-                row[(r & 1) * kS2EW + (r >> 1)] = v[k];
-            }
+            for (int k = 0; k < 4; ++k) v[k] = ok ? ch_xform(t.xf, t.act, t.k, xv[u][k], xv[u][k]) : 0.f;
+            float* row = Ls + c * kS2PL + rr * kS2RS + 2 * q;
+            *reinterpret_cast<f32x2*>(row) = f32x2{v[0], v[2]};
+            *reinterpret_cast<f32x2*>(row + kS2EW) = f32x2{v[1], v[3]};
         }
     }
     __syncthreads();
@@ -652,7 +654,8 @@ __global__ __launch_bounds__(kThreads) void s2k5_fwd_kernel(DownArgs a) {
         for (int kh = 0; kh < K; ++kh)
 #pragma unroll
             for (int kw = 0; kw < K; ++kw) {
-                const int col = (kw & 1) * kS2EW + (kw >> 1);
+                // even tap: input column 2*ox - 2 + kw = even-plane index (ox - ox0) + kw/2 + 1
+                const int col = (kw & 1) * kS2EW + (kw >> 1) + 1;
 #pragma unroll
                 for (int r = 0; r < kS2Rows; ++r)
                     acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[g][kh * K + kw],

@@ -27,29 +27,17 @@ constexpr int kThreads = 256;
 constexpr int kCi = 16, kCm = 4;          // convT input / intermediate channels
 constexpr int TY = 32, TX = 64;           // logit (= intermediate) tile
 constexpr int RY = TY / 4 + 2, RX = TX / 4 + 2;   // input region (1-pixel halo)   10 x 18
-constexpr int RXS = RX + 1;
+constexpr int RXS = RX;
 constexpr int IY = TY + 2, IX = TX + 2;   // intermediate region (3x3 halo)     34 x 66
 constexpr int IXS = IX + 1;
 constexpr int DY = TY + 6, DX = TX + 6;   // dlogits region (backward)         38 x 70
-constexpr int DXS = DX + 1;
+constexpr int DXS = DX;
 constexpr int GY = TY + 4, GX = TX + 4;   // intermediate-gradient region       36 x 68
 constexpr int GJY = GY / 4, GJX = GX / 4; // per phase: 9 x 17
 constexpr int GPL = 16 * GJY * GJX;       // one channel, phase-split             2448
 constexpr int IPL = IY * IXS;             // one channel of the intermediate      2278
 constexpr int XPL = GPL > IPL ? GPL : IPL;
 constexpr int kW1 = kCi * kCm * 64;       // convT weights [16][4][8][8]
-
-// convT weights staged in LDS as Wt[co][ky][kx][ci]: every use reads 4 or 8 consecutive
-// input channels of one (co, ky, kx) with one wave-uniform (broadcast) ds_read_b128
-ISG_DEV void stage_w1(const float* w1, float* Wt) {
-    for (int i = threadIdx.x; i < kW1; i += kThreads) {
-        const int ci = i & 15, k = i >> 4;  // k = (co * 8 + ky) * 8 + kx
-        const int co = k >> 6, kk = k & 63;
-        Wt[i] = w1[(ci * kCm + co) * 64 + kk];
-    }
-}
-
-ISG_DEV f32x4 lds4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 
 // the input region of the tile whose top-left intermediate pixel is (Y0, X0), transformed,
 // zero outside the image
@@ -67,79 +55,96 @@ ISG_DEV void load_input(const isg_mask_head& a, const ChanCoef* coef, int n, int
     }
 }
 
-// The intermediate over the tile + 1-pixel halo into Is[co][ly][lx] (zero outside the
-// image: the 3x3's zero padding). Work is split into (phase, 64-pixel chunk) tasks per
-// wave, so a phase's weights are wave-uniform: per half of the input channels a lane
-// holds its 2 x 2 x 8 input values and reads the weights as broadcast b128 over ci.
-ISG_DEV void intermediate(const isg_mask_head& a, int Y0, int X0, const float (*Ts)[RY][RXS],
-                          const float* Wt, float* Is) {
-    constexpr int NCH = 3;  // chunks per phase: <= 9 x 17 = 153 pixels
+// ---- MFMA form of the convT (v_mfma_f32_16x16x4_f32) ----------------------------------
+// A "cell" (by, bx) is the 4 x 4 block of intermediate pixels (4by - 2 + r, 4bx - 2 + s) that
+// share the same 2 x 2 input neighbourhood (by - 1 + a, bx - 1 + b): per cell the convT is
+// a 64 x 64 matrix product, out[(co, r, s)] = sum_{(a, b, ci)} W1[ci][co][r + 4(1-a)][s + 4(1-b)]
+// * T[ci][by - 1 + a][bx - 1 + b]. One MFMA per (co, ci): A[m = (r, s)][k = (a, b)] (lane: m =
+// l & 15, k = l >> 4, registers for the whole workgroup), B[k = (a, b)][n = cell] (an LDS
+// read of the staged input), D lane: (r, s) = (l >> 4, i) of cell l & 15 — 4 consecutive
+// intermediate pixels of one row, one 16-B LDS store.
+constexpr int CY = TY / 4 + 1, CX = TX / 4 + 1;  // cells covering the tile + halo: 9 x 17
+constexpr int NCELL = CY * CX;
+constexpr int IRS = 4 * CX;                      // cell-region row stride (16-B rows) 68
+constexpr int IRP = 4 * CY * IRS;                // one channel of the cell region   2448
+
+// The convT weight copied into LDS scratch (>= kW1 floats) with coalesced 16-B loads; a
+// per-lane gather straight from global memory (64 scattered loads per lane) bound the
+// kernels on the address unit. Caller: barrier before reading `scratch`.
+ISG_DEV void copy_w1(const float* w1, float* scratch) {
+    for (int e = threadIdx.x; e < kW1 / 4; e += kThreads)
+        reinterpret_cast<f32x4*>(scratch)[e] = gld4(w1, 4 * e);
+}
+
+// A fragments of the cell GEMM for this lane, from the LDS copy of W1: wf[co][ci]
+ISG_DEV void cell_afrag(const float* w1s, float (&wf)[kCm][kCi]) {
+    const int lane = threadIdx.x & 63;
+    const int m = lane & 15, k = lane >> 4;
+    const int r = m >> 2, s = m & 3, aa = k >> 1, bb = k & 1;
+    const int ky = r + 4 * (1 - aa), kx = s + 4 * (1 - bb);
+#pragma unroll
+    for (int co = 0; co < kCm; ++co)
+#pragma unroll
+        for (int ci = 0; ci < kCi; ++ci) wf[co][ci] = w1s[((ci * kCm + co) * 8 + ky) * 8 + kx];
+}
+
+// The intermediate over the cells of the tile region (rows Y0 - 2 .. Y0 + 34, columns
+// X0 - 2 .. X0 + 66) into Ic[co][row][col] (origin (Y0 - 2, X0 - 2)), + bias, zero outside
+// the image.
+ISG_DEV void intermediate_mfma(const isg_mask_head& a, int Y0, int X0, const float (*Ts)[RY][RXS],
+                               const float (&wf)[kCm][kCi], float* Ic) {
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int kq = lane >> 4, aa = kq >> 1, bb = kq & 1;
     const int OH = 4 * a.Hi, OW = 4 * a.Wi;
     float b1[kCm];
 #pragma unroll
     for (int co = 0; co < kCm; ++co) b1[co] = a.b1 ? a.b1[co] : 0.f;
-    for (int task = wave; task < 16 * NCH; task += kThreads / 64) {
-        const int ph = task / NCH, chunk = task - ph * NCH;
-        const int r = ph >> 2, s = ph & 3;
-        const int ly0 = (r + 3) & 3, lx0 = (s + 3) & 3;
-        const int ny = (IY - ly0 + 3) >> 2, nx = (IX - lx0 + 3) >> 2;
-        const int j = chunk * 64 + lane;
-        if (chunk * 64 >= ny * nx) continue;  // wave-uniform
-        const int jj = j < ny * nx ? j : ny * nx - 1;
-        const int ly = ly0 + 4 * (jj / nx), lx = lx0 + 4 * (jj % nx);
-        const int tr = (1 + ly) >> 2, tc = (1 + lx) >> 2;
-        float acc[kCm];
+    for (int grp = wave; grp * 16 < NCELL; grp += kThreads / 64) {
+        const int cell = grp * 16 + (lane & 15);
+        const int cl = cell < NCELL ? cell : NCELL - 1;
+        const int cy = cl / CX, cx = cl - cy * CX;
+        f32x4 acc[kCm];
 #pragma unroll
-        for (int co = 0; co < kCm; ++co) acc[co] = b1[co];
-        const float* wt = Wt + opaque(0);  // no hoisting of weight reads out of the tile loop
+        for (int co = 0; co < kCm; ++co) acc[co] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            float t[4][8];  // [a * 2 + b][ci - 8h]: input pixel (tr + a, tc + b)
+        for (int ci = 0; ci < kCi; ++ci) {
+            const float bv = Ts[ci][cy + aa][cx + bb];
 #pragma unroll
-            for (int c = 0; c < 8; ++c) {
-                t[0][c] = Ts[8 * h + c][tr][tc];
-                t[1][c] = Ts[8 * h + c][tr][tc + 1];
-                t[2][c] = Ts[8 * h + c][tr + 1][tc];
-                t[3][c] = Ts[8 * h + c][tr + 1][tc + 1];
-            }
-#pragma unroll
-            for (int co = 0; co < kCm; ++co) {
-#pragma unroll
-                for (int ab = 0; ab < 4; ++ab) {
-                    // a = 0 (row tr = i0 - 1) uses tap r + 4, a = 1 tap r; same for b / s
-                    const int ky = r + ((ab >> 1) ? 0 : 4), kx = s + ((ab & 1) ? 0 : 4);
-                    const float* w = wt + ((co * 8 + ky) * 8 + kx) * 16 + 8 * h;
-                    const f32x4 wa = lds4(w), wb = lds4(w + 4);
-                    acc[co] += t[ab][0] * wa[0] + t[ab][1] * wa[1] + t[ab][2] * wa[2] + t[ab][3] * wa[3] +
-                               t[ab][4] * wb[0] + t[ab][5] * wb[1] + t[ab][6] * wb[2] + t[ab][7] * wb[3];
-                }
-            }
+            for (int co = 0; co < kCm; ++co)
+                acc[co] = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[co][ci], bv, acc[co], 0, 0, 0);
         }
-        if (j >= ny * nx) continue;
-        const int oy = Y0 - 1 + ly, ox = X0 - 1 + lx;
-        const bool in = oy >= 0 && oy < OH && ox >= 0 && ox < OW;
+        // D: (r, s) = (kq, i) of cell `cl`: pixel (Y0 - 2 + 4cy + kq, X0 - 2 + 4cx + i)
+        const int oy = Y0 - 2 + 4 * cy + kq, ox = X0 - 2 + 4 * cx;
+        const bool rok = cell < NCELL && oy >= 0 && oy < OH;
 #pragma unroll
-        for (int co = 0; co < kCm; ++co) Is[co * IPL + ly * IXS + lx] = in ? acc[co] : 0.f;
+        for (int co = 0; co < kCm; ++co) {
+            f32x4 v;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = (rok && ox + i >= 0 && ox + i < OW) ? acc[co][i] + b1[co] : 0.f;
+            if (cell < NCELL) *reinterpret_cast<f32x4*>(&Ic[co * IRP + (4 * cy + kq) * IRS + 4 * cx]) = v;
+        }
     }
 }
 
-__global__ __launch_bounds__(kThreads) void head_fwd_kernel(isg_mask_head a) {
+__global__ __launch_bounds__(kThreads, 2) void head_fwd_kernel(isg_mask_head a) {
     __shared__ float Ts[kCi][RY][RXS];
-    __shared__ float Is[kCm * IPL];
-    __shared__ __attribute__((aligned(16))) float Wt[kW1];
+    __shared__ __attribute__((aligned(16))) float Ic[kCm * IRP];
     __shared__ ChanCoef coef[kCi];
     const int n = blockIdx.z, Y0 = blockIdx.y * TY, X0 = blockIdx.x * TX;
     const int OH = 4 * a.Hi, OW = 4 * a.Wi;
     load_vt_coefs(a.x, coef, threadIdx.x, kThreads);
-    stage_w1(a.w1, Wt);
+    copy_w1(a.w1, Ic);
+    __syncthreads();
+    float wf[kCm][kCi];
+    cell_afrag(Ic, wf);
     __syncthreads();
     load_input(a, coef, n, Y0, X0, Ts);
     __syncthreads();
-    intermediate(a, Y0, X0, Ts, Wt, Is);
+    intermediate_mfma(a, Y0, X0, Ts, wf, Ic);
     __syncthreads();
-    // 3x3 (4 -> 1): lane = column, 8 rows per thread (10 x 3 reads per channel)
+    // 3x3 (4 -> 1): lane = column, 8 rows per thread (10 x 3 reads per channel); the
+    // intermediate's origin is (Y0 - 2, X0 - 2)
     const int lx = threadIdx.x & 63, rb = threadIdx.x >> 6;
     float out[8];
     const float b2 = a.b2 ? a.b2[0] : 0.f;
@@ -149,7 +154,7 @@ __global__ __launch_bounds__(kThreads) void head_fwd_kernel(isg_mask_head a) {
     for (int co = 0; co < kCm; ++co) {
 #pragma unroll
         for (int rr = 0; rr < 10; ++rr) {
-            const float* row = Is + co * IPL + (rb * 8 + rr) * IXS + lx;
+            const float* row = Ic + co * IRP + (rb * 8 + rr + 1) * IRS + lx + 1;
             const float v0 = row[0], v1 = row[1], v2 = row[2];
 #pragma unroll
             for (int dy = 0; dy < 3; ++dy) {
@@ -168,44 +173,60 @@ __global__ __launch_bounds__(kThreads) void head_fwd_kernel(isg_mask_head a) {
     }
 }
 
+// dT GEMM A operand in LDS: Wd[o = (co, r, s)][k = (a, b)][ci] = W1[ci][co][r + 4(1-a)][s + 4(1-b)]
+// (a lane reads word o * 64 + lane: conflict-free)
+ISG_DEV void stage_wd(const float* w1s, float* Wd) {
+    for (int e = threadIdx.x; e < kW1; e += kThreads) {
+        const int ci = e & 15, k = (e >> 4) & 3, o = e >> 6;
+        const int co = o >> 4, r = (o >> 2) & 3, s = o & 3, aa = k >> 1, bb = k & 1;
+        Wd[e] = w1s[((ci * kCm + co) * 8 + r + 4 * (1 - aa)) * 8 + s + 4 * (1 - bb)];
+    }
+}
+
+constexpr int XPP = NCELL;        // phase-split intermediate gradient: one (co, r, s) plane
+constexpr int XCF = kCm * 16 * XPP > kCm * IRP ? kCm * 16 * XPP : kCm * IRP;
+
 __global__ __launch_bounds__(kThreads, 2) void head_bwd_kernel(isg_mask_head a, int ntx, int nty,
-                                                            int ntiles) {
+                                                               int ntiles) {
     __shared__ float Ts[kCi][RY][RXS];
-    __shared__ __attribute__((aligned(16))) float Ds[DY * DXS];  // then the own input pixels [px][ci]
-    __shared__ float Xs[kCm * XPL];
-    __shared__ __attribute__((aligned(16))) float Wt[kW1];
+    __shared__ float Ds[DY * DXS];
+    __shared__ __attribute__((aligned(16))) float Xc[XCF];  // intermediate, then its gradient
+    __shared__ float Wd[kW1];
     __shared__ ChanCoef coef[kCi];
     __shared__ SinkRow sk[kCi];
-    __shared__ float red[42 * 4];
-    static_assert(DY * DXS >= (TY / 4) * (TX / 4) * kCi, "own-pixel table aliases Ds");
+    __shared__ float red[kCm * 4];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane((int)(tid >> 6));
+    const int kq = lane >> 4, nl = lane & 15;
     const int OH = 4 * a.Hi, OW = 4 * a.Wi;
     const int64_t hw = (int64_t)a.Hi * a.Wi;
     load_vt_coefs(a.x, coef, tid, kThreads);
-    stage_w1(a.w1, Wt);
+    copy_w1(a.w1, Xc);
+    __syncthreads();
+    stage_wd(Xc, Wd);
     if (tid < kCi) {
         SinkRow q = {};
         q.mode = ISG_SINK_NONE;
         if (a.dx.nsink > 0) q = sink_row(a.dx, tid, hw);
         sk[tid] = q;
     }
-    // convT weight gradient: thread <-> (co, ky, kx), all 16 input channels, across tiles
-    const int wco = tid >> 6, wky = (tid >> 3) & 7, wkx = tid & 7;
-    const int woff = (((wky & 3) * 4 + (wkx & 3)) * GJY + (wky >> 2)) * GJX + (wkx >> 2);
-    float dw1[kCi];
+    float wf[kCm][kCi];
+    cell_afrag(Xc, wf);
+    // convT weight gradient: this wave's 4 N-tiles of the [16 ci] x [256 (co, ky, kx)] GEMM
+    f32x4 dw1[4];
 #pragma unroll
-    for (int c = 0; c < kCi; ++c) dw1[c] = 0.f;
-    float dw2[kCm * 9], db2 = 0.f, db1[kCm];
-#pragma unroll
-    for (int i = 0; i < kCm * 9; ++i) dw2[i] = 0.f;
+    for (int t = 0; t < 4; ++t) dw1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // 3x3 weight / bias gradient: per-tile partials wave-reduced into LDS (acc2[37])
+    __shared__ float acc2[kCm * 9 + 1];
+    if (tid < kCm * 9 + 1) acc2[tid] = 0.f;
+    float db1[kCm];
 #pragma unroll
     for (int co = 0; co < kCm; ++co) db1[co] = 0.f;
 
     for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int n = tile / (ntx * nty), t2 = tile - n * ntx * nty;
         const int Y0 = (t2 / ntx) * TY, X0 = (t2 % ntx) * TX;
-        __syncthreads();  // previous tile's LDS consumed (and the coefficient table ready)
+        __syncthreads();  // previous tile's LDS consumed (and the tables ready)
         load_input(a, coef, n, Y0, X0, Ts);
         for (int i = tid; i < DY * DX; i += kThreads) {
             const int r = i / DX, q = i - r * DX;
@@ -216,12 +237,14 @@ __global__ __launch_bounds__(kThreads, 2) void head_bwd_kernel(isg_mask_head a, 
             Ds[r * DXS + q] = v;
         }
         __syncthreads();
-        intermediate(a, Y0, X0, Ts, Wt, Xs);
+        intermediate_mfma(a, Y0, X0, Ts, wf, Xc);  // origin (Y0 - 2, X0 - 2)
         __syncthreads();
         // ---- 3x3 weight / bias gradient over the tile's own logit pixels
         {
             const int lx = tid & 63, rb = tid >> 6;
-            float dl[8];
+            float dl[8], dw2[kCm * 9], db2 = 0.f;
+#pragma unroll
+            for (int i = 0; i < kCm * 9; ++i) dw2[i] = 0.f;
 #pragma unroll
             for (int o = 0; o < 8; ++o) {
                 dl[o] = Ds[(rb * 8 + o + 3) * DXS + lx + 3];  // zero outside the image
@@ -231,7 +254,7 @@ __global__ __launch_bounds__(kThreads, 2) void head_bwd_kernel(isg_mask_head a, 
             for (int co = 0; co < kCm; ++co) {
 #pragma unroll
                 for (int rr = 0; rr < 10; ++rr) {
-                    const float* row = Xs + co * IPL + (rb * 8 + rr) * IXS + lx;
+                    const float* row = Xc + co * IRP + (rb * 8 + rr + 1) * IRS + lx + 1;
                     const float v0 = row[0], v1 = row[1], v2 = row[2];
 #pragma unroll
                     for (int dy = 0; dy < 3; ++dy) {
@@ -243,16 +266,24 @@ __global__ __launch_bounds__(kThreads, 2) void head_bwd_kernel(isg_mask_head a, 
                     }
                 }
             }
+#pragma unroll
+            for (int i = 0; i < kCm * 9; ++i) {
+                const float w = wave_sum(dw2[i]);
+                if (lane == 0) atomicAdd(&acc2[i], w);
+            }
+            const float b = wave_sum(db2);
+            if (lane == 0) atomicAdd(&acc2[kCm * 9], b);
         }
         __syncthreads();
-        // ---- intermediate gradient over the tile + 2-pixel halo, phase-split
+        // ---- intermediate gradient over the cell region (origin (Y0 - 2, X0 - 2)), stored
+        //      phase-split: Xc[((co * 4 + r) * 4 + s) * NCELL + cy * CX + cx]
         for (int p = tid; p < GY * GX; p += kThreads) {
             const int qy = p / GX, qx = p - qy * GX;
             const int oy = Y0 - 2 + qy, ox = X0 - 2 + qx;
             const bool in = oy >= 0 && oy < OH && ox >= 0 && ox < OW;
             const bool own = qy >= 2 && qy < 2 + TY && qx >= 2 && qx < 2 + TX;
             const float* d = Ds + qy * DXS + qx;  // d[(2 - dy) * DXS + 2 - dx] = dl[oy+1-dy][ox+1-dx]
-            const int dst = (((qy & 3) * 4 + (qx & 3)) * GJY + (qy >> 2)) * GJX + (qx >> 2);
+            const int dst = ((qy & 3) * 4 + (qx & 3)) * NCELL + (qy >> 2) * CX + (qx >> 2);
 #pragma unroll
             for (int co = 0; co < kCm; ++co) {
                 float v = 0.f;
@@ -263,64 +294,52 @@ __global__ __launch_bounds__(kThreads, 2) void head_bwd_kernel(isg_mask_head a, 
                         v += a.w2[(co * 3 + dy) * 3 + dx] * d[(2 - dy) * DXS + 2 - dx];
                 v = in ? v : 0.f;
                 if (own) db1[co] += v;
-                Xs[co * XPL + dst] = v;
+                Xc[co * 16 * NCELL + dst] = v;
             }
         }
         __syncthreads();
-        // own input pixels as [px][ci] (into the free dlogits buffer): broadcast b128 reads
-        for (int i = tid; i < (TY / 4) * (TX / 4) * kCi; i += kThreads) {
-            const int c = i & 15, px = i >> 4;
-            Ds[i] = Ts[c][(px >> 4) + 1][(px & 15) + 1];
-        }
-        // ---- input gradient: thread <-> (own input pixel, 8 input channels)
+        // ---- input gradient (MFMA): D[ci][px] = sum_{o, (a,b)} Wd[o][(a,b)][ci] *
+        //      dI[o][cell (ly + 1 - a, lx + 1 - b)]; wave w: own input rows w and w + 4
         {
-            const int px = tid & 127, c0 = (wave >> 1) * 8;
-            const int ly = px >> 4, lx = px & 15;
-            float acc[8];
+            const int aa = kq >> 1, bb = kq & 1;
 #pragma unroll
-            for (int c = 0; c < 8; ++c) acc[c] = 0.f;
-            // (the weights are the same for every tile: an opaque base keeps the compiler
-            // from hoisting all 2 x 256 of their reads out of the tile loop into registers)
-            const float* wt = Wt + opaque(c0);
-#pragma unroll 1
-            for (int co = 0; co < kCm; ++co) {
-#pragma unroll 1
-                for (int ky = 0; ky < 8; ++ky) {
+            for (int h = 0; h < 2; ++h) {
+                const int ly = wave + 4 * h;
+                f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+                const float* bp = Xc + (ly + 1 - aa) * CX + (nl + 1 - bb);
+                const float* ap = Wd + lane;
+#pragma unroll 8
+                for (int o = 0; o < 64; ++o)
+                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ap[o * 64], bp[o * NCELL], acc, 0, 0, 0);
+                // D lane: ci = 4kq + i, px = (ly, nl)
+                const int iy = Y0 / 4 + ly, ix = X0 / 4 + nl;
+                if (iy < a.Hi && ix < a.Wi) {
+                    const int64_t pix = (int64_t)iy * a.Wi + ix;
 #pragma unroll
-                    for (int kx = 0; kx < 8; ++kx) {
-                        const float v = Xs[co * XPL + (((ky & 3) * 4 + (kx & 3)) * GJY + ly + (ky >> 2)) * GJX +
-                                           lx + (kx >> 2)];
-                        const float* w = wt + ((co * 8 + ky) * 8 + kx) * 16;
-                        const f32x4 wa = lds4(w), wb = lds4(w + 4);
-                        acc[0] += wa[0] * v; acc[1] += wa[1] * v; acc[2] += wa[2] * v; acc[3] += wa[3] * v;
-                        acc[4] += wb[0] * v; acc[5] += wb[1] * v; acc[6] += wb[2] * v; acc[7] += wb[3] * v;
+                    for (int i = 0; i < 4; ++i) {
+                        const SinkRow& q = sk[4 * kq + i];
+                        if (q.mode != ISG_SINK_STORE && q.mode != ISG_SINK_ACCUM) continue;
+                        float* p = q.p + (int64_t)n * q.ns + pix;
+                        *p = q.mode == ISG_SINK_ACCUM ? *p + acc[i] : acc[i];
                     }
                 }
             }
-            const int iy = Y0 / 4 + ly, ix = X0 / 4 + lx;
-            if (iy < a.Hi && ix < a.Wi) {
-                const int64_t pix = (int64_t)iy * a.Wi + ix;
-#pragma unroll
-                for (int c = 0; c < 8; ++c) {
-                    const SinkRow& q = sk[c0 + c];  // wave-uniform channel
-                    if (q.mode != ISG_SINK_STORE && q.mode != ISG_SINK_ACCUM) continue;
-                    float* p = q.p + (int64_t)n * q.ns + pix;
-                    *p = q.mode == ISG_SINK_ACCUM ? *p + acc[c] : acc[c];
-                }
-            }
         }
-        __syncthreads();  // the own-pixel table is complete
-        // ---- convT weight gradient (the own input pixels; zero outside the image)
-        for (int ly = 0; ly < TY / 4; ++ly) {
+        // ---- convT weight gradient (MFMA): K = the 128 own input pixels, 4 per step;
+        //      A[ci][px] = input, B[px][(co, ky, kx)] = dI under tap (ky, kx) of px
+        {
 #pragma unroll 2
-            for (int lx = 0; lx < TX / 4; ++lx) {
-                const float v = Xs[wco * XPL + woff + ly * GJX + lx];
-                const float* t = Ds + (ly * (TX / 4) + lx) * kCi;
+            for (int st = 0; st < (TY / 4) * (TX / 4) / 4; ++st) {
+                const int P = st * 4 + kq;
+                const int ly = P >> 4, lx = P & 15;
+                const float av = Ts[nl][ly + 1][lx + 1];
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const f32x4 t4 = lds4(t + 4 * q);
-                    dw1[4 * q + 0] += t4[0] * v; dw1[4 * q + 1] += t4[1] * v;
-                    dw1[4 * q + 2] += t4[2] * v; dw1[4 * q + 3] += t4[3] * v;
+                for (int t = 0; t < 4; ++t) {
+                    const int col = (wave * 4 + t) * 16 + nl;  // (co, ky, kx), kx fastest
+                    const int co = col >> 6, ky = (col >> 3) & 7, kx = col & 7;
+                    const float bv = Xc[((co * 4 + (ky & 3)) * 4 + (kx & 3)) * NCELL +
+                                        (ly + (ky >> 2)) * CX + lx + (kx >> 2)];
+                    dw1[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, dw1[t], 0, 0, 0);
                 }
             }
         }
@@ -329,23 +348,26 @@ __global__ __launch_bounds__(kThreads, 2) void head_bwd_kernel(isg_mask_head a, 
     const int rep = blockIdx.x % a.nrep;
     if (a.dw1) {
         float* d = a.dw1 + (int64_t)rep * a.rep_stride;
+        // D lane: ci = 4kq + i, column (co, ky, kx) = (wave * 4 + t) * 16 + nl
 #pragma unroll
-        for (int c = 0; c < kCi; ++c) atomicAdd(&d[((c * kCm + wco) * 8 + wky) * 8 + wkx], dw1[c]);
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                atomicAdd(&d[(4 * kq + i) * (kCm * 64) + (wave * 4 + t) * 16 + nl], dw1[t][i]);
     }
-    float v[kCm * 9 + 1 + kCm];
+    float v[kCm];
 #pragma unroll
-    for (int i = 0; i < kCm * 9; ++i) v[i] = wave_sum(dw2[i]);
-    v[kCm * 9] = wave_sum(db2);
-#pragma unroll
-    for (int co = 0; co < kCm; ++co) v[kCm * 9 + 1 + co] = wave_sum(db1[co]);
+    for (int co = 0; co < kCm; ++co) v[co] = wave_sum(db1[co]);
     constexpr int NV = kCm * 9 + 1 + kCm;
     __syncthreads();
     if (lane == 0)
 #pragma unroll
-        for (int i = 0; i < NV; ++i) red[i * 4 + wave] = v[i];
+        for (int co = 0; co < kCm; ++co) red[co * 4 + wave] = v[co];
     __syncthreads();
     if (tid < NV) {
-        const float s = (red[tid * 4] + red[tid * 4 + 1]) + (red[tid * 4 + 2] + red[tid * 4 + 3]);
+        const int j = tid - (kCm * 9 + 1);
+        const float s = tid <= kCm * 9 ? acc2[tid]
+                                       : (red[j * 4] + red[j * 4 + 1]) + (red[j * 4 + 2] + red[j * 4 + 3]);
         const int64_t ro = (int64_t)rep * a.rep_stride;
         float* dst = nullptr;
         if (tid < kCm * 9) dst = a.dw2 ? a.dw2 + ro + tid : nullptr;

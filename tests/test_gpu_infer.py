@@ -98,15 +98,17 @@ def test_heatmaps_random_keypoints_match_oracle():
     ref = IO.instance_heatmaps(kp, S)
     got = _heatmaps_gpu(kp, S, S)
     assert np.array_equal(got, ref)
-    # user-supplied coordinates: huge values give empty windows as in the
-    # reference (python int() is exact); NaN / inf, where the reference's int() raises,
-    # make the part not visible instead of an undefined int conversion on the GPU
+    # user-supplied coordinates: NaN / inf / +-1e300, where the reference
+    # raises (int() of a non-finite value; numpy.arange over a window bound beyond int64),
+    # give an all-zero map (the part treated as not visible) instead of an undefined int
+    # conversion on the GPU
     bad = kp.copy()
     bad[0, :4, 2] = 1.0
     bad[0, 0, 0], bad[0, 1, 1], bad[0, 2, 0], bad[0, 3, 1] = np.nan, np.inf, -np.inf, 1e300
     bad[1, 5, 0], bad[1, 5, 2] = -1e300, 1.0
     clean = bad.copy()
-    clean[0, :3, 2] = 0.0
+    clean[0, :4, 2] = 0.0
+    clean[1, 5, 2] = 0.0
     assert np.array_equal(_heatmaps_gpu(bad, S, S), IO.instance_heatmaps(clean, S))
 
 

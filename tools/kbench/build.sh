@@ -7,8 +7,9 @@ OUT=$PWD/_build
 mkdir -p $OUT
 FL="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -DISG_STAMPS -Wno-unused-function"
 objs=""
-for f in conv_mfma pw_gemm tap_conv tap_wgrad thin_conv halo_conv wgrad dw_convt eltwise maskops; do
-  /opt/rocm/bin/hipcc $FL -c $SRC/$f.hip -o $OUT/$f.o &
+for s in $SRC/*.hip; do
+  f=$(basename $s .hip)
+  /opt/rocm/bin/hipcc $FL -c $s -o $OUT/$f.o &
   objs="$objs $OUT/$f.o"
 done
 /opt/rocm/bin/hipcc $FL -x hip -c $SRC/api.cpp -o $OUT/api.o &

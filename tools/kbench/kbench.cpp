@@ -113,9 +113,32 @@ int main(int argc, char** argv) {
         s0.bn = isg_bn{gam, bet, nullptr, nullptr, ostats, Ci, 1, (float)(N * H * W), 1e-5f};
         if (getenv("KB_COEF")) { s0.bn.coef = vx.s[0].bn.coef; s0.bn.C = vx.s[0].bn.C; }
     }
+    // mask head (isg_mask_head_*): x = Ci(16) x H x W plain, logits 4H x 4W
+    isg_mask_head mh{};
+    float *hw1 = nullptr, *hw2 = nullptr, *hdl = nullptr, *hdx = nullptr, *hrep = nullptr;
+    if (!strncmp(op, "head", 4)) {
+        vx.s[0].xform = ISG_XF_PLAIN;
+        mh.x = vx;
+        hw1 = dalloc(16 * 4 * 64, 0.f, 7);
+        hw2 = dalloc(36, 0.f, 8);
+        hdl = dalloc((size_t)N * 16 * H * W, 0.f, 9);
+        CK(hipMalloc(&hdx, (size_t)N * 16 * H * W * sizeof(float)));
+        CK(hipMalloc(&hrep, (size_t)ISG_WREP * 4200 * sizeof(float)));
+        mh.w1 = hw1; mh.b1 = bet; mh.w2 = hw2; mh.b2 = bet;
+        mh.out = out; mh.out_n_stride = (int64_t)16 * H * W;
+        mh.dout = hdl; mh.dout_n_stride = (int64_t)16 * H * W;
+        mh.dx.nsink = 1;
+        mh.dx.s[0].p = hdx; mh.dx.s[0].n_stride = (int64_t)16 * H * W; mh.dx.s[0].C = 16;
+        mh.dx.s[0].mode = ISG_SINK_STORE;
+        mh.dw1 = hrep; mh.db1 = hrep + 4096; mh.dw2 = hrep + 4100; mh.db2 = hrep + 4136;
+        mh.rep_stride = 4200; mh.nrep = ISG_WREP;
+        mh.N = N; mh.Hi = H; mh.Wi = W;
+    }
     auto run = [&]() {
         int rc;
-        if (!strcmp(op, "fwd")) rc = isg_conv_fwd(&g, &vx, wt, &sk, (isg_stream_t)st);
+        if (!strcmp(op, "headf")) rc = isg_mask_head_fwd(&mh, (isg_stream_t)st);
+        else if (!strcmp(op, "headb")) rc = isg_mask_head_bwd(&mh, (isg_stream_t)st);
+        else if (!strcmp(op, "fwd")) rc = isg_conv_fwd(&g, &vx, wt, &sk, (isg_stream_t)st);
         else if (!strcmp(op, "dgrad")) rc = isg_conv_dgrad(&g, &vdy, wt, &sk, (isg_stream_t)st);
         else rc = isg_conv_wgrad_rep(&g, &vdy, &vx, dw, nullptr, nw, ISG_WREP, (isg_stream_t)st);
         if (rc) {
