@@ -643,9 +643,13 @@ __global__ __launch_bounds__(kThreads) void s2k5_fwd_kernel(DownArgs a) {
     }
     __syncthreads();
     // ---- MFMA: wave w owns output columns 16w .. 16w + 15 of every tile row
-    f32x4 acc[kS2Rows];
+    // two partial accumulators per row (alternate channel groups): four independent
+    // MFMA chains, so a dependent MFMA never waits out the 40-cycle result latency
+    f32x4 acc2[2][kS2Rows];
 #pragma unroll
-    for (int r = 0; r < kS2Rows; ++r) acc[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int r = 0; r < kS2Rows; ++r) acc2[h][r] = f32x4{0.f, 0.f, 0.f, 0.f};
     const float* lb = Ls + kq * kS2PL + wave * 16 + pl;
 #pragma unroll
     for (int g = 0; g < kMaxM / 4; ++g) {
@@ -658,10 +662,13 @@ __global__ __launch_bounds__(kThreads) void s2k5_fwd_kernel(DownArgs a) {
                 const int col = (kw & 1) * kS2EW + (kw >> 1) + 1;
 #pragma unroll
                 for (int r = 0; r < kS2Rows; ++r)
-                    acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[g][kh * K + kw],
-                                                                  lg[(2 * r + kh) * kS2RS + col], acc[r], 0, 0, 0);
+                    acc2[g & 1][r] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                        wa[g][kh * K + kw], lg[(2 * r + kh) * kS2RS + col], acc2[g & 1][r], 0, 0, 0);
             }
     }
+    f32x4 acc[kS2Rows];
+#pragma unroll
+    for (int r = 0; r < kS2Rows; ++r) acc[r] = acc2[0][r] + acc2[1][r];
     // ---- epilogue: lane holds D[m = 4kq + i][px = pl] of each tile row
     float bs0[4] = {0.f, 0.f, 0.f, 0.f}, bs1[4] = {0.f, 0.f, 0.f, 0.f}, bs2[4] = {0.f, 0.f, 0.f, 0.f};
     const int ox = ox0 + wave * 16 + pl;
