@@ -354,10 +354,9 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
         }
     }
     tabA[tid] = ch_addr(vs, tc, a.HW);
-    __syncthreads();
-    STAMP(1);
-
-    // ---- phase 2: activation slab loads -------------------------------------------------
+    // ---- phase 2: activation slab loads, issued in the same round trip as phase 1 (the
+    //      channel addresses come from the kernel arguments alone; only the transform
+    //      needs the coefficient table, after the barrier)
     const int q = tid % QPR, cr = tid / QPR;
     const int64_t pg = p0 + 4 * q;
     const bool pv = pg < a.P;
@@ -366,10 +365,12 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
     f32x4 xv[XU], yv[XU];
 #pragma unroll
     for (int u = 0; u < XU; ++u) {
-        const ChSrc t = tabA[min(cr + u * CPP, K - 1)];
+        const ChSrc t = ch_addr(vs, min(cr + u * CPP, K - 1), a.HW);
         xv[u] = gld4(t.p, (int64_t)n * t.ns + pix);
         if (HY) yv[u] = gld4(t.y, (int64_t)n * t.yns + pix);
     }
+    __syncthreads();
+    STAMP(1);
     // phase-1 results -> LDS (waits for phase-1 loads only)
     if (a.fast) {
         if (tid < K) tabK[tid] = coef_finish(vs, tid, cfl);
