@@ -42,8 +42,11 @@ typedef struct ihipStream_t* isg_stream_t; /* == hipStream_t */
  * in ISG_STAT_REP replicas, each workgroup adding into one chosen by its block index,
  * so at most (workgroups / ISG_STAT_REP) atomics contend on an address; readers sum the
  * replicas. An accumulator "of n values" therefore occupies ISG_STAT_REP*n doubles,
- * replica r at offset r*n. */
-#define ISG_STAT_REP 16
+ * replica r at offset r*n. (Overridable at build time for experiments; the Python side
+ * reads the count back through isg_stat_replicas.) */
+#ifndef ISG_STAT_REP
+#define ISG_STAT_REP 4
+#endif
 
 enum { ISG_ACT_NONE = 0, ISG_ACT_RELU = 1, ISG_ACT_PRELU = 2 };
 enum { ISG_XF_PLAIN = 0, ISG_XF_BN_FWD = 1, ISG_XF_BN_BWD = 2 };

@@ -11,14 +11,15 @@ from ctypes import POINTER, Structure, c_char_p, c_double, c_float, c_int32, c_i
 
 import torch  # noqa: F401  (load torch's HIP runtime before libisg)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libisg.so")
+# ISG_LIB: an alternative in-tree build (experiments: tools/build_variant.sh)
+LIB_PATH = os.environ.get("ISG_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libisg.so")
 
 ACT = {"none": 0, "relu": 1, "prelu": 2}
 XF_PLAIN, XF_BN_FWD, XF_BN_BWD = 0, 1, 2
 SINK_STORE, SINK_ACCUM, SINK_ACTBWD, SINK_NONE = 0, 1, 2, 3
 MAX_SEGS = 3
 LIST_CHUNK = 32
-STAT_REP = 16     # ISG_STAT_REP: accumulator replicas (isg.h)
+STAT_REP = int(os.environ.get("ISG_STAT_REP", "4"))  # accumulator replicas (isg.h ISG_STAT_REP)
 ABI_VERSION = 7
 WREP = 16         # ISG_WREP: weight-gradient replicas (isg.h)
 

@@ -811,8 +811,12 @@ int32_t isg_sub2_dgrad(const isg_conv_geom* g, const isg_vtensor* dy, const floa
 // Returns 1 if launched, 0 if the shape is not for this kernel, <0 on error.
 int32_t isg_s2k5_fwd(const isg_conv_geom* g, const isg_vtensor* x, const float* w,
                      const isg_sinks* out, hipStream_t st) {
-    static const bool off = getenv("ISG_NO_S2K5") != nullptr;
-    if (off || g->groups != 1 || g->SH != 2 || g->SW != 2 || g->KH != 5 || g->KW != 5 ||
+    // opt-in (ISG_S2K5=1, read per call so a test can switch it): ~3 us faster than
+    // tap_conv in the bench step, but its summation order tipped one full-size gradient
+    // check (2x800x1344, tests/test_gpu_trainer.py) past the statistical bar; the unit
+    // test holds it to fp64 at that geometry (tests/test_gpu_kernels.py::test_s2k5_fwd)
+    const char* on = getenv("ISG_S2K5");
+    if (!on || on[0] != '1' || g->groups != 1 || g->SH != 2 || g->SW != 2 || g->KH != 5 || g->KW != 5 ||
         g->PH != 2 || g->PW != 2 || g->DH != 1 || g->DW != 1 || g->H != 2 * g->OH ||
         g->W != 2 * g->OW || g->W % 4 || g->Co > kMaxM || g->Ci > kMaxM ||
         (g->w_ci && g->w_ci != g->Ci) || !down_src_ok(x))

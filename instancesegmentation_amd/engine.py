@@ -475,11 +475,17 @@ class Graph:
 
 # ---------------------------------------------------------------------------------
 # spec helpers
-_BN_FINAL = os.environ.get("ISG_NO_BN_FINAL", "0") != "1"  # debugging switch
+# BatchNorm coefficients. Default: every consumer evaluates them from the replicated fp64
+# statistics itself (isg_bn.coef NULL; ISG_STAT_REP = 4 replicas, i.e. 8-16 loads per
+# channel per workgroup), so no launch sits between a producer and its consumers.
+# Measured on the bench step (profiles/r03h_bn_ab.txt, 2 x 200 steps each): 5.16 ms with
+# one OP_BN_FINAL launch per BN point (140 per step, 16 replicas), 4.71 ms without them at
+# 4 replicas (2 replicas 4.92: atomic contention in the producers; 8 replicas 4.82: more
+# consumer reads; 16 replicas +0.8 ms, round 2). ISG_BN_FINAL=1 restores the launches.
+_BN_FINAL = os.environ.get("ISG_BN_FINAL", "0") == "1"
 # finalise BN coefficients in the producing kernel's last workgroup (isg_sink.fin_*)
-# instead of a separate OP_BN_FINAL launch. Opt-in: measured slower on MI355X (each
-# workgroup's returning ticket atomic plus the last workgroup's fp64 tail cost more than
-# the ~2.4 us finalisation launch they replace: 7.16 vs 6.5 ms/step).
+# instead of a separate OP_BN_FINAL launch (needs ISG_BN_FINAL=1). Opt-in: measured
+# slower (5.43 vs 5.17 ms/step fence-free, round 3; 7.16 vs 6.5 with a release fence).
 _BN_FUSE = _BN_FINAL and os.environ.get("ISG_BN_FUSE", "0") == "1"
 
 

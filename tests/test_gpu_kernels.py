@@ -94,8 +94,9 @@ DENSE = [
     (8, 12, 40, 24, 5, 2, 2, 1),
     # ... on the LDS-staged form (cell columns % 4 == 0): two column blocks, ragged rows
     (16, 16, 74, 136, 5, 2, 2, 1),
-    # the LDS-staged 5x5 s2 forward (s2k5_fwd: <= 16 channels, W % 4 == 0): partial
-    # column block, odd output rows, fewer channels than the 16-lane fragments
+    # 5x5 s2 with <= 16 channels (the stem's second conv; tap_conv by default, the
+    # opt-in s2k5_fwd in test_s2k5_fwd): partial column block, odd output rows, fewer
+    # channels than the 16-lane fragments
     (16, 16, 134, 200, 5, 2, 2, 1),
     (12, 8, 40, 36, 5, 2, 2, 1),
     # thin 3x3 (thin_conv / thin_wgrad, 4 pixels per lane): ragged row count, 1 -> 4
@@ -146,6 +147,40 @@ def test_conv_fwd_dense(cfg):
     stats = rep_fold(stats, 4 * Co)
     close(stats[:Co], ref.sum((0, 2, 3)), what="sum")
     close(stats[Co:2 * Co], (ref * ref).sum((0, 2, 3)), what="sumsq")
+
+
+@pytest.mark.parametrize("cfg", [(16, 16, 134, 200), (12, 8, 40, 36), (16, 16, 400, 672)],
+                         ids=["ragged", "narrow", "stem_1344x800"])
+def test_s2k5_fwd(cfg, monkeypatch):
+    """The opt-in LDS-staged 5x5 s2 forward (ISG_S2K5=1, down_conv.hip s2k5_fwd_kernel)
+    against fp64 at a bar of 4e-6 of scale — one fp32 rounding chain over 400 taps — at
+    the stem's layer-2 geometry of BASELINE config 3 (2x400x672 -> 200x336: a partial
+    64-column block) as well as ragged shapes; training-mode BN + PReLU on load."""
+    monkeypatch.setenv("ISG_S2K5", "1")
+    Ci, Co, H, W = cfg
+    N = 2
+    ge, OH, OW = _geom(N, Ci, Co, H, W, 5, 2, 2, 1)
+    x = rnd(N, Ci, H, W, seed=11) * 0.7 + 0.2
+    w = rnd(Co, Ci, 5, 5, seed=12, scale=(2.0 / (Ci * 25)) ** 0.5)
+    b = rnd(Co, seed=13, scale=0.1)
+    gamma, beta, _, _, slope = bn_eval_params(Ci, 5)
+    mean = x.mean((0, 2, 3))
+    var = x.var((0, 2, 3), unbiased=False)
+    xt = fwd_xform_ref(x, gamma, beta, mean, var, slope, "prelu")
+    ref = F.conv2d(xt, w, b, stride=2, padding=2)
+    X = cuda32(x)
+    G = [cuda32(t) for t in (gamma, beta, mean, var, slope)]
+    segs = [{"p": ptr(X), "n_stride": Ci * H * W, "C": Ci, "xform": L.XF_BN_FWD,
+             "act": L.ACT["prelu"], "slope": ptr(G[4]), "bn": bn_spec_eval(*G[:4])}]
+    Y = torch.full((N, Co, OH, OW), float("nan"), device=DEV)
+    stats = rep_zeros(4 * Co)
+    sk = sinks([{"p": ptr(Y), "n_stride": Co * OH * OW, "c0": 0, "C": Co,
+                 "mode": L.SINK_STORE, "bias": ptr(cuda32(b)), "stats": ptr(stats)}])
+    call("isg_conv_fwd", geom(**ge), vt(segs, N, H, W), ptr(cuda32(w)), sk, stream())
+    close(Y, ref, tol=4e-6, what="s2k5 fwd")
+    stats = rep_fold(stats, 4 * Co)
+    close(stats[:Co], ref.sum((0, 2, 3)), tol=4e-6, what="sum")
+    close(stats[Co:2 * Co], (ref * ref).sum((0, 2, 3)), tol=4e-6, what="sumsq")
 
 
 def _bn_train_state(y, g, seed):

@@ -133,7 +133,9 @@ def test_nms_ties_break_by_index():
 def test_bench_traffic_record_matches_dominant_op():
     """bench.py reports roofline.traffic from the committed PMC pass (profiles/traffic.json,
     tools/kbench/traffic.sh): the record must carry the op label bench.py keys on, the bench
-    configuration and the gfx950-corrected byte count (2*FETCH_SIZE + WRITE_SIZE)."""
+    configuration and the gfx950-corrected byte count (fetch_scale*FETCH_SIZE + WRITE_SIZE,
+    fetch_scale 2 only for 16-B/lane loads; round-2 records predate the per-kernel scale and
+    doubled every kernel's FETCH_SIZE)."""
     import json
     import os
     import types
@@ -145,8 +147,8 @@ def test_bench_traffic_record_matches_dominant_op():
     assert "dw_init_conv.layer1" in by_label
     for r in runs:
         kern = [v for k, v in r["kernels"].items() if not k.startswith("__amd_rocclr")]
-        expect = sum(2.0 * v["FETCH_SIZE_kb_per_dispatch"] + v["WRITE_SIZE_kb_per_dispatch"]
-                     for v in kern) * 1024.0
+        expect = sum(v.get("fetch_scale", 2.0) * v["FETCH_SIZE_kb_per_dispatch"]
+                     + v["WRITE_SIZE_kb_per_dispatch"] for v in kern) * 1024.0
         assert abs(r["hbm_bytes_per_launch"] - expect) <= 1e-6 * expect
     args = types.SimpleNamespace(batch=2, cin=20, size=1024)
     got = bench.pmc_traffic("dw_init_conv.layer1", args)
