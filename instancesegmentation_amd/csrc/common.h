@@ -60,13 +60,43 @@ ISG_DEV double rep_sum(const double* base, int n, int i, bool fresh = false) {
     return s;
 }
 
+// The fp64 coefficient math from replica-summed statistics: the one definition shared by
+// fwd_coef / bwd_coef and the branch-free staging path (stage.h coef_issue / coef_finish),
+// so every consumer derives bit-identical coefficients.
+ISG_DEV void mean_rstd_of(double sum, double sumsq, float count, float eps, double& mean,
+                          double& rstd) {
+    double inv = 1.0 / (double)count;
+    mean = sum * inv;
+    double var = sumsq * inv - mean * mean;
+    if (var < 0.0) var = 0.0;
+    rstd = 1.0 / sqrt(var + (double)eps);
+}
+ISG_DEV ChanCoef fwd_coef_of(double mean, double rstd, float gamma, float beta, float slope) {
+    ChanCoef k;
+    k.c0 = (float)mean;
+    k.c1 = (float)((double)gamma * rstd);
+    k.c2 = beta;
+    k.c3 = slope;
+    return k;
+}
+ISG_DEV ChanCoef bwd_coef_of(double mean, double rstd, float gamma, double gs, double gxs,
+                             float count) {
+    const double gam = (double)gamma;
+    const double inv = 1.0 / (double)count;
+    const double mg = gs * inv;
+    const double mgx = rstd * gxs * inv;  // mean(g * xhat); gxs = sum g*(y - mean), centred
+    ChanCoef k;
+    k.c0 = (float)(gam * rstd);
+    k.c1 = (float)(-gam * rstd * rstd * mgx);
+    k.c2 = (float)mean;
+    k.c3 = (float)(-gam * rstd * mg);
+    return k;
+}
+
 ISG_DEV void bn_mean_rstd(const isg_bn& bn, int c, double& mean, double& rstd, bool fresh = false) {
     if (bn.train) {
-        double inv = 1.0 / (double)bn.count;
-        mean = rep_sum(bn.stats, 4 * bn.C, c, fresh) * inv;
-        double var = rep_sum(bn.stats, 4 * bn.C, bn.C + c, fresh) * inv - mean * mean;
-        if (var < 0.0) var = 0.0;
-        rstd = 1.0 / sqrt(var + (double)bn.eps);
+        mean_rstd_of(rep_sum(bn.stats, 4 * bn.C, c, fresh), rep_sum(bn.stats, 4 * bn.C, bn.C + c, fresh),
+                     bn.count, bn.eps, mean, rstd);
     } else {
         mean = (double)bn.running_mean[c];
         rstd = 1.0 / sqrt((double)bn.running_var[c] + (double)bn.eps);
@@ -81,12 +111,7 @@ ISG_DEV ChanCoef fwd_coef(const isg_bn& bn, const float* slope, int c, bool fres
     }
     double mean, rstd;
     bn_mean_rstd(bn, c, mean, rstd, fresh);
-    ChanCoef k;
-    k.c0 = (float)mean;
-    k.c1 = (float)((double)bn.gamma[c] * rstd);
-    k.c2 = bn.beta[c];
-    k.c3 = slope ? slope[c] : 0.f;
-    return k;
+    return fwd_coef_of(mean, rstd, bn.gamma[c], bn.beta[c], slope ? slope[c] : 0.f);
 }
 
 // backward coefficients: dy = A*g + B*(y-mean) + C
@@ -100,15 +125,8 @@ ISG_DEV ChanCoef bwd_coef(const isg_bn& bn, int c, bool fresh = false) {
     double gam = (double)bn.gamma[c];
     ChanCoef k;
     if (bn.train) {
-        double inv = 1.0 / (double)bn.count;
-        double gs = rep_sum(bn.stats, 4 * bn.C, 2 * bn.C + c, fresh);
-        double gxs = rep_sum(bn.stats, 4 * bn.C, 3 * bn.C + c, fresh);  // sum g*(y - mean), centred
-        double mg = gs * inv;
-        double mgx = rstd * gxs * inv;         // mean(g * xhat)
-        k.c0 = (float)(gam * rstd);
-        k.c1 = (float)(-gam * rstd * rstd * mgx);
-        k.c2 = (float)mean;
-        k.c3 = (float)(-gam * rstd * mg);
+        k = bwd_coef_of(mean, rstd, bn.gamma[c], rep_sum(bn.stats, 4 * bn.C, 2 * bn.C + c, fresh),
+                        rep_sum(bn.stats, 4 * bn.C, 3 * bn.C + c, fresh), bn.count);
     } else {
         k.c0 = (float)(gam * rstd);
         k.c1 = 0.f;

@@ -335,7 +335,7 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
     const VtSel vs = vt_sel(a.src);
     const SkSel ks = sk_sel(a.out);
     const int tc = min(tid, K - 1);
-    const CoefLoad cfl = coef_issue(vs, tc);
+    const CoefLoad<HY ? 4 : 2> cfl = coef_issue<HY ? 4 : 2>(vs, tc);
     const int trow = min(tid, Mb - 1);
     const SinkLoad skl = sink_issue(ks, m0 + trow, w);
     f32x4 wv[WU];
@@ -602,8 +602,7 @@ bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 // host mirrors of stage.h vt_fast / sinks_fast
 bool host_seg_fast(const isg_vseg& s) {
-    if (s.xform == ISG_XF_BN_FWD) return s.bn.coef || (!s.bn.stats && s.bn.train);
-    if (s.xform == ISG_XF_BN_BWD) return s.bn.coef != nullptr;
+    if (s.xform == ISG_XF_BN_FWD || s.xform == ISG_XF_BN_BWD) return s.bn.coef || s.bn.train;
     return true;
 }
 bool host_vt_fast(const isg_vtensor& v) {
@@ -614,7 +613,7 @@ bool host_vt_fast(const isg_vtensor& v) {
 bool host_sinks_fast(const isg_sinks& sk) {
     for (int s = 0; s < sk.nsink; ++s) {
         const isg_sink& k = sk.s[s];
-        if (k.mode == ISG_SINK_ACTBWD && !(k.bn.coef || (!k.bn.stats && k.bn.train))) return false;
+        if (k.mode == ISG_SINK_ACTBWD && !(k.bn.coef || k.bn.train)) return false;
     }
     return true;
 }

@@ -237,9 +237,11 @@ ISG_DEV void sink_row_apply(const SinkRow& q, int n, int64_t pix, float v, float
 // weight and activation loads: any branch around a load makes the compiler drain the
 // whole memory queue (s_waitcnt vmcnt(0)) at the join, which serialised the first slab
 // kernels into one HBM round trip per load.
+// "fast" = every record comes from plain branch-free loads: finalised coefficients, or
+// (training mode) the statistics replicas evaluated in coef_finish / sink_finish
+// (consumer-side finalisation). Eval mode (running statistics) takes the slow path.
 ISG_DEV bool seg_fast(const isg_vseg& s) {
-    if (s.xform == ISG_XF_BN_FWD) return s.bn.coef || (!s.bn.stats && s.bn.train);
-    if (s.xform == ISG_XF_BN_BWD) return s.bn.coef != nullptr;
+    if (s.xform == ISG_XF_BN_FWD || s.xform == ISG_XF_BN_BWD) return s.bn.coef || s.bn.train;
     return true;
 }
 ISG_DEV bool vt_fast(const isg_vtensor& v) {
@@ -249,7 +251,7 @@ ISG_DEV bool vt_fast(const isg_vtensor& v) {
     return ok;
 }
 ISG_DEV bool sink_fast(const isg_sink& k) {
-    return k.mode != ISG_SINK_ACTBWD || k.bn.coef || (!k.bn.stats && k.bn.train);
+    return k.mode != ISG_SINK_ACTBWD || k.bn.coef || k.bn.train;
 }
 ISG_DEV bool sinks_fast(const isg_sinks& sk) {
     bool ok = sink_fast(sk.s[0]);
@@ -266,17 +268,57 @@ ISG_DEV int sgpr_i(int v) { return __builtin_amdgcn_readfirstlane(v); }
 template <class T>
 ISG_DEV T* sgpr_p(T* p) { return uniform_ptr(p); }
 
+ISG_DEV float sgpr_f(float v) { return __builtin_bit_cast(float, sgpr_i(__builtin_bit_cast(int, v))); }
+
 struct SegLite {
-    const float *p, *y, *coef, *slope;
+    const float *p, *y, *coef, *slope, *gamma, *beta;
+    const double* stats;
     int ns, yns, xf, act, bnC, C;
+    float count, eps;
 };
 ISG_DEV SegLite seg_lite(const isg_vseg& g) {
     SegLite l;
     l.p = sgpr_p(g.p); l.y = sgpr_p(g.y); l.coef = sgpr_p((const float*)g.bn.coef);
     l.slope = sgpr_p(g.slope);
+    l.gamma = sgpr_p(g.bn.gamma); l.beta = sgpr_p(g.bn.beta);
+    l.stats = sgpr_p((const double*)g.bn.stats);
     l.ns = sgpr_i((int)g.n_stride); l.yns = sgpr_i((int)g.y_n_stride);
     l.xf = sgpr_i(g.xform); l.act = sgpr_i(g.act); l.bnC = sgpr_i(g.bn.C); l.C = sgpr_i(g.C);
+    l.count = sgpr_f(g.bn.count); l.eps = sgpr_f(g.bn.eps);
     return l;
+}
+
+// Consumer-side BatchNorm finalisation in the caller's load round trip: the ISG_STAT_REP
+// replicas of NG statistics groups of one channel (NG = 2: sum, sum^2; NG = 4: + gsum,
+// gxsum for BatchNorm backward) plus gamma / beta, issued branch-free — a NULL `stats`
+// (finalised coefficients present, or no BatchNorm) reads a valid dummy address instead
+// and stat_finish never looks at the values.
+template <int NG>
+struct StatLoad {
+    double v[NG][ISG_STAT_REP];
+    float gamma, beta;
+};
+template <int NG>
+ISG_DEV StatLoad<NG> stat_issue(const double* stats, const float* gamma, const float* beta,
+                                int bnC, int cl, const float* any) {
+    StatLoad<NG> r;
+    const bool on = stats != nullptr;
+    const double* sp = on ? stats : reinterpret_cast<const double*>(any);
+#pragma unroll
+    for (int g = 0; g < NG; ++g)
+#pragma unroll
+        for (int q = 0; q < ISG_STAT_REP; ++q)
+            r.v[g][q] = sp[on ? (int64_t)q * 4 * bnC + (int64_t)g * bnC + cl : 0];
+    r.gamma = gld(gamma && on ? gamma + cl : any, 0);
+    r.beta = gld(beta && on ? beta + cl : any, 0);
+    return r;
+}
+template <int NG>
+ISG_DEV double stat_sum(const StatLoad<NG>& r, int g) {  // rep_sum's order
+    double s = 0.0;
+#pragma unroll
+    for (int q = 0; q < ISG_STAT_REP; ++q) s += r.v[g][q];
+    return s;
 }
 struct VtSel {
     SegLite s0, s1, s2;
@@ -292,9 +334,11 @@ ISG_DEV VtSel vt_sel(const isg_vtensor& vt) {
 }
 #define ISG_SEL3(s, f, v) ((s) == 2 ? (v).s2.f : ((s) == 1 ? (v).s1.f : (v).s0.f))
 
+template <int NG = 4>
 struct CoefLoad {
     f32x4 f;
     float sl;
+    StatLoad<NG> st;
 };
 
 ISG_DEV int vt_seg(const VtSel vt, int c, int& cl) {
@@ -305,7 +349,10 @@ ISG_DEV int vt_seg(const VtSel vt, int c, int& cl) {
     return s;
 }
 
-ISG_DEV CoefLoad coef_issue(const VtSel vt, int c) {
+// NG: statistics groups to load for consumer-side finalisation — 2 when no segment is
+// BN_BWD, 4 otherwise (a BN_FWD channel then loads its 2 groups twice)
+template <int NG = 4>
+ISG_DEV CoefLoad<NG> coef_issue(const VtSel vt, int c) {
     int cl;
     const int s = vt_seg(vt, c, cl);
     const float* coef = ISG_SEL3(s, coef, vt);
@@ -316,24 +363,44 @@ ISG_DEV CoefLoad coef_issue(const VtSel vt, int c) {
     const int idx = xf == ISG_XF_BN_BWD ? bnC + cl : cl;
     const float* cp = coef ? coef + 4 * (int64_t)idx : p;
     const float* sp = slope ? slope + cl : p;
-    CoefLoad r;
+    const bool bn = xf == ISG_XF_BN_FWD || xf == ISG_XF_BN_BWD;
+    const double* st = bn && !coef ? ISG_SEL3(s, stats, vt) : nullptr;
+    CoefLoad<NG> r;
     r.f = f32x4{gld(cp, 0), gld(cp, 1), gld(cp, 2), gld(cp, 3)};
     r.sl = gld(sp, 0);
+    r.st = stat_issue<NG>(st, ISG_SEL3(s, gamma, vt), ISG_SEL3(s, beta, vt), bnC, cl, p);
     return r;
 }
 
-ISG_DEV ChanCoef coef_finish(const VtSel vt, int c, const CoefLoad& r) {
+template <int NG = 4>
+ISG_DEV ChanCoef coef_finish(const VtSel vt, int c, const CoefLoad<NG>& r) {
     int cl;
     const int s = vt_seg(vt, c, cl);
     const bool has_coef = ISG_SEL3(s, coef, vt) != nullptr;
+    const bool has_stats = ISG_SEL3(s, stats, vt) != nullptr;
     const bool has_slope = ISG_SEL3(s, slope, vt) != nullptr;
     const int xf = ISG_SEL3(s, xf, vt);
     ChanCoef k = {0.f, 1.f, 0.f, 0.f};
     if (xf == ISG_XF_BN_FWD) {
-        if (has_coef) { k.c0 = r.f[0]; k.c1 = r.f[1]; k.c2 = r.f[2]; }
+        if (has_coef) {
+            k.c0 = r.f[0]; k.c1 = r.f[1]; k.c2 = r.f[2];
+        } else if (has_stats) {  // training mode, consumer-side finalisation
+            double mean, rstd;
+            mean_rstd_of(stat_sum(r.st, 0), stat_sum(r.st, 1), ISG_SEL3(s, count, vt),
+                         ISG_SEL3(s, eps, vt), mean, rstd);
+            k = fwd_coef_of(mean, rstd, r.st.gamma, r.st.beta, 0.f);
+        }
         k.c3 = has_slope ? r.sl : 0.f;
     } else if (xf == ISG_XF_BN_BWD) {
-        k = ChanCoef{r.f[0], r.f[1], r.f[2], r.f[3]};
+        if (has_coef) {
+            k = ChanCoef{r.f[0], r.f[1], r.f[2], r.f[3]};
+        } else if constexpr (NG == 4) {
+            double mean, rstd;
+            mean_rstd_of(stat_sum(r.st, 0), stat_sum(r.st, 1), ISG_SEL3(s, count, vt),
+                         ISG_SEL3(s, eps, vt), mean, rstd);
+            k = bwd_coef_of(mean, rstd, r.st.gamma, stat_sum(r.st, 2), stat_sum(r.st, 3),
+                            ISG_SEL3(s, count, vt));
+        }
     }
     return k;
 }
@@ -355,15 +422,20 @@ ISG_DEV ChSrc ch_addr(const VtSel vt, int c, int64_t hw) {
 
 struct SinkLite {
     float *p;
-    const float *y, *coef, *bias, *slope;
-    int ns, yns, mode, act, c0;
+    const float *y, *coef, *bias, *slope, *gamma, *beta;
+    const double* stats;
+    int ns, yns, mode, act, c0, bnC;
+    float count, eps;
 };
 ISG_DEV SinkLite sink_lite(const isg_sink& k) {
     SinkLite l;
     l.p = sgpr_p(k.p); l.y = sgpr_p(k.y); l.coef = sgpr_p((const float*)k.bn.coef);
     l.bias = sgpr_p(k.bias); l.slope = sgpr_p(k.slope);
+    l.gamma = sgpr_p(k.bn.gamma); l.beta = sgpr_p(k.bn.beta);
+    l.stats = sgpr_p((const double*)k.bn.stats);
     l.ns = sgpr_i((int)k.n_stride); l.yns = sgpr_i((int)k.y_n_stride);
-    l.mode = sgpr_i(k.mode); l.act = sgpr_i(k.act); l.c0 = sgpr_i(k.c0);
+    l.mode = sgpr_i(k.mode); l.act = sgpr_i(k.act); l.c0 = sgpr_i(k.c0); l.bnC = sgpr_i(k.bn.C);
+    l.count = sgpr_f(k.bn.count); l.eps = sgpr_f(k.bn.eps);
     return l;
 }
 struct SkSel {
@@ -382,6 +454,7 @@ ISG_DEV SkSel sk_sel(const isg_sinks& sk) {
 struct SinkLoad {
     f32x4 f;
     float bias, sl;
+    StatLoad<2> st;  // ACTBWD without finalised coefficients: the output BN's statistics
 };
 
 ISG_DEV int sk_seg(const SkSel sk, int m, int& cl) {
@@ -402,10 +475,14 @@ ISG_DEV SinkLoad sink_issue(const SkSel sk, int m, const float* any) {
     const float* cp = coef ? coef + 4 * (int64_t)cl : any;
     const float* bp = bias ? bias + cl : any;
     const float* sp = slope ? slope + cl : any;
+    const int mode = ISG_SEL3(s, mode, sk);
+    const double* st = mode == ISG_SINK_ACTBWD && !coef ? ISG_SEL3(s, stats, sk) : nullptr;
     SinkLoad r;
     r.f = f32x4{gld(cp, 0), gld(cp, 1), gld(cp, 2), gld(cp, 3)};
     r.bias = gld(bp, 0);
     r.sl = gld(sp, 0);
+    r.st = stat_issue<2>(st, ISG_SEL3(s, gamma, sk), ISG_SEL3(s, beta, sk), ISG_SEL3(s, bnC, sk), cl,
+                         any);
     return r;
 }
 
@@ -424,7 +501,15 @@ ISG_DEV SinkRow sink_finish(const SkSel sk, int m, int64_t hw, const SinkLoad& l
     q.bias = ISG_SEL3(s, bias, sk) ? l.bias : 0.f;
     q.f = SinkCoef{0.f, 1.f, 0.f, 0.f};
     if (q.mode == ISG_SINK_ACTBWD) {
-        if (ISG_SEL3(s, coef, sk)) { q.f.mean = l.f[0]; q.f.scale = l.f[1]; q.f.beta = l.f[2]; }
+        if (ISG_SEL3(s, coef, sk)) {
+            q.f.mean = l.f[0]; q.f.scale = l.f[1]; q.f.beta = l.f[2];
+        } else if (ISG_SEL3(s, stats, sk)) {  // consumer-side finalisation (fwd_coef's math)
+            double mean, rstd;
+            mean_rstd_of(stat_sum(l.st, 0), stat_sum(l.st, 1), ISG_SEL3(s, count, sk),
+                         ISG_SEL3(s, eps, sk), mean, rstd);
+            const ChanCoef f = fwd_coef_of(mean, rstd, l.st.gamma, l.st.beta, 0.f);
+            q.f.mean = f.c0; q.f.scale = f.c1; q.f.beta = f.c2;
+        }
         q.f.slope = ISG_SEL3(s, slope, sk) ? l.sl : 0.f;
     }
     return q;

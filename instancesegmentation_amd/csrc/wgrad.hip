@@ -376,7 +376,8 @@ __global__ __launch_bounds__(kThreads) void pwg_kernel(PwgArgs a) {
     {
         const VtSel vd = vt_sel(a.dy), vx = vt_sel(a.x);
         const ChSrc ad = ch_addr(vd, cdy, a.HW), ax = ch_addr(vx, cx, a.HW);
-        const CoefLoad ld = coef_issue(vd, cdy), lx = coef_issue(vx, cx);
+        const CoefLoad<4> ld = coef_issue<4>(vd, cdy);
+        const CoefLoad<2> lx = coef_issue<2>(vx, cx);
         ChSrc& e = tabA[tid];  // field by field: a select of whole records goes through scratch
         e.p = is_dy ? ad.p : ax.p; e.y = is_dy ? ad.y : ax.y;
         e.ns = is_dy ? ad.ns : ax.ns; e.yns = is_dy ? ad.yns : ax.yns;
@@ -497,8 +498,9 @@ bool pwg_has_y(const isg_vtensor& v) {
 bool pwg_fast(const isg_vtensor& v) {
     for (int s = 0; s < v.nseg; ++s) {
         const isg_vseg& g = v.s[s];
-        if (g.xform == ISG_XF_BN_FWD && !(g.bn.coef || (!g.bn.stats && g.bn.train))) return false;
-        if (g.xform == ISG_XF_BN_BWD && !g.bn.coef) return false;
+        // stage.h seg_fast: finalised coefficients or training-mode statistics
+        if ((g.xform == ISG_XF_BN_FWD || g.xform == ISG_XF_BN_BWD) && !(g.bn.coef || g.bn.train))
+            return false;
     }
     return true;
 }

@@ -311,6 +311,8 @@ class Graph:
             "gamma": self.tptr(bn, "weight"), "beta": self.tptr(bn, "bias"),
             "rm": self.tptr(bn, "running_mean"), "rv": self.tptr(bn, "running_var"),
             "nbt": self.tptr(bn, "num_batches_tracked")})
+        # finalised once per layer by an OP_BN_FINAL launch, or by every consumer
+        ref.fin = _BN_FINAL or count >= _BN_FINAL_COUNT
         ref.gname = (bn, "weight")
         ref.bname = (bn, "bias")
         # finalised coefficients (isg_bn.coef): 8*C floats = 4*C doubles, 64-B aligned
@@ -483,6 +485,12 @@ class Graph:
 # 4 replicas (2 replicas 4.92: atomic contention in the producers; 8 replicas 4.82: more
 # consumer reads; 16 replicas +0.8 ms, round 2). ISG_BN_FINAL=1 restores the launches.
 _BN_FINAL = os.environ.get("ISG_BN_FINAL", "0") == "1"
+# ... except where the consumers are many small workgroups: every one of them re-reads the
+# same statistics lines (an L2 hot spot) and evaluates them in fp64, which cost more than
+# the launch on the 256^2 decoder's 4 <-> 16-channel layers (thin_pw, one-wave workgroups:
+# +9-12 us per op). BN points normalising >= this many values (N*H*W) keep one
+# OP_BN_FINAL launch.
+_BN_FINAL_COUNT = int(os.environ.get("ISG_BN_FINAL_COUNT", "131072"))
 # finalise BN coefficients in the producing kernel's last workgroup (isg_sink.fin_*)
 # instead of a separate OP_BN_FINAL launch (needs ISG_BN_FINAL=1). Opt-in: measured
 # slower (5.43 vs 5.17 ms/step fence-free, round 3; 7.16 vs 6.5 with a release fence).
@@ -564,7 +572,7 @@ def bn_spec(bnr, train, coef=True):
     s = {"gamma": n["gamma"], "beta": n["beta"], "running_mean": n["rm"],
          "running_var": n["rv"], "stats": Ptr(S_STATS, bnr.stats_off * 8), "C": bnr.C,
          "train": 1 if train else 0, "count": float(bnr.count), "eps": float(bnr.mod.eps)}
-    if train and coef and _BN_FINAL:
+    if train and coef and bnr.fin:
         # consumers read the coefficients OP_BN_FINAL wrote (forward half after the
         # producing conv, backward half after the op that completes gsum/gxsum)
         s["coef"] = Ptr(S_STATS, bnr.coef_off * 8)
@@ -647,7 +655,7 @@ class GradState:
                     s["fin_bn"] = s["bn"]
                     s["fin_mode"] = 2
                     s["_fin_ctr"] = Ptr(S_STATS, val.bn.ctr_bwd * 8)
-                else:
+                elif val.bn.fin:
                     self.pending_final.append(val.bn)
             return s
         d = self.dbuf(val.buf)
@@ -939,7 +947,8 @@ class TailOp:
                     assert v.c0 == 0 and v.C == v.buf.C
                     assert id(v.buf) not in gs.G
                     gs.G[id(v.buf)] = gb
-                    gs.pending_final.append(v.bn)
+                    if v.bn.fin:
+                        gs.pending_final.append(v.bn)
         dterm, dns, dacc = [None] * 3, [0] * 3, [0] * 3
         for i, (v, up) in enumerate(self.terms):
             if v.bn is None and v.grad:
@@ -990,7 +999,7 @@ class Plan:
             i0 = len(fw.recs)
             op.fwd(fw)
             bnr = getattr(op, "bnr", None)
-            if train and bnr is not None and _BN_FINAL and not getattr(op, "fused_final", False):
+            if train and bnr is not None and bnr.fin and not getattr(op, "fused_final", False):
                 fw.add(bn_final_record([bnr], False))
             if getattr(op, "side", False):
                 rng = [_buf_range(op.out)]
@@ -1101,7 +1110,7 @@ class Plan:
         gs.pending_final = []
         for op in reversed(g.ops):
             op.bwd(body, gs)
-            if g.train and gs.pending_final and _BN_FINAL:
+            if g.train and gs.pending_final:
                 body.add(bn_final_record(gs.pending_final, True))
                 gs.pending_final = []
         for r in body.recs:
