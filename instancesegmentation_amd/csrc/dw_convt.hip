@@ -139,7 +139,12 @@ struct DwArgs {
 
 // forward (dgrad=false): out[c,oy,ox] = sum_t w[c,t] * x[c, oy-PH+kh*DH, ox-PW+kw*DW]
 // dgrad (dgrad=true)   : dx[c,iy,ix] = sum_t w[c,t] * dy[c, iy+PH-kh*DH, ix+PW-kw*DW]
-template <bool DGRAD>
+// KH_ x KW_: the tap grid at compile time (3x3, 5x1, 1x5 in this network), 0 = runtime.
+// The taps' raw values are loaded before the channel's coefficients are evaluated (from
+// the BatchNorm statistics when no finalisation launch wrote them), so the two round
+// trips overlap; out-of-range taps stay unloaded (a branch-free form with clamped loads
+// measured slower, round 2).
+template <bool DGRAD, int KH_, int KW_>
 __global__ __launch_bounds__(kThreads) void dw_kernel(DwArgs a) {
     __shared__ float sh[12];
     const int c = blockIdx.y, n = blockIdx.z;
@@ -148,23 +153,58 @@ __global__ __launch_bounds__(kThreads) void dw_kernel(DwArgs a) {
     const int DH_ = DGRAD ? a.H : a.OH, DW_ = DGRAD ? a.W : a.OW;
     const int64_t dhw = (int64_t)DH_ * DW_, shw = (int64_t)SH_ * SW_;
     const int64_t pix = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-    const ChanCoef k = seg_coef(a.x, c);
-    const Sink1 f = sink1_coef(a.out, c);
     float red[3] = {0.f, 0.f, 0.f};
-    if (pix < dhw) {
-        const int oy = (int)(pix / DW_), ox = (int)(pix - (int64_t)oy * DW_);
-        const float* wc = a.w + c * a.KH * a.KW;
-        float acc = 0.f;
-        for (int kh = 0; kh < a.KH; ++kh) {
-            const int iy = DGRAD ? oy + a.PH - kh * a.DH : oy - a.PH + kh * a.DH;
-            if (iy < 0 || iy >= SH_) continue;
-            for (int kw = 0; kw < a.KW; ++kw) {
+    if constexpr (KH_ > 0) {
+        constexpr int KK = KH_ * KW_;
+        const bool live = pix < dhw;
+        const int oy = live ? (int)(pix / DW_) : 0, ox = live ? (int)(pix - (int64_t)oy * DW_) : 0;
+        const float* xp = a.x.p + (int64_t)n * a.x.n_stride + (int64_t)c * shw;
+        const bool bwd = a.x.xform == ISG_XF_BN_BWD;
+        const float* yp = bwd ? a.x.y + (int64_t)n * a.x.y_n_stride + (int64_t)c * shw : xp;
+        float xr[KK], yr[KK];
+        bool ok[KK];
+#pragma unroll
+        for (int kh = 0; kh < KH_; ++kh)
+#pragma unroll
+            for (int kw = 0; kw < KW_; ++kw) {
+                const int t = kh * KW_ + kw;
+                const int iy = DGRAD ? oy + a.PH - kh * a.DH : oy - a.PH + kh * a.DH;
                 const int ix = DGRAD ? ox + a.PW - kw * a.DW : ox - a.PW + kw * a.DW;
-                if (ix < 0 || ix >= SW_) continue;
-                acc += wc[kh * a.KW + kw] * seg_load(a.x, k, n, c, shw, (int64_t)iy * SW_ + ix);
+                ok[t] = live && iy >= 0 && iy < SH_ && ix >= 0 && ix < SW_;
+                xr[t] = yr[t] = 0.f;
+                if (ok[t]) {
+                    xr[t] = xp[(int64_t)iy * SW_ + ix];
+                    if (bwd) yr[t] = yp[(int64_t)iy * SW_ + ix];
+                }
             }
+        const ChanCoef k = seg_coef(a.x, c);
+        const Sink1 f = sink1_coef(a.out, c);
+        if (live) {
+            const float* wc = a.w + c * KK;
+            float acc = 0.f;
+#pragma unroll
+            for (int t = 0; t < KK; ++t)
+                if (ok[t]) acc += wc[t] * seg_xform(a.x, k, xr[t], yr[t]);
+            sink1_apply(a.out, f, c, n, dhw, pix, acc, red);
         }
-        sink1_apply(a.out, f, c, n, dhw, pix, acc, red);
+    } else {
+        const ChanCoef k = seg_coef(a.x, c);
+        const Sink1 f = sink1_coef(a.out, c);
+        if (pix < dhw) {
+            const int oy = (int)(pix / DW_), ox = (int)(pix - (int64_t)oy * DW_);
+            const float* wc = a.w + c * a.KH * a.KW;
+            float acc = 0.f;
+            for (int kh = 0; kh < a.KH; ++kh) {
+                const int iy = DGRAD ? oy + a.PH - kh * a.DH : oy - a.PH + kh * a.DH;
+                if (iy < 0 || iy >= SH_) continue;
+                for (int kw = 0; kw < a.KW; ++kw) {
+                    const int ix = DGRAD ? ox + a.PW - kw * a.DW : ox - a.PW + kw * a.DW;
+                    if (ix < 0 || ix >= SW_) continue;
+                    acc += wc[kh * a.KW + kw] * seg_load(a.x, k, n, c, shw, (int64_t)iy * SW_ + ix);
+                }
+            }
+            sink1_apply(a.out, f, c, n, dhw, pix, acc, red);
+        }
     }
     if (sink1_needs_red(a.out)) {
         block_reduce<3>(red, sh);
@@ -174,6 +214,14 @@ __global__ __launch_bounds__(kThreads) void dw_kernel(DwArgs a) {
         fin_sink(a.out);
         fin_reset(a.fin_counter);
     }
+}
+
+template <bool DGRAD>
+void dw_launch(const isg_conv_geom* g, const DwArgs& a, dim3 grid, hipStream_t st) {
+    if (g->KH == 3 && g->KW == 3) hipLaunchKernelGGL((dw_kernel<DGRAD, 3, 3>), grid, dim3(kThreads), 0, st, a);
+    else if (g->KH == 5 && g->KW == 1) hipLaunchKernelGGL((dw_kernel<DGRAD, 5, 1>), grid, dim3(kThreads), 0, st, a);
+    else if (g->KH == 1 && g->KW == 5) hipLaunchKernelGGL((dw_kernel<DGRAD, 1, 5>), grid, dim3(kThreads), 0, st, a);
+    else hipLaunchKernelGGL((dw_kernel<DGRAD, 0, 0>), grid, dim3(kThreads), 0, st, a);
 }
 
 // weight gradient: dw[c,t] += sum_p dy[c,p] * x[c, p + tap_t]; dbias[c] += sum_p dy.
@@ -196,8 +244,9 @@ struct DwWgArgs {
 __global__ __launch_bounds__(kThreads) void dw_wgrad_kernel(DwWgArgs a) {
     __shared__ float sh[(kMaxTaps + 1) * 4];
     const int c = blockIdx.y;
-    const ChanCoef kd = seg_coef(a.dy, c);
-    const ChanCoef kx = seg_coef(a.x, c);
+    // the coefficients are evaluated after the first pass's raw loads are in flight
+    ChanCoef kd = {0.f, 1.f, 0.f, 0.f}, kx = {0.f, 1.f, 0.f, 0.f};
+    bool coefs = false;
     const int64_t ohw = (int64_t)a.OH * a.OW, xhw = (int64_t)a.H * a.W;
     const int64_t P = (int64_t)a.N * ohw;
     const int64_t pb = (int64_t)blockIdx.x * a.pix_per_block;
@@ -214,8 +263,10 @@ __global__ __launch_bounds__(kThreads) void dw_wgrad_kernel(DwWgArgs a) {
     float acc[kMaxTaps + 1];
 #pragma unroll
     for (int t = 0; t <= kMaxTaps; ++t) acc[t] = 0.f;
+    const bool dbwd = a.dy.xform == ISG_XF_BN_BWD;
     for (int64_t p0 = pb + threadIdx.x; p0 < pe; p0 += kDwPix) {
-        float d[kDwU], xv[kDwU][kMaxTaps];
+        float d[kDwU], dyr[kDwU], xr[kDwU][kMaxTaps];
+        bool xo[kDwU][kMaxTaps], dv[kDwU];
 #pragma unroll
         for (int u = 0; u < kDwU; ++u) {
             const int64_t p = p0 + (int64_t)u * kThreads;
@@ -223,14 +274,30 @@ __global__ __launch_bounds__(kThreads) void dw_wgrad_kernel(DwWgArgs a) {
             const int n = pv ? (int)(p / ohw) : 0;
             const int64_t pix = pv ? p - (int64_t)n * ohw : 0;
             const int oy = (int)(pix / a.OW), ox = (int)(pix - (int64_t)oy * a.OW);
-            d[u] = pv ? seg_load(a.dy, kd, n, c, ohw, pix) : 0.f;
+            dv[u] = pv;
+            const int64_t od = (int64_t)n * a.dy.n_stride + (int64_t)c * ohw + pix;
+            d[u] = pv ? a.dy.p[od] : 0.f;
+            dyr[u] = pv && dbwd ? a.dy.y[(int64_t)n * a.dy.y_n_stride + (int64_t)c * ohw + pix] : 0.f;
 #pragma unroll
             for (int t = 0; t < kMaxTaps; ++t) {
                 const int iy = oy + tdy[t], ix = ox + tdx[t];
-                xv[u][t] = (pv && t < KK && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
-                               ? seg_load(a.x, kx, n, c, xhw, (int64_t)iy * a.W + ix)
-                               : 0.f;
+                xo[u][t] = pv && t < KK && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+                xr[u][t] = xo[u][t] ? a.x.p[(int64_t)n * a.x.n_stride + (int64_t)c * xhw +
+                                            (int64_t)iy * a.W + ix]
+                                    : 0.f;
             }
+        }
+        if (!coefs) {  // first pass only
+            kd = seg_coef(a.dy, c);
+            kx = seg_coef(a.x, c);
+            coefs = true;
+        }
+        float xv[kDwU][kMaxTaps];
+#pragma unroll
+        for (int u = 0; u < kDwU; ++u) {
+            d[u] = dv[u] ? seg_xform(a.dy, kd, d[u], dyr[u]) : 0.f;
+#pragma unroll
+            for (int t = 0; t < kMaxTaps; ++t) xv[u][t] = xo[u][t] ? seg_xform(a.x, kx, xr[u][t], 0.f) : 0.f;
         }
 #pragma unroll
         for (int u = 0; u < kDwU; ++u) {
@@ -392,7 +459,7 @@ int32_t isg_depthwise_fwd(const isg_conv_geom* g, const isg_vtensor* x, const fl
     DwArgs a{x->s[0], out->s[0], out->fin_counter, w, g->N, g->Ci, g->H, g->W, g->OH, g->OW,
              g->KH, g->KW, g->PH, g->PW, g->DH, g->DW};
     dim3 grid((unsigned)(((int64_t)g->OH * g->OW + kThreads - 1) / kThreads), g->Ci, g->N);
-    hipLaunchKernelGGL(dw_kernel<false>, grid, dim3(kThreads), 0, st, a);
+    dw_launch<false>(g, a, grid, st);
     if (a.fin_counter) isg_fin_note_handled();
     return isg_check_launch("dw_kernel<fwd>");
 }
@@ -404,7 +471,7 @@ int32_t isg_depthwise_dgrad(const isg_conv_geom* g, const isg_vtensor* dy, const
     DwArgs a{dy->s[0], dx->s[0], dx->fin_counter, w, g->N, g->Ci, g->H, g->W, g->OH, g->OW,
              g->KH, g->KW, g->PH, g->PW, g->DH, g->DW};
     dim3 grid((unsigned)(((int64_t)g->H * g->W + kThreads - 1) / kThreads), g->Ci, g->N);
-    hipLaunchKernelGGL(dw_kernel<true>, grid, dim3(kThreads), 0, st, a);
+    dw_launch<true>(g, a, grid, st);
     if (a.fin_counter) isg_fin_note_handled();
     return isg_check_launch("dw_kernel<dgrad>");
 }
@@ -412,8 +479,8 @@ int32_t isg_depthwise_dgrad(const isg_conv_geom* g, const isg_vtensor* dy, const
 int32_t isg_depthwise_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x,
                             float* dw, float* dbias, int64_t rep_stride, int32_t nrep,
                             hipStream_t st) {
-    if (dy->nseg != 1 || x->nseg != 1 || g->KH * g->KW > kMaxTaps)
-        return isg_set_error(ISG_ERR_UNSUPPORTED, "depthwise wgrad: need 1 seg, <= 9 taps");
+    if (dy->nseg != 1 || x->nseg != 1 || g->KH * g->KW > kMaxTaps || x->s[0].xform == ISG_XF_BN_BWD)
+        return isg_set_error(ISG_ERR_UNSUPPORTED, "depthwise wgrad: need 1 seg, <= 9 taps, x not BN-backward");
     DwWgArgs a{};
     a.dy = dy->s[0]; a.x = x->s[0]; a.dw = dw; a.dbias = dbias;
     a.rep_stride = rep_stride; a.nrep = nrep;

@@ -74,12 +74,33 @@ __global__ __launch_bounds__(kThreads) void tail_fwd_kernel(isg_tail t) {
     const int64_t q = (int64_t)blockIdx.x * kThreads + threadIdx.x;
     if (q >= nq) return;
     const int qy = (int)(q / qw), qx = (int)(q - (int64_t)qy * qw);
+    const int64_t hw = (int64_t)H * W;
+    // the quad's raw term values first: their loads do not depend on the coefficients
+    // (consumer-side BatchNorm finalisation reads the statistics below), so both round
+    // trips overlap instead of running back to back
+    float2 raw[2][3];
+#pragma unroll
+    for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            raw[dy][i] = make_float2(0.f, 0.f);
+            if (i >= t.nterm) continue;
+            const isg_vseg& tm = t.term[i];
+            const int y = 2 * qy + dy;
+            if (t.up[i]) {
+                float dummy;
+                const float x0 = term_raw(tm, 1, n, c, H, W, y, 2 * qx, &dummy);
+                raw[dy][i] = make_float2(x0, x0);
+            } else {
+                const int64_t off = (int64_t)n * tm.n_stride + (int64_t)c * hw + (int64_t)y * W + 2 * qx;
+                raw[dy][i] = *reinterpret_cast<const float2*>(tm.p + off);
+            }
+        }
     ChanCoef k[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i)
         if (i < t.nterm) k[i] = seg_coef(t.term[i], c);
     const float slope = (t.act == ISG_ACT_PRELU) ? t.slope[c] : 0.f;
-    const int64_t hw = (int64_t)H * W;
     float* out = t.out + (int64_t)n * t.out_n_stride + (int64_t)c * hw;
 #pragma unroll
     for (int dy = 0; dy < 2; ++dy) {
@@ -88,19 +109,8 @@ __global__ __launch_bounds__(kThreads) void tail_fwd_kernel(isg_tail t) {
         for (int i = 0; i < 3; ++i) {
             if (i >= t.nterm) continue;
             const isg_vseg& tm = t.term[i];
-            const int y = 2 * qy + dy;
-            if (t.up[i]) {
-                float dummy;
-                const float x0 = term_raw(tm, 1, n, c, H, W, y, 2 * qx, &dummy);
-                const float tv = seg_val(tm, k[i], x0, 0.f);
-                v[0] += tv;
-                v[1] += tv;
-            } else {
-                const int64_t off = (int64_t)n * tm.n_stride + (int64_t)c * hw + (int64_t)y * W + 2 * qx;
-                const float2 xv = *reinterpret_cast<const float2*>(tm.p + off);
-                v[0] += seg_val(tm, k[i], xv.x, 0.f);
-                v[1] += seg_val(tm, k[i], xv.y, 0.f);
-            }
+            v[0] += seg_val(tm, k[i], raw[dy][i].x, 0.f);
+            v[1] += seg_val(tm, k[i], raw[dy][i].y, 0.f);
         }
         float2 o;
         o.x = apply_act(v[0], t.act, slope);
@@ -119,12 +129,38 @@ __global__ __launch_bounds__(kThreads) void tail_bwd_kernel(isg_tail_grad tg) {
     const int64_t q = (int64_t)blockIdx.x * kThreads + threadIdx.x;
     const bool valid = q < nq;
     const int qy = valid ? (int)(q / qw) : 0, qx = valid ? (int)(q - (int64_t)qy * qw) : 0;
+    const int64_t hw = (int64_t)H * W;
+    // every load of the quad first (dout and the raw terms), then the coefficients: the
+    // loads do not depend on them, so the two round trips overlap (tail_fwd_kernel)
+    float2 dld[2], rld[2][3];
+#pragma unroll
+    for (int dy = 0; dy < 2; ++dy) {
+        const int y = 2 * qy + dy;
+        const int64_t prow = (int64_t)y * W + 2 * qx;
+        // unconditional (an invalid lane reads quad (0, 0) of its plane): a load behind a
+        // per-lane branch makes the compiler drain the memory queue at the join
+        dld[dy] = *reinterpret_cast<const float2*>(tg.dout + (int64_t)n * tg.dout_n_stride +
+                                                   (int64_t)c * hw + prow);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            rld[dy][i] = make_float2(0.f, 0.f);
+            if (i >= t.nterm) continue;
+            const isg_vseg& tm = t.term[i];
+            if (t.up[i]) {
+                float dummy;
+                const float x0 = term_raw(tm, 1, n, c, H, W, y, 2 * qx, &dummy);
+                rld[dy][i] = make_float2(x0, x0);
+            } else {
+                rld[dy][i] = *reinterpret_cast<const float2*>(tm.p + (int64_t)n * tm.n_stride +
+                                                              (int64_t)c * hw + prow);
+            }
+        }
+    }
     ChanCoef k[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i)
         if (i < t.nterm) k[i] = seg_coef(t.term[i], c);
     const float slope = (t.act == ISG_ACT_PRELU) ? t.slope[c] : 0.f;
-    const int64_t hw = (int64_t)H * W;
     // red: [0..2] gsum per term (same g), [3..5] g*(y-mean) per term, [6] slope grad
     float red[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     float gq[2][2];
@@ -134,8 +170,7 @@ __global__ __launch_bounds__(kThreads) void tail_bwd_kernel(isg_tail_grad tg) {
         for (int dy = 0; dy < 2; ++dy) {
             const int y = 2 * qy + dy;
             const int64_t prow = (int64_t)y * W + 2 * qx;
-            const float2 d = *reinterpret_cast<const float2*>(
-                tg.dout + (int64_t)n * tg.dout_n_stride + (int64_t)c * hw + prow);
+            const float2 d = dld[dy];
             float pre[2] = {0.f, 0.f};
             float raw[3][2];
 #pragma unroll
@@ -143,16 +178,8 @@ __global__ __launch_bounds__(kThreads) void tail_bwd_kernel(isg_tail_grad tg) {
                 raw[i][0] = raw[i][1] = 0.f;
                 if (i >= t.nterm) continue;
                 const isg_vseg& tm = t.term[i];
-                if (t.up[i]) {
-                    float dummy;
-                    const float x0 = term_raw(tm, 1, n, c, H, W, y, 2 * qx, &dummy);
-                    raw[i][0] = raw[i][1] = x0;
-                } else {
-                    const float2 xv = *reinterpret_cast<const float2*>(
-                        tm.p + (int64_t)n * tm.n_stride + (int64_t)c * hw + prow);
-                    raw[i][0] = xv.x;
-                    raw[i][1] = xv.y;
-                }
+                raw[i][0] = rld[dy][i].x;
+                raw[i][1] = rld[dy][i].y;
                 pre[0] += seg_val(tm, k[i], raw[i][0], 0.f);
                 pre[1] += seg_val(tm, k[i], raw[i][1], 0.f);
             }

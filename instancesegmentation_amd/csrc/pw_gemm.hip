@@ -288,6 +288,9 @@ struct PwxArgs {
     int off_k, off_ri, off_a, off_x;  // dynamic LDS byte offsets (tabA at 0)
     int wmode;                        // 1: f32x4 along k (forward), 2: f32x4 along m (dgrad)
     int fast;                         // every record is plain loads (finalised BN coefficients)
+    int wu, xu;                       // weight / activation quads per lane actually needed
+    int wsh;                          // log2 of the weight quads per row, padded to a power of 2
+    int stat_on;                      // some channel or sink row evaluates its BN statistics
     int64_t P;
 };
 
@@ -298,7 +301,10 @@ struct PwxArgs {
 //      output when HY), while phase-1 results are written to LDS;
 //   3. the producer transform on the way into Xs; 4. MFMA; 5. epilogue with its sink
 //      operands (saved y / old value) loaded for all accumulator elements at once.
-template <int TPW, int BP, bool HY>
+// SEG1: one source segment and one sink — the per-lane segment selection folds away (the
+// prologue's address arithmetic was the first phase's cost: ~1,250 instructions per wave
+// before the first barrier with three-way selects, 64-bit and runtime-divisor integer math)
+template <int TPW, int BP, bool HY, bool SEG1>
 __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
     extern __shared__ f32x4 pwx_smem[];
     char* const smem = reinterpret_cast<char*>(pwx_smem);
@@ -332,26 +338,34 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
         }
     }
     // ---- phase 1 ------------------------------------------------------------------------
-    const VtSel vs = vt_sel(a.src);
-    const SkSel ks = sk_sel(a.out);
+    VtSel vs = vt_sel(a.src);
+    SkSel ks = sk_sel(a.out);
+    if constexpr (SEG1) {
+        vs.nseg = 1;
+        ks.nsink = 1;
+    }
     const int tc = min(tid, K - 1);
-    const CoefLoad<HY ? 4 : 2> cfl = coef_issue<HY ? 4 : 2>(vs, tc);
+    // every load below is issued only where it is needed: a lane-invariant (SGPR) guard per
+    // unrolled slot — the per-CU vector-memory issue of dummy duplicates was the first round
+    // trip's cost (kbench stamps: 5.2 us for ~60 load instructions per wave)
+    const bool stat_on = a.stat_on != 0;
+    const CoefLoad<HY ? 4 : 2> cfl = coef_issue<HY ? 4 : 2>(vs, tc, stat_on);
     const int trow = min(tid, Mb - 1);
-    const SinkLoad skl = sink_issue(ks, m0 + trow, w);
+    const SinkLoad skl = sink_issue(ks, m0 + trow, w, stat_on);
+    // weight slot i -> (row, quad): quads per row padded to 2^wsh, so the split is a shift
+    // and a mask; forward rows are m with k contiguous, dgrad rows are k with m contiguous.
+    // Padding slots load a clamped duplicate and are dropped at the LDS store.
+    const int wsh = a.wsh, wmask = (1 << wsh) - 1;
     f32x4 wv[WU];
-    {
-        const int kq = Kp / 4, mq = BM / 4;
-        const int nq = BM * kq;  // == mq * Kp
 #pragma unroll
-        for (int u = 0; u < WU; ++u) {
-            const int i = min(tid + u * kThreads, nq - 1);
-            // forward: (m, k4) with k contiguous; dgrad: (k, m4) with m contiguous
-            const int m1 = i / kq, k1 = (i - m1 * kq) * 4;
-            const int k2 = i / mq, m2 = (i - k2 * mq) * 4;
-            const int64_t o1 = (int64_t)(m0 + min(m1, Mb - 1)) * a.rs + min(k1, K - 4);
-            const int64_t o2 = (int64_t)min(k2, K - 1) * a.cs + m0 + min(m2, Mb - 4);
-            wv[u] = gld4(w, a.wmode == 1 ? o1 : o2);
-        }
+    for (int u = 0; u < WU; ++u) {
+        wv[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (u >= a.wu) continue;
+        const int i = tid + u * kThreads;
+        const int r = i >> wsh, qd = (i & wmask) * 4;
+        const int o = a.wmode == 1 ? (m0 + min(r, Mb - 1)) * a.rs + min(qd, K - 4)
+                                   : min(r, K - 1) * a.cs + m0 + min(qd, Mb - 4);
+        wv[u] = gld4(w, o);
     }
     tabA[tid] = ch_addr(vs, tc, a.HW);
     // ---- phase 2: activation slab loads, issued in the same round trip as phase 1 (the
@@ -360,11 +374,13 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
     const int q = tid % QPR, cr = tid / QPR;
     const int64_t pg = p0 + 4 * q;
     const bool pv = pg < a.P;
-    const int n = pv ? (int)(pg / a.HW) : 0;
-    const int pix = pv ? (int)(pg - (int64_t)n * a.HW) : 0;
+    const int n = pv ? (int)((uint32_t)pg / (uint32_t)a.HW) : 0;  // P < 2^31 (host check)
+    const int pix = pv ? (int)pg - n * a.HW : 0;
     f32x4 xv[XU], yv[XU];
 #pragma unroll
     for (int u = 0; u < XU; ++u) {
+        xv[u] = yv[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (u >= a.xu) continue;
         const ChSrc t = ch_addr(vs, min(cr + u * CPP, K - 1), a.HW);
         xv[u] = gld4(t.p, (int64_t)n * t.ns + pix);
         if (HY) yv[u] = gld4(t.y, (int64_t)n * t.yns + pix);
@@ -382,24 +398,19 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
         }
     }
     if (tid >= Mb && tid < BM) ri[tid].mode = -1;
-    {
-        const int kq = Kp / 4, mq = BM / 4;
-        const int nq = BM * kq;
 #pragma unroll
-        for (int u = 0; u < WU; ++u) {
-            const int i = tid + u * kThreads;
-            if (i < nq) {
-                if (a.wmode == 1) {
-                    const int m = i / kq, k4 = (i - m * kq) * 4;
-                    const bool ok = m < Mb && k4 < K;
-                    *reinterpret_cast<f32x4*>(&As[m * AS + k4]) = ok ? wv[u] : f32x4{0.f, 0.f, 0.f, 0.f};
-                } else {
-                    const int k = i / mq, m4 = (i - k * mq) * 4;
-#pragma unroll
-                    for (int e = 0; e < 4; ++e)
-                        As[(m4 + e) * AS + k] = (k < K && m4 + e < Mb) ? wv[u][e] : 0.f;
-                }
+    for (int u = 0; u < WU; ++u) {
+        if (u >= a.wu) continue;
+        const int i = tid + u * kThreads;
+        const int r = i >> wsh, qd = (i & wmask) * 4;
+        if (a.wmode == 1) {  // r = m, qd = k4
+            if (r < BM && qd < Kp) {
+                const bool ok = r < Mb && qd < K;
+                *reinterpret_cast<f32x4*>(&As[r * AS + qd]) = ok ? wv[u] : f32x4{0.f, 0.f, 0.f, 0.f};
             }
+        } else if (r < Kp && qd < BM) {  // r = k, qd = m4
+#pragma unroll
+            for (int e = 0; e < 4; ++e) As[(qd + e) * AS + r] = (r < K && qd + e < Mb) ? wv[u][e] : 0.f;
         }
     }
     __syncthreads();
@@ -459,8 +470,8 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
         const int rt = t / CT, ct = t % CT;
         const int64_t pe = p0 + ct * 16 + pl;
         const bool pve = pe < a.P;
-        const int ne = pve ? (int)(pe / a.HW) : 0;
-        const int pixe = pve ? (int)(pe - (int64_t)ne * a.HW) : 0;
+        const int ne = pve ? (int)((uint32_t)pe / (uint32_t)a.HW) : 0;
+        const int pixe = pve ? (int)pe - ne * a.HW : 0;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const RowInfo& qi = ri[rt * 16 + kk * 4 + r];
@@ -488,8 +499,8 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
         if (rt * 16 >= Mb) continue;
         const int64_t pe = p0 + ct * 16 + pl;
         const bool pve = pe < a.P;
-        const int ne = pve ? (int)(pe / a.HW) : 0;
-        const int pixe = pve ? (int)(pe - (int64_t)ne * a.HW) : 0;
+        const int ne = pve ? (int)((uint32_t)pe / (uint32_t)a.HW) : 0;
+        const int pixe = pve ? (int)pe - ne * a.HW : 0;
         float s0[4], s1[4], s2[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -573,9 +584,9 @@ int pwx_lds(int K, int Kp, int BM, int BP, int& off_k, int& off_ri, int& off_a, 
     return off_x + xbytes;
 }
 
-template <int TPW, int BP, bool HY>
+template <int TPW, int BP, bool HY, bool SEG1>
 int32_t pwx_launch(const PwxArgs& a, dim3 grid, int lds, hipStream_t st) {
-    auto k = pwx_kernel<TPW, BP, HY>;
+    auto k = pwx_kernel<TPW, BP, HY, SEG1>;
     static bool attr = false;
     if (!attr) {
         if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, kPxMaxLds) != hipSuccess)
@@ -586,16 +597,27 @@ int32_t pwx_launch(const PwxArgs& a, dim3 grid, int lds, hipStream_t st) {
     return isg_check_launch("pwx_kernel");
 }
 
-template <int BP, bool HY>
+template <int BP, bool HY, bool SEG1>
 int32_t pwx_dispatch(const PwxArgs& a, dim3 grid, int lds, int tpw, hipStream_t st) {
     switch (tpw) {
-        case 1: return pwx_launch<1, BP, HY>(a, grid, lds, st);
-        case 2: return pwx_launch<2, BP, HY>(a, grid, lds, st);
-        case 3: return pwx_launch<3, BP, HY>(a, grid, lds, st);
-        case 4: return pwx_launch<4, BP, HY>(a, grid, lds, st);
-        case 5: case 6: return pwx_launch<6, BP, HY>(a, grid, lds, st);
-        default: return pwx_launch<8, BP, HY>(a, grid, lds, st);
+        case 1: return pwx_launch<1, BP, HY, SEG1>(a, grid, lds, st);
+        case 2: return pwx_launch<2, BP, HY, SEG1>(a, grid, lds, st);
+        case 3: return pwx_launch<3, BP, HY, SEG1>(a, grid, lds, st);
+        case 4: return pwx_launch<4, BP, HY, SEG1>(a, grid, lds, st);
+        case 5: case 6: return pwx_launch<6, BP, HY, SEG1>(a, grid, lds, st);
+        default: return pwx_launch<8, BP, HY, SEG1>(a, grid, lds, st);
     }
+}
+template <int BP, bool HY>
+int32_t pwx_dispatch_seg(const PwxArgs& a, dim3 grid, int lds, int tpw, bool seg1, hipStream_t st) {
+    return seg1 ? pwx_dispatch<BP, HY, true>(a, grid, lds, tpw, st)
+                : pwx_dispatch<BP, HY, false>(a, grid, lds, tpw, st);
+}
+// weight quads per row padded to a power of two (pwx_kernel's slot split), and the rows
+int pwx_wrow_quads(int wmode, int BM, int Kp) {
+    int q = wmode == 1 ? Kp / 4 : BM / 4, p = 1;
+    while (p < q) p *= 2;
+    return p;
 }
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
@@ -821,14 +843,28 @@ int32_t isg_pw_gemm(const isg_conv_geom* g, const isg_vtensor* src, const float*
     static const bool slab_all = getenv("ISG_PW_SLAB_ALL") != nullptr;
     // (r02g per-op tables: the 64^2 128 -> 48 forwards 13.8 -> 12.5 us on the slab)
     static const bool fwd_small = getenv("ISG_NO_PW_FWD_SLAB_SMALL") == nullptr;
+    // (round 3, after the single-segment prologue: the 48 -> 128 expansions and their
+    // transposes, M = 128 rows over K = 48, on 32 x 64 tiles — kbench fwd 15.3 -> 14.8 us,
+    // dgrad 18.4 -> 17.2 us against the chunked kernel)
+    static const bool wide_rows = getenv("ISG_NO_PWX_WIDE_ROWS") == nullptr;
     const bool slab_pays = slab_all || (!dgrad && a.P >= 65536) || (dgrad && a.M <= 64 && a.K <= 128) ||
-                           (fwd_small && !dgrad && a.M <= 64 && a.K <= 128);
-    if (!slab_off && slab_pays && wmode && pwx_src_ok(*src, a.HW)) {
+                           (fwd_small && !dgrad && a.M <= 64 && a.K <= 128) ||
+                           (wide_rows && a.M <= 128 && a.K <= 64);
+    if (!slab_off && slab_pays && wmode && pwx_src_ok(*src, a.HW) && a.P < ((int64_t)1 << 31)) {
         PwxArgs b{};
         b.src = a.src; b.out = a.out; b.w = w; b.rs = a.rs; b.cs = a.cs;
         b.HW = a.HW; b.M = a.M; b.K = a.K; b.Kp = (a.K + 15) / 16 * 16; b.P = a.P;
         b.wmode = wmode;
         b.fast = host_vt_fast(*src) && host_sinks_fast(*out);
+        b.stat_on = 0;
+        for (int s = 0; s < src->nseg; ++s) {
+            const isg_vseg& g = src->s[s];
+            if ((g.xform == ISG_XF_BN_FWD || g.xform == ISG_XF_BN_BWD) && !g.bn.coef && g.bn.stats) b.stat_on = 1;
+        }
+        for (int s = 0; s < out->nsink; ++s) {
+            const isg_sink& k = out->s[s];
+            if (k.mode == ISG_SINK_ACTBWD && !k.bn.coef && k.bn.stats) b.stat_on = 1;
+        }
         bool hy = false;
         for (int s = 0; s < src->nseg; ++s)
             if (src->s[s].xform == ISG_XF_BN_BWD && src->s[s].y && src->s[s].y != src->s[s].p) hy = true;
@@ -842,11 +878,18 @@ int32_t isg_pw_gemm(const isg_conv_geom* g, const isg_vtensor* src, const float*
         bool done = false;
         static const int env_bm = getenv("ISG_PWX_BM") ? atoi(getenv("ISG_PWX_BM")) : 0;
         static const int env_bp = getenv("ISG_PWX_BP") ? atoi(getenv("ISG_PWX_BP")) : 0;
-        for (int bm = std::min(R, 8) * 16; bm >= 16 && !done; bm -= 16) {
+        // more than 64 rows: the widest pixel tile first (fewer weight re-reads per pixel,
+        // kbench (32, 64) beat (128, 16) on M = 128), else the most rows first
+        const bool bp_first = a.M > 64;
+        for (int it = 0; it < 8 * 3 && !done; ++it) {
+            const int bm = bp_first ? std::min(R, 8) * 16 - 16 * (it % 8) : std::min(R, 8) * 16 - 16 * (it / 3);
+            const int bp = bp_first ? (64 >> (it / 8)) : (64 >> (it % 3));
+            if (bm < 16) continue;
             if (env_bm && bm != env_bm) continue;
-            for (int bp : {64, 32, 16}) {
+            {
                 if (env_bp && bp != env_bp) continue;
-                if ((bm / 16) * (bp / 16) < 4 || bm * b.Kp > 8 * 4 * kThreads) continue;
+                const int wq = pwx_wrow_quads(wmode, bm, b.Kp) * (wmode == 1 ? bm : b.Kp);
+                if ((bm / 16) * (bp / 16) < 4 || wq > 8 * kThreads) continue;
                 if (b.Kp > 8 * (kThreads / (bp / 4))) continue;
                 int o0, o1, o2, o3, as, xs;
                 const int lds = pwx_lds(a.K, b.Kp, bm, bp, o0, o1, o2, o3, as, xs);
@@ -860,16 +903,22 @@ int32_t isg_pw_gemm(const isg_conv_geom* g, const isg_vtensor* src, const float*
         }
         if (best_bp) {
             b.BM = best_bm;
+            const int wqp = pwx_wrow_quads(wmode, best_bm, b.Kp);
+            b.wu = (wqp * (wmode == 1 ? best_bm : b.Kp) + kThreads - 1) / kThreads;
+            b.wsh = 0;
+            while ((1 << b.wsh) < wqp) ++b.wsh;
+            b.xu = (b.Kp + kThreads / (best_bp / 4) - 1) / (kThreads / (best_bp / 4));
             pwx_lds(a.K, b.Kp, best_bm, best_bp, b.off_k, b.off_ri, b.off_a, b.off_x, b.AS, b.XS);
             const int tpw = ((best_bm / 16) * (best_bp / 16) + 3) / 4;
             const dim3 grid((unsigned)((a.P + best_bp - 1) / best_bp), (unsigned)((a.M + best_bm - 1) / best_bm));
             int32_t rc;
-            if (best_bp == 64) rc = hy ? pwx_dispatch<64, true>(b, grid, best_lds, tpw, st)
-                                       : pwx_dispatch<64, false>(b, grid, best_lds, tpw, st);
-            else if (best_bp == 32) rc = hy ? pwx_dispatch<32, true>(b, grid, best_lds, tpw, st)
-                                            : pwx_dispatch<32, false>(b, grid, best_lds, tpw, st);
-            else rc = hy ? pwx_dispatch<16, true>(b, grid, best_lds, tpw, st)
-                         : pwx_dispatch<16, false>(b, grid, best_lds, tpw, st);
+            const bool seg1 = src->nseg == 1 && out->nsink == 1;
+            if (best_bp == 64) rc = hy ? pwx_dispatch_seg<64, true>(b, grid, best_lds, tpw, seg1, st)
+                                       : pwx_dispatch_seg<64, false>(b, grid, best_lds, tpw, seg1, st);
+            else if (best_bp == 32) rc = hy ? pwx_dispatch_seg<32, true>(b, grid, best_lds, tpw, seg1, st)
+                                            : pwx_dispatch_seg<32, false>(b, grid, best_lds, tpw, seg1, st);
+            else rc = hy ? pwx_dispatch_seg<16, true>(b, grid, best_lds, tpw, seg1, st)
+                         : pwx_dispatch_seg<16, false>(b, grid, best_lds, tpw, seg1, st);
             if (rc == 0 && out->fin_counter) isg_fin_note_handled();
             return rc;
         }

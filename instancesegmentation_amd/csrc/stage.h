@@ -300,8 +300,16 @@ struct StatLoad {
 };
 template <int NG>
 ISG_DEV StatLoad<NG> stat_issue(const double* stats, const float* gamma, const float* beta,
-                                int bnC, int cl, const float* any) {
+                                int bnC, int cl, const float* any, bool issue = true) {
     StatLoad<NG> r;
+    if (!issue) {  // lane-invariant: no channel of the launch needs its statistics
+        r.gamma = r.beta = 0.f;
+#pragma unroll
+        for (int g = 0; g < NG; ++g)
+#pragma unroll
+            for (int q = 0; q < ISG_STAT_REP; ++q) r.v[g][q] = 0.0;
+        return r;
+    }
     const bool on = stats != nullptr;
     const double* sp = on ? stats : reinterpret_cast<const double*>(any);
 #pragma unroll
@@ -352,7 +360,7 @@ ISG_DEV int vt_seg(const VtSel vt, int c, int& cl) {
 // NG: statistics groups to load for consumer-side finalisation — 2 when no segment is
 // BN_BWD, 4 otherwise (a BN_FWD channel then loads its 2 groups twice)
 template <int NG = 4>
-ISG_DEV CoefLoad<NG> coef_issue(const VtSel vt, int c) {
+ISG_DEV CoefLoad<NG> coef_issue(const VtSel vt, int c, bool stat_on = true) {
     int cl;
     const int s = vt_seg(vt, c, cl);
     const float* coef = ISG_SEL3(s, coef, vt);
@@ -368,7 +376,7 @@ ISG_DEV CoefLoad<NG> coef_issue(const VtSel vt, int c) {
     CoefLoad<NG> r;
     r.f = f32x4{gld(cp, 0), gld(cp, 1), gld(cp, 2), gld(cp, 3)};
     r.sl = gld(sp, 0);
-    r.st = stat_issue<NG>(st, ISG_SEL3(s, gamma, vt), ISG_SEL3(s, beta, vt), bnC, cl, p);
+    r.st = stat_issue<NG>(st, ISG_SEL3(s, gamma, vt), ISG_SEL3(s, beta, vt), bnC, cl, p, stat_on);
     return r;
 }
 
@@ -466,7 +474,7 @@ ISG_DEV int sk_seg(const SkSel sk, int m, int& cl) {
 }
 
 // `any` is a valid global address (stands in for NULL pointers)
-ISG_DEV SinkLoad sink_issue(const SkSel sk, int m, const float* any) {
+ISG_DEV SinkLoad sink_issue(const SkSel sk, int m, const float* any, bool stat_on = true) {
     int cl;
     const int s = sk_seg(sk, m, cl);
     const float* coef = ISG_SEL3(s, coef, sk);
@@ -482,7 +490,7 @@ ISG_DEV SinkLoad sink_issue(const SkSel sk, int m, const float* any) {
     r.bias = gld(bp, 0);
     r.sl = gld(sp, 0);
     r.st = stat_issue<2>(st, ISG_SEL3(s, gamma, sk), ISG_SEL3(s, beta, sk), ISG_SEL3(s, bnC, sk), cl,
-                         any);
+                         any, stat_on);
     return r;
 }
 

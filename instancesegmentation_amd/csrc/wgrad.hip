@@ -331,6 +331,7 @@ struct PwgArgs {
     int nrep;
     int HW, R, C, BR, BC, ncb;
     int fast;   // finalised BatchNorm coefficients everywhere (stage.h vt_fast)
+    int stat_on;  // some channel evaluates its BatchNorm statistics (consumer-side)
     int off_k, off_x;  // byte offsets: coefficient table, slab (addressing table at 0)
     int64_t P, ntiles, tiles_per_block;
 };
@@ -376,8 +377,8 @@ __global__ __launch_bounds__(kThreads) void pwg_kernel(PwgArgs a) {
     {
         const VtSel vd = vt_sel(a.dy), vx = vt_sel(a.x);
         const ChSrc ad = ch_addr(vd, cdy, a.HW), ax = ch_addr(vx, cx, a.HW);
-        const CoefLoad<4> ld = coef_issue<4>(vd, cdy);
-        const CoefLoad<2> lx = coef_issue<2>(vx, cx);
+        const CoefLoad<4> ld = coef_issue<4>(vd, cdy, a.stat_on != 0);
+        const CoefLoad<2> lx = coef_issue<2>(vx, cx, a.stat_on != 0);
         ChSrc& e = tabA[tid];  // field by field: a select of whole records goes through scratch
         e.p = is_dy ? ad.p : ax.p; e.y = is_dy ? ad.y : ax.y;
         e.ns = is_dy ? ad.ns : ax.ns; e.yns = is_dy ? ad.yns : ax.yns;
@@ -545,6 +546,12 @@ int32_t pwg_try(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor
     a.HW = HW; a.R = g->Co; a.C = g->Ci;
     a.P = (int64_t)g->N * HW;
     a.fast = pwg_fast(*dy) && pwg_fast(*x);
+    a.stat_on = 0;
+    for (const isg_vtensor* v : {dy, x})
+        for (int s = 0; s < v->nseg; ++s) {
+            const isg_vseg& q = v->s[s];
+            if ((q.xform == ISG_XF_BN_FWD || q.xform == ISG_XF_BN_BWD) && !q.bn.coef && q.bn.stats) a.stat_on = 1;
+        }
     const bool hy = pwg_has_y(*dy) || pwg_has_y(*x);
     a.ntiles = (a.P + kGTP - 1) / kGTP;
     int br = std::min(64, (a.R + 15) / 16 * 16);

@@ -174,9 +174,11 @@ def test_s2k5_fwd(cfg, monkeypatch):
              "act": L.ACT["prelu"], "slope": ptr(G[4]), "bn": bn_spec_eval(*G[:4])}]
     Y = torch.full((N, Co, OH, OW), float("nan"), device=DEV)
     stats = rep_zeros(4 * Co)
+    B, Wt = cuda32(b), cuda32(w)  # held: the kernel reads them after this frame's temporaries die
     sk = sinks([{"p": ptr(Y), "n_stride": Co * OH * OW, "c0": 0, "C": Co,
-                 "mode": L.SINK_STORE, "bias": ptr(cuda32(b)), "stats": ptr(stats)}])
-    call("isg_conv_fwd", geom(**ge), vt(segs, N, H, W), ptr(cuda32(w)), sk, stream())
+                 "mode": L.SINK_STORE, "bias": ptr(B), "stats": ptr(stats)}])
+    call("isg_conv_fwd", geom(**ge), vt(segs, N, H, W), ptr(Wt), sk, stream())
+    torch.cuda.synchronize()
     close(Y, ref, tol=4e-6, what="s2k5 fwd")
     stats = rep_fold(stats, 4 * Co)
     close(stats[:Co], ref.sum((0, 2, 3)), tol=4e-6, what="sum")
