@@ -244,9 +244,8 @@ struct DwWgArgs {
 __global__ __launch_bounds__(kThreads) void dw_wgrad_kernel(DwWgArgs a) {
     __shared__ float sh[(kMaxTaps + 1) * 4];
     const int c = blockIdx.y;
-    // the coefficients are evaluated after the first pass's raw loads are in flight
-    ChanCoef kd = {0.f, 1.f, 0.f, 0.f}, kx = {0.f, 1.f, 0.f, 0.f};
-    bool coefs = false;
+    const ChanCoef kd = seg_coef(a.dy, c);
+    const ChanCoef kx = seg_coef(a.x, c);
     const int64_t ohw = (int64_t)a.OH * a.OW, xhw = (int64_t)a.H * a.W;
     const int64_t P = (int64_t)a.N * ohw;
     const int64_t pb = (int64_t)blockIdx.x * a.pix_per_block;
@@ -263,10 +262,8 @@ __global__ __launch_bounds__(kThreads) void dw_wgrad_kernel(DwWgArgs a) {
     float acc[kMaxTaps + 1];
 #pragma unroll
     for (int t = 0; t <= kMaxTaps; ++t) acc[t] = 0.f;
-    const bool dbwd = a.dy.xform == ISG_XF_BN_BWD;
     for (int64_t p0 = pb + threadIdx.x; p0 < pe; p0 += kDwPix) {
-        float d[kDwU], dyr[kDwU], xr[kDwU][kMaxTaps];
-        bool xo[kDwU][kMaxTaps], dv[kDwU];
+        float d[kDwU], xv[kDwU][kMaxTaps];
 #pragma unroll
         for (int u = 0; u < kDwU; ++u) {
             const int64_t p = p0 + (int64_t)u * kThreads;
@@ -274,30 +271,14 @@ __global__ __launch_bounds__(kThreads) void dw_wgrad_kernel(DwWgArgs a) {
             const int n = pv ? (int)(p / ohw) : 0;
             const int64_t pix = pv ? p - (int64_t)n * ohw : 0;
             const int oy = (int)(pix / a.OW), ox = (int)(pix - (int64_t)oy * a.OW);
-            dv[u] = pv;
-            const int64_t od = (int64_t)n * a.dy.n_stride + (int64_t)c * ohw + pix;
-            d[u] = pv ? a.dy.p[od] : 0.f;
-            dyr[u] = pv && dbwd ? a.dy.y[(int64_t)n * a.dy.y_n_stride + (int64_t)c * ohw + pix] : 0.f;
+            d[u] = pv ? seg_load(a.dy, kd, n, c, ohw, pix) : 0.f;
 #pragma unroll
             for (int t = 0; t < kMaxTaps; ++t) {
                 const int iy = oy + tdy[t], ix = ox + tdx[t];
-                xo[u][t] = pv && t < KK && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
-                xr[u][t] = xo[u][t] ? a.x.p[(int64_t)n * a.x.n_stride + (int64_t)c * xhw +
-                                            (int64_t)iy * a.W + ix]
-                                    : 0.f;
+                xv[u][t] = (pv && t < KK && iy >= 0 && iy < a.H && ix >= 0 && ix < a.W)
+                               ? seg_load(a.x, kx, n, c, xhw, (int64_t)iy * a.W + ix)
+                               : 0.f;
             }
-        }
-        if (!coefs) {  // first pass only
-            kd = seg_coef(a.dy, c);
-            kx = seg_coef(a.x, c);
-            coefs = true;
-        }
-        float xv[kDwU][kMaxTaps];
-#pragma unroll
-        for (int u = 0; u < kDwU; ++u) {
-            d[u] = dv[u] ? seg_xform(a.dy, kd, d[u], dyr[u]) : 0.f;
-#pragma unroll
-            for (int t = 0; t < kMaxTaps; ++t) xv[u][t] = xo[u][t] ? seg_xform(a.x, kx, xr[u][t], 0.f) : 0.f;
         }
 #pragma unroll
         for (int u = 0; u < kDwU; ++u) {
@@ -323,6 +304,8 @@ struct CtArgs {
     int Co;          // all output channels; blockIdx.y selects CO of them
 };
 
+constexpr int kCtMaxCi = 128;
+
 // CO output channels per thread, channel group blockIdx.y: the small up-sampling convs
 // (bottle4_1up / bottle5_1up, 64^2 and 128^2 inputs) have only 32-128 blocks of input
 // cells, so the output channels are spread over the grid's y dimension instead.
@@ -331,6 +314,11 @@ __global__ __launch_bounds__(kThreads) void convT_kernel(CtArgs a) {
     constexpr int K = 2 * S, P = S / 2;
     const int co0 = blockIdx.y * CO;
     __shared__ float sh[CO][2][4];
+    // the input channels' coefficients once per workgroup (each thread evaluating every
+    // channel's fp64 BatchNorm finalisation itself cost +6 us per launch, round 3)
+    __shared__ ChanCoef cf[kCtMaxCi];
+    for (int c = threadIdx.x; c < a.Ci; c += kThreads) cf[c] = seg_coef(a.x, c);
+    __syncthreads();
     const int64_t hw = (int64_t)a.H * a.W;
     const int64_t cell = (int64_t)blockIdx.x * kThreads + threadIdx.x;
     const int64_t ncell = (int64_t)a.N * hw;
@@ -370,7 +358,7 @@ __global__ __launch_bounds__(kThreads) void convT_kernel(CtArgs a) {
                 rx[dy][dx] = gld(xp, o);
                 ry[dy][dx] = xbwd ? gld(yp, o) : 0.f;
             }
-        const ChanCoef kc = seg_coef(a.x, ci);
+        const ChanCoef kc = cf[ci];
         float nb[3][3];
 #pragma unroll
         for (int dy = 0; dy < 3; ++dy)
@@ -499,8 +487,8 @@ int32_t isg_depthwise_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const
 
 int32_t isg_convT_fwd(const isg_conv_geom* g, const isg_vtensor* x, const float* w,
                       const isg_sinks* out, isg_stream_t st) {
-    if (x->nseg != 1 || out->nsink != 1 || out->s[0].mode != ISG_SINK_STORE)
-        return isg_set_error(ISG_ERR_UNSUPPORTED, "convT fwd: need 1 seg / 1 STORE sink");
+    if (x->nseg != 1 || out->nsink != 1 || out->s[0].mode != ISG_SINK_STORE || g->Ci > kCtMaxCi)
+        return isg_set_error(ISG_ERR_UNSUPPORTED, "convT fwd: need 1 seg / 1 STORE sink, Ci <= %d", kCtMaxCi);
     const int S = g->SH;
     if (g->SW != S || g->KH != 2 * S || g->KW != 2 * S || g->PH != S / 2 || g->PW != S / 2 ||
         g->OH != g->H * S || g->OW != g->W * S)

@@ -706,23 +706,28 @@ ISG_DEV void sink_row_apply4(const SinkRow& q, int n, int64_t pix, f32x4 v, floa
     }
 }
 
+// kThinWaves waves per workgroup (round 3; one-wave workgroups before): the BN partials
+// meet in LDS, so a launch adds (quads / 64 / kThinWaves) atomics per statistics address —
+// at 4 replicas the one-wave form queued 512 atomics on each address (+10 us per op)
+constexpr int kThinWaves = 4;
 template <int K, int M>
-__global__ __launch_bounds__(64) void thin_pw_kernel(ThinPwArgs a) {
+__global__ __launch_bounds__(64 * kThinWaves) void thin_pw_kernel(ThinPwArgs a) {
     constexpr int M4 = M / 4;
     __shared__ f32x4 wl[K * M4];  // [k][m/4]
     __shared__ ChT tab[K];
     __shared__ SinkRow ri[M];
-    const int lane = threadIdx.x;
+    __shared__ float part[kThinWaves][M][3];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int m0 = blockIdx.y * M;  // this workgroup's M output rows
-    if (lane < K) tab[lane] = ch_table_entry(a.src, lane, a.HW);
-    if (lane < M) ri[lane] = sink_row(a.out, m0 + lane, a.HW);
+    if (tid < K) tab[tid] = ch_table_entry(a.src, tid, a.HW);
+    if (tid >= 64 && tid < 64 + M) ri[tid - 64] = sink_row(a.out, m0 + tid - 64, a.HW);
     float* const wf = reinterpret_cast<float*>(wl);
-    for (int i = lane; i < K * M; i += 64) {
+    for (int i = tid; i < K * M; i += 64 * kThinWaves) {
         const int k = i / M, m = i - k * M;
         wf[i] = gld(a.w, (int64_t)(m0 + m) * a.rs + (int64_t)k * a.cs);
     }
     __syncthreads();
-    const int64_t qd = (int64_t)blockIdx.x * 64 + lane;
+    const int64_t qd = (int64_t)blockIdx.x * 64 * kThinWaves + tid;
     const bool pv = qd < a.Q;
     const int64_t p = (pv ? qd : 0) * 4;
     const int n = (int)(p / a.HW);
@@ -760,7 +765,25 @@ __global__ __launch_bounds__(64) void thin_pw_kernel(ThinPwArgs a) {
             s0 = wave_sum(s0);
             s1 = wave_sum(s1);
             s2 = wave_sum(s2);
-            if (lane == m) sink_row_flush(a.out, m0 + m, s0, s1, s2);
+            if (lane == m) {
+                part[wave][m][0] = s0;
+                part[wave][m][1] = s1;
+                part[wave][m][2] = s2;
+            }
+        }
+    }
+    if (red) {
+        __syncthreads();
+        if (tid < M) {
+            float r3[3];
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                float v = 0.f;
+#pragma unroll
+                for (int w = 0; w < kThinWaves; ++w) v += part[w][tid][j];
+                r3[j] = v;
+            }
+            sink_row_flush(a.out, m0 + tid, r3[0], r3[1], r3[2]);
         }
     }
 }
@@ -788,10 +811,10 @@ int32_t thin_pw(const PwArgs& a, hipStream_t st) {
     // stay on the MFMA kernels)
     static const bool tile_on = getenv("ISG_THIN_PW_TILE") != nullptr;
     const int mt = tile_on && a.M > 16 && a.M % 16 == 0 && a.M <= 64 ? 16 : a.M;
-    const dim3 grid((unsigned)((b.Q + 63) / 64), (unsigned)(a.M / mt));
+    const dim3 grid((unsigned)((b.Q + 64 * kThinWaves - 1) / (64 * kThinWaves)), (unsigned)(a.M / mt));
 #define ISG_THIN_PW(KK, MM)                                                          \
     if (a.K == KK && mt == MM) {                                                     \
-        hipLaunchKernelGGL((thin_pw_kernel<KK, MM>), grid, dim3(64), 0, st, b);     \
+        hipLaunchKernelGGL((thin_pw_kernel<KK, MM>), grid, dim3(64 * kThinWaves), 0, st, b); \
         const int32_t e = isg_check_launch("thin_pw_kernel");                        \
         return e ? e : 1;                                                            \
     }
