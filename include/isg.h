@@ -421,6 +421,13 @@ int32_t isg_exec(const void* ops, int32_t nops, void* const* table, isg_stream_t
 int32_t isg_exec_ms(const void* ops, int32_t nops, void* const* table, isg_stream_t stream,
                     isg_stream_t side);
 
+/* Same with a second side stream: a forked batch made only of weight gradients (independent
+ * atomic accumulations) is dealt alternately over `side` and `side2`, so two of their small
+ * grids run at once; every other side op stays in order on `side`. side2 == NULL is
+ * isg_exec_ms. */
+int32_t isg_exec_ms2(const void* ops, int32_t nops, void* const* table, isg_stream_t stream,
+                     isg_stream_t side, isg_stream_t side2);
+
 /* sizeof() of the ABI structs and executor records (0 vtensor, 1 sinks, 2 conv record,
  * 3 wgrad record, 4 pool record, 5 tail, 6 tail_grad, 7 bn_update, 8 grad_final,
  * 9 bce record, 10 conv_geom, 11 bn, 12 vseg, 13 sink, 14 sum_rep record, 15 kp_stem,

@@ -188,6 +188,7 @@ SIGNATURES = {
     "isg_mask_head_bwd": (c_int32, [POINTER(MaskHead), c_void_p]),
     "isg_exec": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p]),
     "isg_exec_ms": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p]),
+    "isg_exec_ms2": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p]),
     "isg_last_error": (c_char_p, []),
     "isg_abi_version": (c_int32, []),
     "isg_stat_replicas": (c_int32, []),
@@ -248,3 +249,19 @@ def side_stream_ptr(device=None):
     if d not in _SIDE:
         _SIDE[d] = torch.cuda.Stream(device=d)
     return _SIDE[d].cuda_stream
+
+
+_SIDE2 = {}
+
+
+def side_stream2_ptr(device=None):
+    """The executor's second side stream (batches of weight gradients are dealt over both),
+    or None when disabled (ISG_NO_SIDE2=1 or ISG_NO_SIDE_STREAM=1)."""
+    if os.environ.get("ISG_NO_SIDE2", "0") == "1" or side_stream_ptr(device) is None:
+        return None
+    d = torch.cuda.current_device() if device is None else torch.device(device).index
+    if d is None:
+        d = torch.cuda.current_device()
+    if d not in _SIDE2:
+        _SIDE2[d] = torch.cuda.Stream(device=d)
+    return _SIDE2[d].cuda_stream

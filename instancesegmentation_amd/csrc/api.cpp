@@ -207,20 +207,22 @@ struct OpHdr {
 };
 enum { ISG_OPF_SIDE = 1, ISG_OPF_JOIN = 2, ISG_OPF_FORK_NOW = 4 };  // FORK_NOW: no batching
 
-// fork / join events of the executor's side stream, one pair per device (created on
-// first use, never destroyed; timing disabled)
-static int32_t side_events(hipEvent_t* fork, hipEvent_t* join) {
-    static hipEvent_t ev[64][2];
+// fork / join events of the executor's side streams, per device (created on first use,
+// never destroyed; timing disabled): ev[0] fork, ev[1] join of side stream 0, ev[2] join
+// of side stream 1
+static int32_t side_events(hipEvent_t* fork, hipEvent_t* join, hipEvent_t* join2) {
+    static hipEvent_t ev[64][3];
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64)
         return isg_set_error(ISG_ERR_HIP, "exec: no device for the side stream");
     if (!ev[dev][0]) {
-        if (hipEventCreateWithFlags(&ev[dev][0], hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&ev[dev][1], hipEventDisableTiming) != hipSuccess)
-            return isg_check_launch("exec: side-stream events");
+        for (int i = 0; i < 3; ++i)
+            if (hipEventCreateWithFlags(&ev[dev][i], hipEventDisableTiming) != hipSuccess)
+                return isg_check_launch("exec: side-stream events");
     }
     *fork = ev[dev][0];
     *join = ev[dev][1];
+    *join2 = ev[dev][2];
     return ISG_OK;
 }
 struct Fix {
@@ -344,12 +346,12 @@ static int32_t run_op_raw(int32_t kind, char* buf, isg_stream_t st) {
     return rc;
 }
 
-int32_t isg_exec_ms(const void* ops, int32_t nops, void* const* table, isg_stream_t main_st,
-                    isg_stream_t side) {
+int32_t isg_exec_ms2(const void* ops, int32_t nops, void* const* table, isg_stream_t main_st,
+                     isg_stream_t side, isg_stream_t side2) {
     const char* p = (const char*)ops;
     alignas(16) char buf[8192];
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    bool forked = false;  // side-stream work outstanding since the last join
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_join2 = nullptr;
+    bool forked = false, forked2 = false;  // side-stream work outstanding since the last join
     static const int batch = [] {
         const char* e = getenv("ISG_SIDE_BATCH");
         const int b = e ? atoi(e) : 24;
@@ -358,23 +360,38 @@ int32_t isg_exec_ms(const void* ops, int32_t nops, void* const* table, isg_strea
     std::vector<std::pair<int32_t, std::string>> pending;
     auto flush = [&]() -> int32_t {
         if (pending.empty()) return ISG_OK;
-        if (hipEventRecord(ev_fork, main_st) != hipSuccess || hipStreamWaitEvent(side, ev_fork, 0) != hipSuccess)
+        // a batch of weight gradients only (independent accumulations into the replica
+        // buffers) is dealt over both side streams: their grids (128-512 workgroups) leave
+        // most of the chip idle one at a time; anything else keeps its order on stream 0
+        bool spread = side2 != nullptr;
+        for (auto& op : pending)
+            spread = spread && (op.first == OP_CONV_WGRAD || op.first == OP_KP_STEM_WGRAD);
+        if (hipEventRecord(ev_fork, main_st) != hipSuccess || hipStreamWaitEvent(side, ev_fork, 0) != hipSuccess ||
+            (spread && hipStreamWaitEvent(side2, ev_fork, 0) != hipSuccess))
             return isg_check_launch("exec: fork side stream");
         forked = true;
+        forked2 = forked2 || spread;
         alignas(16) char pb[8192];
+        int k = 0;
         for (auto& op : pending) {
             std::memcpy(pb, op.second.data(), op.second.size());
-            if (int32_t e = run_op(op.first, pb, side)) return e;
+            if (int32_t e = run_op(op.first, pb, spread && (k++ & 1) ? side2 : side)) return e;
         }
         pending.clear();
         return ISG_OK;
     };
     auto join = [&]() -> int32_t {
         if (int32_t e = flush()) return e;
-        if (!forked) return ISG_OK;
-        forked = false;
-        if (hipEventRecord(ev_join, side) != hipSuccess || hipStreamWaitEvent(main_st, ev_join, 0) != hipSuccess)
-            return isg_check_launch("exec: join side stream");
+        if (forked) {
+            forked = false;
+            if (hipEventRecord(ev_join, side) != hipSuccess || hipStreamWaitEvent(main_st, ev_join, 0) != hipSuccess)
+                return isg_check_launch("exec: join side stream");
+        }
+        if (forked2) {
+            forked2 = false;
+            if (hipEventRecord(ev_join2, side2) != hipSuccess || hipStreamWaitEvent(main_st, ev_join2, 0) != hipSuccess)
+                return isg_check_launch("exec: join side stream 2");
+        }
         return ISG_OK;
     };
     for (int i = 0; i < nops; ++i) {
@@ -387,7 +404,7 @@ int32_t isg_exec_ms(const void* ops, int32_t nops, void* const* table, isg_strea
         if ((h.flags & ISG_OPF_SIDE) && side) {
             // the op depends on everything issued so far on the main stream
             if (!ev_fork) {
-                if (int32_t e = side_events(&ev_fork, &ev_join)) return e;
+                if (int32_t e = side_events(&ev_fork, &ev_join, &ev_join2)) return e;
             }
             st = side;
         }
@@ -421,8 +438,13 @@ int32_t isg_exec_ms(const void* ops, int32_t nops, void* const* table, isg_strea
     return join();
 }
 
+int32_t isg_exec_ms(const void* ops, int32_t nops, void* const* table, isg_stream_t main_st,
+                    isg_stream_t side) {
+    return isg_exec_ms2(ops, nops, table, main_st, side, nullptr);
+}
+
 int32_t isg_exec(const void* ops, int32_t nops, void* const* table, isg_stream_t st) {
-    return isg_exec_ms(ops, nops, table, st, nullptr);
+    return isg_exec_ms2(ops, nops, table, st, nullptr, nullptr);
 }
 
 // sizes of the executor records, so the Python planner can verify its ctypes mirrors

@@ -126,13 +126,13 @@ class OpList:
         self._buf = ctypes.create_string_buffer(self.blob, len(self.blob))
         return self
 
-    def run(self, table, stream, side=None):
+    def run(self, table, stream, side=None, side2=None):
         if side is None:
             L.check(L.lib().isg_exec(ctypes.addressof(self._buf), len(self.recs), table, stream),
                     "exec")
         else:
-            L.check(L.lib().isg_exec_ms(ctypes.addressof(self._buf), len(self.recs), table,
-                                        stream, side), "exec")
+            L.check(L.lib().isg_exec_ms2(ctypes.addressof(self._buf), len(self.recs), table,
+                                         stream, side, side2), "exec")
 
     def slice(self, i, j):
         """A compiled sub-list recs[i:j] (to bracket one op with events)."""
@@ -969,7 +969,13 @@ class TailOp:
 class Plan:
     """Compiled forward (+ optional backward) op lists of one module at one shape."""
 
-    def __init__(self, owner, in_shapes, train, need_grad, in_grad):
+    def __init__(self, owner, in_shapes, train, need_grad, in_grad, buckets=2):
+        """buckets: gradient buckets of the backward (2: the stem's parameters finalised in a
+        second part after the others, for a data-parallel exchange that overlaps the stem
+        backward; 1: one part, every finalisation at the end — at world size 1 nothing
+        needs bucket 1 early, and the part boundary's side-stream join made the stem's
+        input-gradient chain wait ~0.6 ms for the queued weight gradients)."""
+        self.n_buckets = buckets
         N = in_shapes[0][0]
         g = Graph(owner, N, train, need_grad)
         ins = [g.input(i, s[1], s[2], s[3], in_grad[i]) if len(s) == 4 else
@@ -1042,7 +1048,7 @@ class Plan:
         touches (by any pointer) bucket 1's gradient replicas or the statistics its
         finalisation reads. Returns (0, len(recs)) when no such split exists."""
         late = self._late_prefix(g)
-        if late is None or not g.train:
+        if late is None or not g.train or self.n_buckets < 2:
             return 0, len(recs)
         cut = 0
         for k in g.param_names:

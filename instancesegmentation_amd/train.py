@@ -19,6 +19,8 @@ statistics per replica, rank 0's running statistics on every replica after each 
 """
 import ctypes
 
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -124,8 +126,10 @@ class Trainer:
         self.comm = torch.zeros(n + max(nb, 1), dtype=torch.float32, device=dev)
         self.flat, self.flatb, self.index = flatten_module(self.model, dev, self.comm[n:])
         self.in_shapes = [tuple(s) for s in in_shapes]
+        # two gradient buckets only where an exchange overlaps the stem backward (Plan)
         self.plan = Plan(self.model, self.in_shapes, True, True,
-                         tuple(False for _ in self.in_shapes))
+                         tuple(False for _ in self.in_shapes),
+                         buckets=int(os.environ.get("ISG_BUCKETS", "0")) or (2 if self.world > 1 else 1))
         g = self.plan.graph
         assert g.pgrad_size == n
         self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
@@ -226,7 +230,8 @@ class Trainer:
         'coll1'/'coll2' (eager RCCL bucket exchange), 'tic'/'toc' (timing events around
         one op). split=(phase, idx) isolates op `idx` of the forward/backward list."""
         def run_list(ol):
-            return lambda: ol.run(self.table, L.stream_ptr(self.device), L.side_stream_ptr(self.device))
+            return lambda: ol.run(self.table, L.stream_ptr(self.device), L.side_stream_ptr(self.device),
+                                  L.side_stream2_ptr(self.device))
         dp = self.world > 1
         lists = [("fwd", self.plan.fwd)] + [("bwd", p) for p in self.plan.bwd_parts]
         units = []

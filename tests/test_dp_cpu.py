@@ -129,15 +129,20 @@ def test_single_process_exchange_is_identity():
 def test_bucket_split_covers_parameters():
     """Bucket 2 is the stem's parameters (a leading range of the flat gradient); the
     backward parts finalise exactly [cut, n) and [0, cut)."""
+    from instancesegmentation_amd.engine import Plan
     m = Segment(20)
-    tr = Trainer(m, 2, [(2, 3, 64, 64), (2, 17, 64, 64)], device="cpu")
+    shapes = [(2, 3, 64, 64), (2, 17, 64, 64)]
+    plan = Plan(m, shapes, True, True, (False, False), buckets=2)
     names = [k for k, _ in m.named_parameters()]
-    cut = tr.plan.bucket_cut
+    cut = plan.bucket_cut
     stem = sum(p.numel() for k, p in m.named_parameters() if k.startswith("init_conv."))
     assert cut == stem and names[0].startswith("init_conv.")
-    assert tr.buckets[0].numel() + tr.buckets[1].numel() == tr.comm.numel()
-    p1, p2 = tr.plan.bwd_parts
+    p1, p2 = plan.bwd_parts
     assert [r.label for r in p2.recs if r.label.startswith("dw_")] == \
         ["dw_init_conv.layer2", "dw_init_conv.layer1"]
     assert not any(r.label.startswith(("dw_init", "dx_init")) for r in p1.recs)
-    assert len(p1.recs) + len(p2.recs) == len(tr.plan.bwd.recs)
+    assert len(p1.recs) + len(p2.recs) == len(plan.bwd.recs)
+    # world size 1: one backward part, one bucket (the whole flat gradient)
+    tr = Trainer(m, 2, shapes, device="cpu")
+    assert tr.world == 1 and len(tr.plan.bwd_parts) == 1 and tr.plan.bucket_cut == 0
+    assert tr.buckets[0].numel() + tr.buckets[1].numel() == tr.comm.numel()
