@@ -291,6 +291,7 @@ struct PwxArgs {
     int wu, xu;                       // weight / activation quads per lane actually needed
     int wsh;                          // log2 of the weight quads per row, padded to a power of 2
     int stat_on;                      // some channel or sink row evaluates its BN statistics
+    int pre_on;                       // some sink reads an operand (ACTBWD y / ACCUM old value)
     int64_t P;
 };
 
@@ -344,6 +345,23 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
         vs.nseg = 1;
         ks.nsink = 1;
     }
+    // ---- phase 2 first: the activation slab loads (HBM, the longest latency) lead the
+    //      round trip; their channel addresses come from the kernel arguments alone, only
+    //      the transform needs the coefficient table, after the barrier
+    const int q = tid % QPR, cr = tid / QPR;
+    const int64_t pg = p0 + 4 * q;
+    const bool pv = pg < a.P;
+    const int n = pv ? (int)((uint32_t)pg / (uint32_t)a.HW) : 0;  // P < 2^31 (host check)
+    const int pix = pv ? (int)pg - n * a.HW : 0;
+    f32x4 xv[XU], yv[XU];
+#pragma unroll
+    for (int u = 0; u < XU; ++u) {
+        xv[u] = yv[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (u >= a.xu) continue;
+        const ChSrc t = ch_addr(vs, min(cr + u * CPP, K - 1), a.HW);
+        xv[u] = gld4(t.p, (int64_t)n * t.ns + pix);
+        if (HY) yv[u] = gld4(t.y, (int64_t)n * t.yns + pix);
+    }
     const int tc = min(tid, K - 1);
     // every load below is issued only where it is needed: a lane-invariant (SGPR) guard per
     // unrolled slot — the per-CU vector-memory issue of dummy duplicates was the first round
@@ -368,22 +386,35 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
         wv[u] = gld4(w, o);
     }
     tabA[tid] = ch_addr(vs, tc, a.HW);
-    // ---- phase 2: activation slab loads, issued in the same round trip as phase 1 (the
-    //      channel addresses come from the kernel arguments alone; only the transform
-    //      needs the coefficient table, after the barrier)
-    const int q = tid % QPR, cr = tid / QPR;
-    const int64_t pg = p0 + 4 * q;
-    const bool pv = pg < a.P;
-    const int n = pv ? (int)((uint32_t)pg / (uint32_t)a.HW) : 0;  // P < 2^31 (host check)
-    const int pix = pv ? (int)pg - n * a.HW : 0;
-    f32x4 xv[XU], yv[XU];
+    // the epilogue's sink operands (saved forward output for ACTBWD, old value for ACCUM):
+    // with one sink their addresses come from the kernel arguments, so they are issued in
+    // this same round trip instead of after the MFMA loop
+    constexpr int CT_ = BP / 16;
+    const int nt_ = (BM / 16) * CT_;
+    float pre[TPW][4];
 #pragma unroll
-    for (int u = 0; u < XU; ++u) {
-        xv[u] = yv[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (u >= a.xu) continue;
-        const ChSrc t = ch_addr(vs, min(cr + u * CPP, K - 1), a.HW);
-        xv[u] = gld4(t.p, (int64_t)n * t.ns + pix);
-        if (HY) yv[u] = gld4(t.y, (int64_t)n * t.yns + pix);
+    for (int i = 0; i < TPW; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pre[i][r] = 0.f;
+    if (SEG1 && a.pre_on) {
+        const SinkLite& k0 = ks.s0;
+        const bool ab = k0.mode == ISG_SINK_ACTBWD;
+        const float* base = ab ? k0.y : k0.p;
+        const int bns = ab ? k0.yns : k0.ns;
+#pragma unroll
+        for (int i = 0; i < TPW; ++i) {
+            const int t = min(wave + 4 * i, nt_ - 1);
+            const int rt = t / CT_, ct = t % CT_;
+            const int64_t pe = p0 + ct * 16 + pl;
+            const bool pve = pe < a.P;
+            const int ne = pve ? (int)((uint32_t)pe / (uint32_t)a.HW) : 0;
+            const int pixe = pve ? (int)pe - ne * a.HW : 0;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int cl = min(rt * 16 + kk * 4 + r, Mb - 1) + m0 - k0.c0;
+                pre[i][r] = gld(base, (int64_t)cl * a.HW + (int64_t)ne * bns + pixe);
+            }
+        }
     }
     __syncthreads();
     STAMP(1);
@@ -463,24 +494,25 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
     // ---- phase 5: epilogue; lane holds D[row = rt*16 + kk*4 + r][pixel = ct*16 + pl] ----
     // sink operands first (saved forward output for ACTBWD, old value for ACCUM), all in
     // flight together; other rows load a dummy word
-    float pre[TPW][4];
+    if (!SEG1 && a.pre_on) {
 #pragma unroll
-    for (int i = 0; i < TPW; ++i) {
-        const int t = min(wave + 4 * i, nt - 1);
-        const int rt = t / CT, ct = t % CT;
-        const int64_t pe = p0 + ct * 16 + pl;
-        const bool pve = pe < a.P;
-        const int ne = pve ? (int)((uint32_t)pe / (uint32_t)a.HW) : 0;
-        const int pixe = pve ? (int)pe - ne * a.HW : 0;
+        for (int i = 0; i < TPW; ++i) {
+            const int t = min(wave + 4 * i, nt - 1);
+            const int rt = t / CT, ct = t % CT;
+            const int64_t pe = p0 + ct * 16 + pl;
+            const bool pve = pe < a.P;
+            const int ne = pve ? (int)((uint32_t)pe / (uint32_t)a.HW) : 0;
+            const int pixe = pve ? (int)pe - ne * a.HW : 0;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const RowInfo& qi = ri[rt * 16 + kk * 4 + r];
-            const float* src = w;
-            int64_t off = 0;
-            if (qi.mode == ISG_SINK_ACTBWD) { src = qi.y; off = (int64_t)ne * qi.yns + pixe; }
-            if (qi.mode == ISG_SINK_ACCUM) { src = qi.p; off = (int64_t)ne * qi.ns + pixe; }
-            if (!pve) { src = w; off = 0; }
-            pre[i][r] = gld(src, off);
+            for (int r = 0; r < 4; ++r) {
+                const RowInfo& qi = ri[rt * 16 + kk * 4 + r];
+                const float* src = w;
+                int64_t off = 0;
+                if (qi.mode == ISG_SINK_ACTBWD) { src = qi.y; off = (int64_t)ne * qi.yns + pixe; }
+                if (qi.mode == ISG_SINK_ACCUM) { src = qi.p; off = (int64_t)ne * qi.ns + pixe; }
+                if (!pve) { src = w; off = 0; }
+                pre[i][r] = gld(src, off);
+            }
         }
     }
     const bool need_red = sinks_need_red(a.out);
@@ -879,6 +911,9 @@ int32_t isg_pw_gemm(const isg_conv_geom* g, const isg_vtensor* src, const float*
         b.HW = a.HW; b.M = a.M; b.K = a.K; b.Kp = (a.K + 15) / 16 * 16; b.P = a.P;
         b.wmode = wmode;
         b.fast = host_vt_fast(*src) && host_sinks_fast(*out);
+        b.pre_on = 0;
+        for (int s = 0; s < out->nsink; ++s)
+            if (out->s[s].mode == ISG_SINK_ACTBWD || out->s[s].mode == ISG_SINK_ACCUM) b.pre_on = 1;
         b.stat_on = 0;
         for (int s = 0; s < src->nseg; ++s) {
             const isg_vseg& g = src->s[s];
