@@ -216,6 +216,148 @@ __global__ __launch_bounds__(kThreads) void dw_kernel(DwArgs a) {
     }
 }
 
+// ---- LDS-tiled depthwise (round 3) -----------------------------------------------------
+// One workgroup = one (image, channel) tile of 16 x 64 outputs; a thread owns 4 adjacent
+// outputs of one row. The input region (tile + the taps' halo) is staged ONCE into LDS
+// with the producer's BatchNorm / activation (or BatchNorm backward) applied once per
+// element — the per-pixel kernel above transformed every input 9 times and issued 9
+// (18 for BatchNorm backward) 4-B loads per output. Outputs leave as 16-B stores through
+// the sink. Same-size convolutions only (stride 1, OH == H, OW == W, W % 4 == 0).
+constexpr int kDtY = 16, kDtX = 64;
+constexpr int kDtMaxR = kDtY + 2 * 4 * 2, kDtMaxC = kDtX + 2 * 4 * 2;  // halo <= 8 per side
+
+template <bool DGRAD, int KH_, int KW_>
+__global__ __launch_bounds__(kThreads) void dw_tile_kernel(DwArgs a) {
+    __shared__ float Ts[kDtMaxR * kDtMaxC];
+    __shared__ float sh[12];
+    const int c = blockIdx.z % a.C, n = blockIdx.z / a.C;
+    const int H = a.H, W = a.W;  // source == destination size
+    const int oy0 = blockIdx.y * kDtY, ox0 = blockIdx.x * kDtX;
+    // tap offsets relative to the output pixel: fwd +(k*D - P), dgrad +(P - k*D); the region
+    // starts at the smallest
+    const int ay0 = DGRAD ? a.PH - (KH_ - 1) * a.DH : -a.PH;
+    const int ax0 = DGRAD ? a.PW - (KW_ - 1) * a.DW : -a.PW;
+    const int RH = kDtY + (KH_ - 1) * a.DH, RW = kDtX + (KW_ - 1) * a.DW;
+    const int64_t hw = (int64_t)H * W;
+    const isg_vseg& sg = a.x;
+    const float* xp = sg.p + (int64_t)n * sg.n_stride + (int64_t)c * hw;
+    const bool bwd = sg.xform == ISG_XF_BN_BWD;
+    const float* yp = bwd ? sg.y + (int64_t)n * sg.y_n_stride + (int64_t)c * hw : xp;
+    // ---- stage: every element's raw load in flight, then the coefficients, then LDS
+    constexpr int kU = (kDtMaxR * kDtMaxC + kThreads - 1) / kThreads;
+    float xr[kU], yr[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+        xr[u] = yr[u] = 0.f;
+        if (u * kThreads >= RH * RW) continue;  // workgroup-uniform
+        const int e = threadIdx.x + u * kThreads;
+        const int rr = e / RW, cc = e - rr * RW;
+        const int iy = oy0 + ay0 + rr, ix = ox0 + ax0 + cc;
+        const bool ok = rr < RH && iy >= 0 && iy < H && ix >= 0 && ix < W;
+        const int64_t o = ok ? (int64_t)iy * W + ix : 0;
+        xr[u] = xp[o];
+        yr[u] = bwd ? yp[o] : 0.f;
+    }
+    const ChanCoef k = seg_coef(sg, c);
+    const Sink1 f = sink1_coef(a.out, c);
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+        if (u * kThreads >= RH * RW) continue;
+        const int e = threadIdx.x + u * kThreads;
+        const int rr = e / RW, cc = e - rr * RW;
+        const int iy = oy0 + ay0 + rr, ix = ox0 + ax0 + cc;
+        const bool ok = rr < RH && iy >= 0 && iy < H && ix >= 0 && ix < W;
+        if (rr < RH) Ts[rr * kDtMaxC + cc] = ok ? seg_xform(sg, k, xr[u], yr[u]) : 0.f;  // zero padding after the transform
+    }
+    __syncthreads();
+    // ---- compute: thread -> row ty, 4 outputs from column 4 * tq
+    const int ty = threadIdx.x >> 4, tq = threadIdx.x & 15;
+    const float* wc = a.w + c * KH_ * KW_;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kh = 0; kh < KH_; ++kh) {
+        const int rrow = ty + (DGRAD ? (KH_ - 1 - kh) : kh) * a.DH;
+#pragma unroll
+        for (int kw = 0; kw < KW_; ++kw) {
+            const float wv = wc[kh * KW_ + kw];
+            const float* rp = Ts + rrow * kDtMaxC + 4 * tq + (DGRAD ? (KW_ - 1 - kw) : kw) * a.DW;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[j] += wv * rp[j];
+        }
+    }
+    // ---- sink: 16-B accesses, 4 outputs
+    float red[3] = {0.f, 0.f, 0.f};
+    const int oy = oy0 + ty, ox = ox0 + 4 * tq;
+    if (oy < H && ox < W) {
+        const isg_sink& o = a.out;
+        const int64_t off = (int64_t)n * o.n_stride + (int64_t)c * hw + (int64_t)oy * W + ox;
+        typedef f32x4 __attribute__((address_space(1)))* g4p;
+        if (o.mode == ISG_SINK_STORE || o.mode == ISG_SINK_ACCUM) {
+            f32x4 v = {acc[0], acc[1], acc[2], acc[3]};
+            if (o.mode == ISG_SINK_STORE && o.bias) v += o.bias[c];
+            if (o.mode == ISG_SINK_ACCUM) v += *(g4p)((gfloat_p)o.p + off);
+            else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    red[0] += v[j];
+                    red[1] += v[j] * v[j];
+                }
+            }
+            if (o.mode == ISG_SINK_ACCUM) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    red[0] += acc[j];
+                    red[1] += acc[j] * acc[j];
+                }
+            }
+            *(g4p)((gfloat_p)o.p + off) = v;
+        } else if (o.mode == ISG_SINK_ACTBWD) {
+            const f32x4 y4 = *(const f32x4 __attribute__((address_space(1)))*)((gcfloat_p)o.y +
+                              (int64_t)n * o.y_n_stride + (int64_t)c * hw + (int64_t)oy * W + ox);
+            f32x4 g4;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float z = (y4[j] - f.mean) * f.scale + f.beta;
+                float gv = acc[j];
+                if (o.act == ISG_ACT_RELU) {
+                    gv = z > 0.f ? acc[j] : 0.f;
+                } else if (o.act == ISG_ACT_PRELU) {
+                    gv = z > 0.f ? acc[j] : acc[j] * f.slope;
+                    red[2] += z > 0.f ? 0.f : z * acc[j];
+                }
+                g4[j] = gv;
+                red[0] += gv;
+                red[1] += gv * (y4[j] - f.mean);
+            }
+            *(g4p)((gfloat_p)o.p + off) = g4;
+        }
+    }
+    if (sink1_needs_red(a.out)) {
+        block_reduce<3>(red, sh);
+        if (threadIdx.x == 0) sink1_flush(a.out, c, red);
+    }
+}
+
+// 1: launched, 0: shape not for the tiled kernel
+template <bool DGRAD>
+int dw_tile_try(const isg_conv_geom* g, const DwArgs& a, hipStream_t st) {
+    static const bool off = getenv("ISG_NO_DW_TILE") != nullptr;
+    if (off || a.fin_counter || g->SH != 1 || g->SW != 1 || g->OH != g->H || g->OW != g->W || g->W % 4)
+        return 0;
+    const isg_sink& o = a.out;
+    if (o.mode == ISG_SINK_NONE || ((uintptr_t)o.p & 15) || o.n_stride % 4 ||
+        (o.mode == ISG_SINK_ACTBWD && (((uintptr_t)o.y & 15) || o.y_n_stride % 4)))
+        return 0;
+    if ((g->KH - 1) * g->DH > 16 || (g->KW - 1) * g->DW > 16) return 0;
+    const dim3 grid((unsigned)((g->W + kDtX - 1) / kDtX), (unsigned)((g->H + kDtY - 1) / kDtY),
+                    (unsigned)(g->Ci * g->N));
+    if (g->KH == 3 && g->KW == 3) hipLaunchKernelGGL((dw_tile_kernel<DGRAD, 3, 3>), grid, dim3(kThreads), 0, st, a);
+    else if (g->KH == 5 && g->KW == 1) hipLaunchKernelGGL((dw_tile_kernel<DGRAD, 5, 1>), grid, dim3(kThreads), 0, st, a);
+    else if (g->KH == 1 && g->KW == 5) hipLaunchKernelGGL((dw_tile_kernel<DGRAD, 1, 5>), grid, dim3(kThreads), 0, st, a);
+    else return 0;
+    return 1;
+}
+
 template <bool DGRAD>
 void dw_launch(const isg_conv_geom* g, const DwArgs& a, dim3 grid, hipStream_t st) {
     if (g->KH == 3 && g->KW == 3) hipLaunchKernelGGL((dw_kernel<DGRAD, 3, 3>), grid, dim3(kThreads), 0, st, a);
@@ -446,6 +588,7 @@ int32_t isg_depthwise_fwd(const isg_conv_geom* g, const isg_vtensor* x, const fl
         return isg_set_error(ISG_ERR_UNSUPPORTED, "depthwise fwd: need 1 seg/sink, stride 1");
     DwArgs a{x->s[0], out->s[0], out->fin_counter, w, g->N, g->Ci, g->H, g->W, g->OH, g->OW,
              g->KH, g->KW, g->PH, g->PW, g->DH, g->DW};
+    if (dw_tile_try<false>(g, a, st)) return isg_check_launch("dw_tile_kernel<fwd>");
     dim3 grid((unsigned)(((int64_t)g->OH * g->OW + kThreads - 1) / kThreads), g->Ci, g->N);
     dw_launch<false>(g, a, grid, st);
     if (a.fin_counter) isg_fin_note_handled();
@@ -458,6 +601,7 @@ int32_t isg_depthwise_dgrad(const isg_conv_geom* g, const isg_vtensor* dy, const
         return isg_set_error(ISG_ERR_UNSUPPORTED, "depthwise dgrad: need 1 seg/sink, stride 1");
     DwArgs a{dy->s[0], dx->s[0], dx->fin_counter, w, g->N, g->Ci, g->H, g->W, g->OH, g->OW,
              g->KH, g->KW, g->PH, g->PW, g->DH, g->DW};
+    if (dw_tile_try<true>(g, a, st)) return isg_check_launch("dw_tile_kernel<dgrad>");
     dim3 grid((unsigned)(((int64_t)g->H * g->W + kThreads - 1) / kThreads), g->Ci, g->N);
     dw_launch<true>(g, a, grid, st);
     if (a.fin_counter) isg_fin_note_handled();

@@ -156,6 +156,26 @@ __global__ __launch_bounds__(kThreads) void tail_bwd_kernel(isg_tail_grad tg) {
             }
         }
     }
+    // the old values of accumulated term gradients, in the same round trip
+    float2 old[2][3];
+    float oldup[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        oldup[i] = 0.f;
+#pragma unroll
+        for (int dy = 0; dy < 2; ++dy) old[dy][i] = make_float2(0.f, 0.f);
+        if (i >= t.nterm || t.term[i].xform != ISG_XF_PLAIN || !tg.dterm[i] || !tg.dterm_accum[i]) continue;
+        if (t.up[i]) {
+            const int64_t lhw = (int64_t)(H >> 1) * (W >> 1);
+            oldup[i] = tg.dterm[i][(int64_t)n * tg.dterm_n_stride[i] + (int64_t)c * lhw + (valid ? q : 0)];
+        } else {
+#pragma unroll
+            for (int dy = 0; dy < 2; ++dy)
+                old[dy][i] = *reinterpret_cast<const float2*>(
+                    tg.dterm[i] + (int64_t)n * tg.dterm_n_stride[i] + (int64_t)c * hw +
+                    (int64_t)(2 * qy + dy) * W + 2 * qx);
+        }
+    }
     ChanCoef k[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i)
@@ -213,9 +233,8 @@ __global__ __launch_bounds__(kThreads) void tail_bwd_kernel(isg_tail_grad tg) {
                 float* dst = tg.dterm[i] + (int64_t)n * tg.dterm_n_stride[i] + (int64_t)c * hw + prow;
                 float2 o = make_float2(gq[dy][0], gq[dy][1]);
                 if (tg.dterm_accum[i]) {
-                    const float2 old = *reinterpret_cast<const float2*>(dst);
-                    o.x += old.x;
-                    o.y += old.y;
+                    o.x += old[dy][i].x;
+                    o.y += old[dy][i].y;
                 }
                 *reinterpret_cast<float2*>(dst) = o;
             }
@@ -226,7 +245,7 @@ __global__ __launch_bounds__(kThreads) void tail_bwd_kernel(isg_tail_grad tg) {
             if (i >= t.nterm || t.term[i].xform != ISG_XF_PLAIN || !tg.dterm[i] || !t.up[i]) continue;
             const int64_t lhw = (int64_t)(H >> 1) * (W >> 1);
             float* dst = tg.dterm[i] + (int64_t)n * tg.dterm_n_stride[i] + (int64_t)c * lhw + q;
-            *dst = tg.dterm_accum[i] ? *dst + upsum : upsum;
+            *dst = tg.dterm_accum[i] ? oldup[i] + upsum : upsum;
         }
     }
     bool need = (t.act == ISG_ACT_PRELU && tg.slope_grad);

@@ -305,6 +305,10 @@ DW_CFG = [  # (C, H, W, kh, kw, ph, pw, d)
     (48, 16, 16, 3, 3, 4, 4, 4),
     (48, 16, 16, 5, 1, 2, 0, 1),
     (48, 16, 16, 1, 5, 0, 2, 1),
+    # the LDS-tiled kernel (16 x 64 tiles): partial tiles in both directions, dilation 4
+    (16, 40, 84, 3, 3, 1, 1, 1),
+    (24, 50, 84, 3, 3, 4, 4, 4),
+    (8, 37, 132, 5, 1, 2, 0, 1),
 ]
 
 
