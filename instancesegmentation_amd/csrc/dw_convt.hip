@@ -437,6 +437,82 @@ __global__ __launch_bounds__(kThreads) void dw_wgrad_kernel(DwWgArgs a) {
     }
 }
 
+// LDS-tiled depthwise weight gradient (round 3): one workgroup per (image, channel) 16 x 64
+// tile of dy; the x region under the taps (tile + halo) staged ONCE into LDS with its
+// BatchNorm / activation applied once per element, dy read as 16-B quads (BatchNorm backward
+// rebuilt in registers); each lane accumulates its 4 pixels' products per tap, reduced over
+// the workgroup and added into this workgroup's weight-gradient replica. Same-size layers,
+// W % 4 == 0 (dw_wgrad_kernel otherwise).
+template <int KH_, int KW_>
+__global__ __launch_bounds__(kThreads) void dw_wgrad_tile_kernel(DwWgArgs a) {
+    constexpr int KK = KH_ * KW_;
+    __shared__ float Ts[kDtMaxR * kDtMaxC];
+    __shared__ float sh[(KK + 1) * 4];
+    const int c = blockIdx.z % a.C, n = blockIdx.z / a.C;
+    const int H = a.H, W = a.W;
+    const int oy0 = blockIdx.y * kDtY, ox0 = blockIdx.x * kDtX;
+    const int RH = kDtY + (KH_ - 1) * a.DH, RW = kDtX + (KW_ - 1) * a.DW;
+    const int64_t hw = (int64_t)H * W;
+    const isg_vseg& sx = a.x;
+    const isg_vseg& sd = a.dy;
+    const float* xp = sx.p + (int64_t)n * sx.n_stride + (int64_t)c * hw;
+    // this lane's 4 dy pixels (row ty, columns 4 tq ..)
+    const int ty = threadIdx.x >> 4, tq = threadIdx.x & 15;
+    const int oy = oy0 + ty, ox = ox0 + 4 * tq;
+    const bool dv = oy < H && ox < W;
+    const int64_t dpix = dv ? (int64_t)oy * W + ox : 0;
+    typedef const f32x4 __attribute__((address_space(1)))* gc4p;
+    const f32x4 d4 = *(gc4p)((gcfloat_p)sd.p + (int64_t)n * sd.n_stride + (int64_t)c * hw + dpix);
+    const bool dbwd = sd.xform == ISG_XF_BN_BWD;
+    const f32x4 y4 = dbwd ? *(gc4p)((gcfloat_p)sd.y + (int64_t)n * sd.y_n_stride + (int64_t)c * hw + dpix)
+                          : f32x4{0.f, 0.f, 0.f, 0.f};
+    constexpr int kU = (kDtMaxR * kDtMaxC + kThreads - 1) / kThreads;
+    float xr[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+        xr[u] = 0.f;
+        if (u * kThreads >= RH * RW) continue;  // workgroup-uniform
+        const int e = threadIdx.x + u * kThreads;
+        const int rr = e / RW, cc = e - rr * RW;
+        const int iy = oy0 - a.PH + rr, ix = ox0 - a.PW + cc;
+        const bool ok = rr < RH && iy >= 0 && iy < H && ix >= 0 && ix < W;
+        xr[u] = xp[ok ? (int64_t)iy * W + ix : 0];
+    }
+    const ChanCoef kx = seg_coef(sx, c);
+    const ChanCoef kd = seg_coef(sd, c);
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+        if (u * kThreads >= RH * RW) continue;
+        const int e = threadIdx.x + u * kThreads;
+        const int rr = e / RW, cc = e - rr * RW;
+        const int iy = oy0 - a.PH + rr, ix = ox0 - a.PW + cc;
+        const bool ok = rr < RH && iy >= 0 && iy < H && ix >= 0 && ix < W;
+        if (rr < RH) Ts[rr * kDtMaxC + cc] = ok ? seg_xform(sx, kx, xr[u], 0.f) : 0.f;
+    }
+    float dyv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dyv[j] = dv ? seg_xform(sd, kd, d4[j], y4[j]) : 0.f;
+    __syncthreads();
+    float acc[KK + 1];
+    acc[KK] = (dyv[0] + dyv[1]) + (dyv[2] + dyv[3]);
+#pragma unroll
+    for (int kh = 0; kh < KH_; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < KW_; ++kw) {
+            const float* rp = Ts + (ty + kh * a.DH) * kDtMaxC + 4 * tq + kw * a.DW;
+            float v = 0.f;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v = fmaf(dyv[j], rp[j], v);
+            acc[kh * KW_ + kw] = v;
+        }
+    block_reduce<KK + 1>(acc, sh);
+    if (threadIdx.x == 0) {
+        const int64_t ro = (int64_t)((blockIdx.x + 3u * blockIdx.y + 7u * blockIdx.z) % (unsigned)a.nrep) * a.rep_stride;
+        for (int t = 0; t < KK; ++t) atomicAdd(&a.dw[ro + c * KK + t], acc[t]);
+        if (a.dbias) atomicAdd(&a.dbias[ro + c], acc[KK]);
+    }
+}
+
 // ---- transposed convolution, kernel 2S, stride S, pad S/2 --------------------------
 struct CtArgs {
     isg_vseg x;      // [N][Ci][H][W]
@@ -618,6 +694,28 @@ int32_t isg_depthwise_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const
     a.rep_stride = rep_stride; a.nrep = nrep;
     a.N = g->N; a.C = g->Ci; a.H = g->H; a.W = g->W; a.OH = g->OH; a.OW = g->OW;
     a.KH = g->KH; a.KW = g->KW; a.PH = g->PH; a.PW = g->PW; a.DH = g->DH; a.DW = g->DW;
+    {
+        static const bool off = getenv("ISG_NO_DW_TILE") != nullptr;
+        const isg_vseg& d = a.dy;
+        const bool ok = !off && g->SH == 1 && g->SW == 1 && g->OH == g->H && g->OW == g->W && g->W % 4 == 0 &&
+                        !((uintptr_t)d.p & 15) && d.n_stride % 4 == 0 &&
+                        (d.xform != ISG_XF_BN_BWD || (!((uintptr_t)d.y & 15) && d.y_n_stride % 4 == 0)) &&
+                        (g->KH - 1) * g->DH <= 16 && (g->KW - 1) * g->DW <= 16;
+        const dim3 grid((unsigned)((g->W + kDtX - 1) / kDtX), (unsigned)((g->H + kDtY - 1) / kDtY),
+                        (unsigned)(g->Ci * g->N));
+        if (ok && g->KH == 3 && g->KW == 3) {
+            hipLaunchKernelGGL((dw_wgrad_tile_kernel<3, 3>), grid, dim3(kThreads), 0, st, a);
+            return isg_check_launch("dw_wgrad_tile_kernel");
+        }
+        if (ok && g->KH == 5 && g->KW == 1) {
+            hipLaunchKernelGGL((dw_wgrad_tile_kernel<5, 1>), grid, dim3(kThreads), 0, st, a);
+            return isg_check_launch("dw_wgrad_tile_kernel");
+        }
+        if (ok && g->KH == 1 && g->KW == 5) {
+            hipLaunchKernelGGL((dw_wgrad_tile_kernel<1, 5>), grid, dim3(kThreads), 0, st, a);
+            return isg_check_launch("dw_wgrad_tile_kernel");
+        }
+    }
     const int64_t P = (int64_t)g->N * g->OH * g->OW;
     // one pass of kDwPix pixels per block while that still leaves >= ~1024 blocks
     int64_t splits = (P + kDwPix - 1) / kDwPix;
