@@ -485,12 +485,11 @@ class Graph:
 # 4 replicas (2 replicas 4.92: atomic contention in the producers; 8 replicas 4.82: more
 # consumer reads; 16 replicas +0.8 ms, round 2). ISG_BN_FINAL=1 restores the launches.
 _BN_FINAL = os.environ.get("ISG_BN_FINAL", "0") == "1"
-# ... except where the consumers are many small workgroups: every one of them re-reads the
-# same statistics lines (an L2 hot spot) and evaluates them in fp64, which cost more than
-# the launch on the 256^2 decoder's 4 <-> 16-channel layers (thin_pw, one-wave workgroups:
-# +9-12 us per op). BN points normalising >= this many values (N*H*W) keep one
-# OP_BN_FINAL launch.
-_BN_FINAL_COUNT = int(os.environ.get("ISG_BN_FINAL_COUNT", "131072"))
+# ISG_BN_FINAL_COUNT=n keeps one OP_BN_FINAL launch at BN points normalising >= n values
+# (N*H*W). Default: none. (131072 — the stem and the 256^2 decoder — paid while thin_pw ran
+# one-wave workgroups whose statistics atomics and reads piled on the same lines; after its
+# four-wave form all-consumer-side measured 4.39 vs 4.41 ms/step, profiles/r03u_ab.txt.)
+_BN_FINAL_COUNT = int(os.environ.get("ISG_BN_FINAL_COUNT", str(1 << 62)))
 # finalise BN coefficients in the producing kernel's last workgroup (isg_sink.fin_*)
 # instead of a separate OP_BN_FINAL launch (needs ISG_BN_FINAL=1). Opt-in: measured
 # slower (5.43 vs 5.17 ms/step fence-free, round 3; 7.16 vs 6.5 with a release fence).
