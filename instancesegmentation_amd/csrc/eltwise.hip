@@ -267,6 +267,197 @@ __global__ __launch_bounds__(kThreads) void tail_bwd_kernel(isg_tail_grad tg) {
     }
 }
 
+// ---- residual tail, 2 x 4 pixel units (W % 4 == 0, 16-B aligned planes) --------------
+// The same tails as above with a thread owning two rows of 4 pixels: every full-resolution
+// operand moves as 16-B accesses (an x2-upsampled term as one 8-B pair of low-resolution
+// values per row pair), half the threads, workgroups and reductions of the quad form.
+typedef f32x4 __attribute__((address_space(1)))* t4p;
+typedef const f32x4 __attribute__((address_space(1)))* tc4p;
+typedef float tf32x2 __attribute__((ext_vector_type(2)));
+typedef const tf32x2 __attribute__((address_space(1)))* tc2p;
+typedef tf32x2 __attribute__((address_space(1)))* t2p;
+
+ISG_DEV f32x4 tail_term4(const isg_vseg& tm, int up, int n, int c, int H, int W, int y, int x4) {
+    if (up) {
+        const int w2 = W >> 1;
+        const int64_t off = (int64_t)n * tm.n_stride + (int64_t)c * (H >> 1) * w2 + (int64_t)(y >> 1) * w2 + (x4 >> 1);
+        const tf32x2 v = *(tc2p)((gcfloat_p)tm.p + off);
+        return f32x4{v.x, v.x, v.y, v.y};
+    }
+    const int64_t off = (int64_t)n * tm.n_stride + (int64_t)c * H * W + (int64_t)y * W + x4;
+    return *(tc4p)((gcfloat_p)tm.p + off);
+}
+
+__global__ __launch_bounds__(kThreads) void tail_fwd4_kernel(isg_tail t) {
+    const int c = blockIdx.y, n = blockIdx.z;
+    const int H = t.H, W = t.W;
+    const int qw = W >> 2;
+    const int nq = (H >> 1) * qw;
+    const int q = blockIdx.x * kThreads + threadIdx.x;
+    if (q >= nq) return;
+    const int qy = q / qw, x4 = (q - qy * qw) * 4;
+    f32x4 raw[2][3];
+#pragma unroll
+    for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            raw[dy][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (i < t.nterm) raw[dy][i] = tail_term4(t.term[i], t.up[i], n, c, H, W, 2 * qy + dy, x4);
+        }
+    ChanCoef k[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+        if (i < t.nterm) k[i] = seg_coef(t.term[i], c);
+    const float slope = (t.act == ISG_ACT_PRELU) ? t.slope[c] : 0.f;
+    float* out = t.out + (int64_t)n * t.out_n_stride + (int64_t)c * H * W;
+#pragma unroll
+    for (int dy = 0; dy < 2; ++dy) {
+        f32x4 o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            if (i >= t.nterm) continue;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] += seg_val(t.term[i], k[i], raw[dy][i][e], 0.f);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = apply_act(o[e], t.act, slope);
+        *(t4p)((gfloat_p)out + (int64_t)(2 * qy + dy) * W + x4) = o;
+    }
+}
+
+__global__ __launch_bounds__(kThreads) void tail_bwd4_kernel(isg_tail_grad tg) {
+    __shared__ float sh[8 * 4];
+    const isg_tail& t = tg.f;
+    const int c = blockIdx.y, n = blockIdx.z;
+    const int H = t.H, W = t.W;
+    const int qw = W >> 2;
+    const int nq = (H >> 1) * qw;
+    const int q0 = blockIdx.x * kThreads + threadIdx.x;
+    const bool valid = q0 < nq;
+    const int q = valid ? q0 : 0;  // invalid lanes load unit 0 (no per-lane branch on loads)
+    const int qy = q / qw, x4 = (q - qy * qw) * 4;
+    const int64_t hw = (int64_t)H * W;
+    const int w2 = W >> 1;
+    const int64_t lhw = (int64_t)(H >> 1) * w2;
+    f32x4 dld[2], rld[2][3], old[2][3];
+    tf32x2 oldup[3];
+#pragma unroll
+    for (int dy = 0; dy < 2; ++dy) {
+        const int64_t prow = (int64_t)(2 * qy + dy) * W + x4;
+        dld[dy] = *(tc4p)((gcfloat_p)tg.dout + (int64_t)n * tg.dout_n_stride + (int64_t)c * hw + prow);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            rld[dy][i] = old[dy][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (i >= t.nterm) continue;
+            rld[dy][i] = tail_term4(t.term[i], t.up[i], n, c, H, W, 2 * qy + dy, x4);
+            if (t.term[i].xform == ISG_XF_PLAIN && tg.dterm[i] && tg.dterm_accum[i] && !t.up[i])
+                old[dy][i] = *(tc4p)((gcfloat_p)tg.dterm[i] + (int64_t)n * tg.dterm_n_stride[i] +
+                                     (int64_t)c * hw + prow);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        oldup[i] = tf32x2{0.f, 0.f};
+        if (i < t.nterm && t.term[i].xform == ISG_XF_PLAIN && tg.dterm[i] && tg.dterm_accum[i] && t.up[i])
+            oldup[i] = *(tc2p)((gcfloat_p)tg.dterm[i] + (int64_t)n * tg.dterm_n_stride[i] + (int64_t)c * lhw +
+                               (int64_t)qy * w2 + (x4 >> 1));
+    }
+    ChanCoef k[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+        if (i < t.nterm) k[i] = seg_coef(t.term[i], c);
+    const float slope = (t.act == ISG_ACT_PRELU) ? t.slope[c] : 0.f;
+    float red[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    f32x4 gq[2];
+    if (valid) {
+#pragma unroll
+        for (int dy = 0; dy < 2; ++dy) {
+            const int64_t prow = (int64_t)(2 * qy + dy) * W + x4;
+            f32x4 pre = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                if (i >= t.nterm) continue;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) pre[e] += seg_val(t.term[i], k[i], rld[dy][i][e], 0.f);
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float dv = dld[dy][e];
+                float g = dv;
+                if (t.act == ISG_ACT_RELU) {
+                    g = pre[e] > 0.f ? dv : 0.f;
+                } else if (t.act == ISG_ACT_PRELU) {
+                    g = pre[e] > 0.f ? dv : dv * slope;
+                    red[6] += pre[e] > 0.f ? 0.f : pre[e] * dv;
+                }
+                gq[dy][e] = g;
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    if (i >= t.nterm || t.term[i].xform != ISG_XF_BN_FWD) continue;
+                    red[i] += g;
+                    red[3 + i] += g * (rld[dy][i][e] - k[i].c0);  // centred (c0 = mean)
+                }
+            }
+            if (tg.g) *(t4p)((gfloat_p)tg.g + (int64_t)n * tg.g_n_stride + (int64_t)c * hw + prow) = gq[dy];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                if (i >= t.nterm || t.term[i].xform != ISG_XF_PLAIN || !tg.dterm[i] || t.up[i]) continue;
+                f32x4 o = gq[dy];
+                if (tg.dterm_accum[i]) o += old[dy][i];
+                *(t4p)((gfloat_p)tg.dterm[i] + (int64_t)n * tg.dterm_n_stride[i] + (int64_t)c * hw + prow) = o;
+            }
+        }
+        // x2-upsampled terms: each low-resolution pixel's gradient is its 2x2 block's sum
+        const tf32x2 us = {(gq[0][0] + gq[0][1]) + (gq[1][0] + gq[1][1]),
+                           (gq[0][2] + gq[0][3]) + (gq[1][2] + gq[1][3])};
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            if (i >= t.nterm || t.term[i].xform != ISG_XF_PLAIN || !tg.dterm[i] || !t.up[i]) continue;
+            tf32x2 o = us;
+            if (tg.dterm_accum[i]) o += oldup[i];
+            *(t2p)((gfloat_p)tg.dterm[i] + (int64_t)n * tg.dterm_n_stride[i] + (int64_t)c * lhw +
+                   (int64_t)qy * w2 + (x4 >> 1)) = o;
+        }
+    }
+    bool need = (t.act == ISG_ACT_PRELU && tg.slope_grad);
+    for (int i = 0; i < t.nterm; ++i) need |= (t.term[i].xform == ISG_XF_BN_FWD);
+    if (!need) return;
+    float rv[8] = {red[0], red[1], red[2], red[3], red[4], red[5], red[6], 0.f};
+    block_reduce<8>(rv, sh);
+    if (threadIdx.x == 0) {
+        for (int i = 0; i < t.nterm; ++i) {
+            const isg_vseg& tm = t.term[i];
+            if (tm.xform == ISG_XF_BN_FWD && tm.bn.stats) {
+                double* sp = rep_ptr(tm.bn.stats, 4 * tm.bn.C);
+                atomicAdd(&sp[2 * tm.bn.C + c], (double)rv[i]);
+                atomicAdd(&sp[3 * tm.bn.C + c], (double)rv[3 + i]);
+            }
+        }
+        if (t.act == ISG_ACT_PRELU && tg.slope_grad)
+            atomicAdd(&rep_ptr(tg.slope_grad, t.C)[c], (double)rv[6]);
+    }
+}
+
+// the 2 x 4 form applies: W % 4 == 0 and every full-resolution plane 16-B aligned (the
+// upsampled terms 8-B), image strides multiples of 4 floats
+bool al(const void* p, int b) { return ((uintptr_t)p % b) == 0; }
+bool tail4_ok(const isg_tail& t, const isg_tail_grad* tg) {
+    // planes of >= 128^2 pixels only: at 64^2 the halved grid (512 workgroups at 128
+    // channels) measured 0.3-0.4 us slower per op, at 128^2 and up 1.3-2.5 us faster (r03v)
+    static const bool off = getenv("ISG_NO_TAIL4") != nullptr;
+    if (off || t.W % 4 || (int64_t)t.H * t.W < 16384) return false;
+    for (int i = 0; i < t.nterm; ++i) {
+        const isg_vseg& s = t.term[i];
+        if (!al(s.p, t.up[i] ? 8 : 16) || s.n_stride % (t.up[i] ? 2 : 4)) return false;
+        if (tg && tg->dterm[i] && (!al(tg->dterm[i], t.up[i] ? 8 : 16) || tg->dterm_n_stride[i] % (t.up[i] ? 2 : 4)))
+            return false;
+    }
+    if (!tg) return al(t.out, 16) && t.out_n_stride % 4 == 0;
+    if (!al(tg->dout, 16) || tg->dout_n_stride % 4) return false;
+    if (tg->g && (!al(tg->g, 16) || tg->g_n_stride % 4)) return false;
+    return true;
+}
+
 // ---- max-pool ---------------------------------------------------------------------
 struct PoolArgs {
     isg_vtensor x;
@@ -611,6 +802,11 @@ extern "C" {
 int32_t isg_tail_fwd(const isg_tail* t, isg_stream_t st) {
     if ((t->H & 1) || (t->W & 1) || t->nterm < 1 || t->nterm > 3)
         return isg_set_error(ISG_ERR_UNSUPPORTED, "tail fwd: H, W must be even, 1..3 terms");
+    if (tail4_ok(*t, nullptr)) {
+        dim3 grid4((unsigned)((((int64_t)t->H / 2) * (t->W / 4) + kThreads - 1) / kThreads), t->C, t->N);
+        hipLaunchKernelGGL(tail_fwd4_kernel, grid4, dim3(kThreads), 0, st, *t);
+        return isg_check_launch("tail_fwd4_kernel");
+    }
     dim3 grid((unsigned)((((int64_t)t->H / 2) * (t->W / 2) + kThreads - 1) / kThreads), t->C, t->N);
     hipLaunchKernelGGL(tail_fwd_kernel, grid, dim3(kThreads), 0, st, *t);
     return isg_check_launch("tail_fwd_kernel");
@@ -620,6 +816,11 @@ int32_t isg_tail_bwd(const isg_tail_grad* t, isg_stream_t st) {
     const isg_tail& f = t->f;
     if ((f.H & 1) || (f.W & 1) || f.nterm < 1 || f.nterm > 3)
         return isg_set_error(ISG_ERR_UNSUPPORTED, "tail bwd: H, W must be even, 1..3 terms");
+    if (tail4_ok(f, t)) {
+        dim3 grid4((unsigned)((((int64_t)f.H / 2) * (f.W / 4) + kThreads - 1) / kThreads), f.C, f.N);
+        hipLaunchKernelGGL(tail_bwd4_kernel, grid4, dim3(kThreads), 0, st, *t);
+        return isg_check_launch("tail_bwd4_kernel");
+    }
     dim3 grid((unsigned)((((int64_t)f.H / 2) * (f.W / 2) + kThreads - 1) / kThreads), f.C, f.N);
     hipLaunchKernelGGL(tail_bwd_kernel, grid, dim3(kThreads), 0, st, *t);
     return isg_check_launch("tail_bwd_kernel");

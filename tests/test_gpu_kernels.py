@@ -409,8 +409,13 @@ def test_maxpool(k):
 
 @pytest.mark.parametrize("act", ["prelu", "relu"])
 @pytest.mark.parametrize("up", [False, True])
-def test_tail(act, up):
-    N, C, H, W = 2, 8, 16, 12
+@pytest.mark.parametrize("H,W,accum", [(128, 132, True), (16, 14, False)],
+                         ids=["128x132_2x4_accum", "16x14_quad"])
+def test_tail(act, up, H, W, accum):
+    """A >= 128^2 plane with W % 4 == 0 runs the 2x4-unit kernels (tail_fwd4 / tail_bwd4),
+    16 x 14 the 2x2 form; accum: the term gradient adds onto an existing value (prefetched
+    old value)."""
+    N, C = 2, 8
     y = rnd(N, C, H, W, seed=51) + 0.2
     r = rnd(N, C, H // 2, W // 2, seed=52) if up else rnd(N, C, H, W, seed=52)
     gamma, beta, st0, slope = _bn_train_state(y, torch.zeros_like(y), 53)
@@ -443,13 +448,18 @@ def test_tail(act, up):
         else torch.where(pre > 0, dout, torch.zeros_like(dout))
     dr = F.avg_pool2d(g, 2) * 4 if up else g
     Gt = torch.full((N, C, H, W), float("nan"), device=DEV)
-    DR = torch.full(tuple(r.shape), float("nan"), device=DEV)
+    DR0 = rnd(*tuple(r.shape), seed=55)
+    DR = cuda32(DR0) if accum else torch.full(tuple(r.shape), float("nan"), device=DEV)
+    if accum:
+        dr = dr + DR0
     sg = rep_zeros(C)
-    tg = {"f": t, "dout": ptr(cuda32(dout)), "dout_n_stride": C * H * W, "g": ptr(Gt),
+    DO = cuda32(dout)  # held until the kernel has run
+    tg = {"f": t, "dout": ptr(DO), "dout_n_stride": C * H * W, "g": ptr(Gt),
           "g_n_stride": C * H * W, "dterm": [None, ptr(DR), None],
-          "dterm_n_stride": [0, R[0].numel(), 0], "dterm_accum": [0, 0, 0],
+          "dterm_n_stride": [0, R[0].numel(), 0], "dterm_accum": [0, 1 if accum else 0, 0],
           "slope_grad": ptr(sg)}
     call("isg_tail_bwd", struct(LL.TailGrad, tg), stream())
+    torch.cuda.synchronize()
     close(Gt, g, what="tail g")
     close(DR, dr, what="tail dterm")
     ST, sg = rep_fold(ST, 4 * C), rep_fold(sg, C)
