@@ -550,6 +550,34 @@ def _fork_branches(ol, side_recs):
                 break
 
 
+def _fork_late_wgrads(recs, late):
+    """The executor defers side-stream weight gradients in batches until a join; at the end
+    of the backward that parks the last batch (and the stem's own weight gradients, whose
+    dy is ready before the stem's input-gradient chain runs) behind the whole stem chain.
+    Fork the pending batch where the stem's backward begins, and each stem weight gradient
+    at its place (OPF_FORK_NOW), so they overlap the stem's input-gradient kernels."""
+    if os.environ.get("ISG_NO_LATE_FORK", "0") == "1" or not late:
+        return
+    tag = late.rstrip(".")
+    first_late = next((i for i, r in enumerate(recs) if tag in r.label), None)
+    if first_late is None:
+        return
+    prev = [r for r in recs[:first_late] if r.flags & Record.OPF_SIDE]
+    if prev:
+        prev[-1].flags |= Record.OPF_FORK_NOW
+    for r in recs[first_late:]:
+        if r.flags & Record.OPF_SIDE:
+            r.flags |= Record.OPF_FORK_NOW
+    # a stem weight gradient right behind its own input gradient moves in front of it: its
+    # operands (dy, the forward input) are ready, so it forks before that kernel instead of
+    # behind it (a weight gradient reads nothing the input gradient writes)
+    for i in range(first_late, len(recs) - 1):
+        a, b = recs[i], recs[i + 1]
+        if (a.kind == L.OP_CONV_DGRAD and b.kind == L.OP_CONV_WGRAD and a.label.startswith("dx_")
+                and b.label == "dw_" + a.label[3:]):
+            recs[i], recs[i + 1] = b, a
+
+
 def sinks_spec(sinks):
     """isg_sinks spec from sink specs; a sink's private '_fin_ctr' (the ticket of a fused
     BN finalisation) becomes the launch's fin_counter."""
@@ -1121,6 +1149,7 @@ class Plan:
         for r in body.recs:
             if r.kind in (L.OP_CONV_WGRAD, L.OP_KP_STEM_WGRAD):
                 r.flags |= Record.OPF_SIDE  # nothing later in the list reads a weight gradient
+        _fork_late_wgrads(body.recs, self._late_prefix(g))
         self.din_written = [isinstance(v, Value) and v.grad and
                             bool(gs.inited.get(id(v.segs[0].buf))) for v in ins]
         # finalisation of BN / PReLU / conv-bias-before-BN gradients: (module, item)

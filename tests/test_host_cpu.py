@@ -225,9 +225,14 @@ def test_forward_side_branches_fork_and_join():
             assert any(recs[j].flags & Record.OPF_JOIN for j in range(i + 1, readers[0] + 1)), \
                 op.out.name
     # backward: no branch work on the side stream (shared dx sinks); only bucket 1's
-    # replica fold and gradient finalisation fork there (after every statistic is done)
+    # replica fold and gradient finalisation fork there (after every statistic is done),
+    # and weight gradients (engine._fork_late_wgrads: the batch pending when the stem's
+    # backward begins, and the stem's own weight gradients)
     assert not any(r.flags & Record.OPF_FORK_NOW for r in p.bwd.recs
-                   if r.kind not in (L.OP_SUM_REP, L.OP_GRAD_FINAL))
+                   if r.kind not in (L.OP_SUM_REP, L.OP_GRAD_FINAL, L.OP_CONV_WGRAD,
+                                     L.OP_KP_STEM_WGRAD))
+    assert all(r.flags & Record.OPF_SIDE for r in p.bwd.recs if r.flags & Record.OPF_FORK_NOW
+               and r.kind in (L.OP_CONV_WGRAD, L.OP_KP_STEM_WGRAD))
 
 
 @pytest.mark.parametrize("n", [1, 2])
