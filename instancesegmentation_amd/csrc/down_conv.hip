@@ -708,6 +708,247 @@ __global__ __launch_bounds__(kThreads) void s2k5_fwd_kernel(DownArgs a) {
     sinks_finalize(a.out);
 }
 
+// ---- 5x5 stride-2 pad-2 weight gradient, LDS-staged (the stem's second conv) ------------
+//   dW[m][c][kh][kw] = sum_{n,oy,ox} dy[m][n][oy][ox] * X[c][n][2oy - 2 + kh][2ox - 2 + kw]
+// One v_mfma_f32_16x16x4_f32 per tap and pixel quad: D[m][c] += A[m][4 pixels] x
+// B[4 pixels][c], A = dy (lane: m = l&15, pixel = l>>4), B = the band value of channel
+// c = l&15 under the tap for pixel l>>4 — one A read serves the 25 taps (25 accumulators
+// per lane, no dependent MFMA chain). A tile is kWgRows output rows (wave w = row w) x
+// kWgX output columns of one image: its input band (2*kWgRows + 3 rows x 72 columns x 16
+// channels, producer BatchNorm + activation applied once per element, split into even /
+// odd column planes as in s2k5_fwd_kernel) and its dy block (BatchNorm backward rebuilt
+// once per element) go to LDS with 16-B loads. Persistent workgroups walk a contiguous run
+// of tiles (runs grouped per XCD so neighbouring bands share an L2), the next tile's loads
+// in flight during this tile's MFMAs. Epilogue: the 4 waves' partials summed in LDS, one
+// coalesced f32 atomic per dW element per workgroup into an ISG_WREP replica.
+constexpr int kWgRows = 4;
+constexpr int kWgX = 32;                   // output columns per tile
+constexpr int kWgNR = 2 * kWgRows + 3;     // staged input rows
+constexpr int kWgQ = kWgX / 2 + 2;         // 16-B quads per staged row (from column 2*ox0 - 4)
+constexpr int kWgEW = 2 * kWgQ;            // columns per parity plane
+constexpr int kWgRS = 2 * kWgEW;           // staged row: [even | odd]
+constexpr int kWgPL = 802;                 // channel plane (>= 11 * 72; 2 mod 32: B reads conflict-free)
+constexpr int kWgDQ = 130;                 // dy channel block (>= 4 * 32; 2 mod 32: A reads conflict-free)
+constexpr int kWgLds = kMaxM * kWgPL + kMaxM * kWgDQ;  // floats
+constexpr int kWgNW = kMaxM * kMaxM * 25;  // dW elements of one workgroup's partial
+static_assert(kWgPL >= kWgNR * kWgRS && kWgPL % 32 == 2 && kWgDQ % 32 == 2 && kWgDQ >= kWgRows * kWgX,
+              "s2k5 wgrad layout");
+static_assert(2 * kWgNW <= kWgLds, "s2k5 wgrad epilogue regions");
+
+struct S2wArgs {
+    isg_vtensor dy;  // the conv's output gradient: M channels, OH x OW
+    isg_vtensor x;   // its input: C channels, 2 OH x 2 OW
+    float* dw;
+    float* dbias;
+    int64_t rep_stride;
+    int nrep;
+    int N, M, C, OH, OW;
+    int tiles_x, tiles_y, ntiles, tpw;
+    int dbg;  // ablation bits (ISG_S2W_DBG, experiments only): 1 no MFMA loop, 2 no global loads, 4 no LDS staging
+};
+
+// Branch-free staging record: x side v = (raw - k0) * k1 + k2, then v > 0 ? v : v * k3
+// (PLAIN: identity, ReLU: k3 = 0, PReLU: k3 = slope, none: k3 = 1); dy side
+// k0 * raw + k1 * (y - k2) + k3 (PLAIN: k0 = 1). A per-lane channel (the staging items
+// span channels within a wave) otherwise makes every transform a divergent branch tree.
+struct S2Ch {
+    const float* p;
+    const float* y;
+    int ns, yns;
+    f32x4 k;
+};
+
+ISG_DEV S2Ch s2_ch_addr(const isg_vtensor& vt, int c, int hw) {
+    const ChSrc t = ch_src(vt_lite(vt), c, hw);
+    return S2Ch{t.p, t.y, t.ns, t.yns, f32x4{0.f, 0.f, 0.f, 0.f}};
+}
+
+ISG_DEV f32x4 s2_coef_x(const isg_vtensor& vt, int c, int hw) {
+    const ChSrc t = ch_src(vt_lite(vt), c, hw);
+    f32x4 k{0.f, 1.f, 0.f, 1.f};
+    const ChanCoef q = vt_coef(vt, c);
+    if (t.xf == ISG_XF_BN_FWD) { k[0] = q.c0; k[1] = q.c1; k[2] = q.c2; }
+    k[3] = t.act == ISG_ACT_RELU ? 0.f : t.act == ISG_ACT_PRELU ? q.c3 : 1.f;
+    return k;
+}
+
+ISG_DEV f32x4 s2_coef_dy(const isg_vtensor& vt, int c, int hw) {
+    const ChSrc t = ch_src(vt_lite(vt), c, hw);
+    if (t.xf != ISG_XF_BN_BWD) return f32x4{1.f, 0.f, 0.f, 0.f};
+    const ChanCoef q = vt_coef(vt, c);
+    return f32x4{q.c0, q.c1, q.c2, q.c3};
+}
+
+template <bool YB>
+__global__ __launch_bounds__(kThreads, 2) void s2k5_wgrad_kernel(S2wArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float s2w_lds[];
+    float* const Xs = s2w_lds;                 // [16][kWgPL]
+    float* const Ds = s2w_lds + kMaxM * kWgPL;  // [16][kWgDQ]
+    __shared__ S2Ch tabx[kMaxM];
+    __shared__ S2Ch taby[kMaxM];
+    __shared__ float bred[4][64];
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
+    const int kq = lane >> 4, pl = lane & 15;
+    const int G = gridDim.x, b = blockIdx.x;
+    const int L = (G % 8 == 0) ? (b % 8) * (G / 8) + b / 8 : b;  // XCD-grouped runs
+    const int t0 = L * a.tpw, t1 = min(t0 + a.tpw, a.ntiles);
+    if (t0 >= t1) return;
+    STAMP(0);
+    const int Ho = a.OH, Wo = a.OW, Hi = 2 * Ho, Wi = 2 * Wo;
+    // addresses first: the first tile's loads are in flight while the BatchNorm
+    // coefficients are evaluated from the statistics (fp64, one thread per channel)
+    if (tid < kMaxM) {
+        tabx[tid] = s2_ch_addr(a.x, min(tid, a.C - 1), Hi * Wi);
+        taby[tid] = s2_ch_addr(a.dy, min(tid, a.M - 1), Ho * Wo);
+    }
+    __syncthreads();
+    STAMP(1);
+
+    constexpr int NE = kMaxM * kWgNR * kWgQ;
+    constexpr int UX = (NE + kThreads - 1) / kThreads;
+    constexpr int ND = kMaxM * kWgRows * (kWgX / 4);
+    constexpr int UD = (ND + kThreads - 1) / kThreads;
+    f32x4 xv[UX], dv[UD], yv[UD];
+    int n = 0, oy0 = 0, ox0 = 0;
+    auto tile_geo = [&](int t) {
+        const int tpi = a.tiles_x * a.tiles_y;
+        n = t / tpi;
+        const int r = t - n * tpi, ty = r / a.tiles_x;
+        oy0 = ty * kWgRows;
+        ox0 = (r - ty * a.tiles_x) * kWgX;
+    };
+    auto load = [&](int t) {
+        tile_geo(t);
+#pragma unroll
+        for (int u = 0; u < UX; ++u) {
+            const int e = min(tid + u * kThreads, NE - 1);
+            const int c = e / (kWgNR * kWgQ), rq = e - c * (kWgNR * kWgQ);
+            const int rr = rq / kWgQ, q = rq - rr * kWgQ;
+            const int iy = 2 * oy0 - 2 + rr, ix = 2 * ox0 - 4 + 4 * q;
+            const bool ok = c < a.C && (unsigned)iy < (unsigned)Hi && ix >= 0 && ix < Wi;
+            const S2Ch& t = tabx[c];
+            xv[u] = gld4(t.p + (int64_t)n * t.ns, ok ? (int64_t)iy * Wi + ix : 0);
+        }
+#pragma unroll
+        for (int u = 0; u < UD; ++u) {
+            const int e = min(tid + u * kThreads, ND - 1);
+            const int m = e / (kWgRows * kWgX / 4), rem = e - m * (kWgRows * kWgX / 4);
+            const int r = rem / (kWgX / 4), qx = rem - r * (kWgX / 4);
+            const int oy = oy0 + r, ox = ox0 + 4 * qx;
+            const bool ok = m < a.M && oy < Ho && ox < Wo;
+            const S2Ch& t = taby[m];
+            const int64_t o = ok ? (int64_t)oy * Wo + ox : 0;
+            dv[u] = gld4(t.p + (int64_t)n * t.ns, o);
+            if constexpr (YB) yv[u] = gld4(t.y + (int64_t)n * t.yns, o);
+        }
+    };
+    auto store = [&]() {
+#pragma unroll
+        for (int u = 0; u < UX; ++u) {
+            const int e = tid + u * kThreads;
+            if (e >= NE) continue;
+            const int c = e / (kWgNR * kWgQ), rq = e - c * (kWgNR * kWgQ);
+            const int rr = rq / kWgQ, q = rq - rr * kWgQ;
+            const int iy = 2 * oy0 - 2 + rr, ix = 2 * ox0 - 4 + 4 * q;
+            const bool ok = c < a.C && (unsigned)iy < (unsigned)Hi && ix >= 0 && ix < Wi;
+            const f32x4 kk = tabx[c].k;
+            f32x4 v;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float z = (xv[u][k] - kk[0]) * kk[1] + kk[2];
+                v[k] = ok ? (z > 0.f ? z : z * kk[3]) : 0.f;
+            }
+            float* row = Xs + c * kWgPL + rr * kWgRS + 2 * q;
+            *reinterpret_cast<f32x2*>(row) = f32x2{v[0], v[2]};
+            *reinterpret_cast<f32x2*>(row + kWgEW) = f32x2{v[1], v[3]};
+        }
+#pragma unroll
+        for (int u = 0; u < UD; ++u) {
+            const int e = tid + u * kThreads;
+            if (e >= ND) continue;
+            const int m = e / (kWgRows * kWgX / 4), rem = e - m * (kWgRows * kWgX / 4);
+            const int r = rem / (kWgX / 4), qx = rem - r * (kWgX / 4);
+            const bool ok = m < a.M && oy0 + r < Ho && ox0 + 4 * qx < Wo;
+            const f32x4 kk = taby[m].k;
+            f32x4 v;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                v[k] = ok ? kk[0] * dv[u][k] + kk[1] * ((YB ? yv[u][k] : dv[u][k]) - kk[2]) + kk[3] : 0.f;
+            float* d = Ds + m * kWgDQ + r * kWgX + 4 * qx;
+            *reinterpret_cast<f32x2*>(d) = f32x2{v[0], v[1]};
+            *reinterpret_cast<f32x2*>(d + 2) = f32x2{v[2], v[3]};
+        }
+    };
+
+    f32x4 acc[25];
+#pragma unroll
+    for (int t = 0; t < 25; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float bsum = 0.f;
+    const float* const ab = Ds + pl * kWgDQ + wave * kWgX + kq;
+    const float* const bb = Xs + pl * kWgPL + 2 * wave * kWgRS + kq + 1;
+    if (!(a.dbg & 2)) load(t0);
+    if (tid < kMaxM) {
+        tabx[tid].k = s2_coef_x(a.x, min(tid, a.C - 1), Hi * Wi);
+    } else if (tid >= 64 && tid < 64 + kMaxM) {
+        taby[tid - 64].k = s2_coef_dy(a.dy, min(tid - 64, a.M - 1), Ho * Wo);
+    }
+    const int nq = (a.dbg & 1) ? 0 : kWgX / 4;
+    for (int t = t0; t < t1; ++t) {
+        __syncthreads();  // the previous tile's operand reads are done
+        if (!(a.dbg & 4)) store();
+        __syncthreads();
+        if (t == t0) STAMP(2);
+        if (t + 1 < t1 && !(a.dbg & 2)) load(t + 1);
+#pragma unroll 1
+        for (int q = 0; q < nq; ++q) {
+            const float av = ab[4 * q];
+            bsum += av;
+#pragma unroll
+            for (int kh = 0; kh < 5; ++kh)
+#pragma unroll
+                for (int kw = 0; kw < 5; ++kw)
+                    acc[kh * 5 + kw] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                        av, bb[kh * kWgRS + (kw & 1) * kWgEW + (kw >> 1) + 4 * q], acc[kh * 5 + kw], 0, 0, 0);
+        }
+    }
+
+    // ---- epilogue: lane holds D[m = 4kq + i][c = pl] of every tap
+    STAMP(3);
+    __syncthreads();
+    float* const R = s2w_lds;  // two regions of [16][16][25]
+    if (wave < 2) {
+#pragma unroll
+        for (int t = 0; t < 25; ++t)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) R[wave * kWgNW + ((4 * kq + i) * kMaxM + pl) * 25 + t] = acc[t][i];
+    }
+    bred[wave][lane] = bsum;
+    __syncthreads();
+    if (wave >= 2) {
+#pragma unroll
+        for (int t = 0; t < 25; ++t)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) R[(wave - 2) * kWgNW + ((4 * kq + i) * kMaxM + pl) * 25 + t] += acc[t][i];
+    }
+    __syncthreads();
+    float* const dwr = a.dw + (int64_t)(blockIdx.x % a.nrep) * a.rep_stride;
+    for (int e = tid; e < kWgNW; e += kThreads) {
+        const int m = e / (kMaxM * 25), rem = e - m * (kMaxM * 25);
+        const int c = rem / 25, tap = rem - c * 25;
+        if (m < a.M && c < a.C) atomicAdd(&dwr[(m * a.C + c) * 25 + tap], R[e] + R[kWgNW + e]);
+    }
+    if (a.dbias && tid < a.M) {
+        float s = 0.f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w)
+            s += ((bred[w][tid] + bred[w][16 + tid]) + bred[w][32 + tid]) + bred[w][48 + tid];
+        atomicAdd(&(a.dbias + (int64_t)(blockIdx.x % a.nrep) * a.rep_stride)[tid], s);
+    }
+    STAMP(4);
+}
+
 bool down_geom(const isg_conv_geom* g, int& S) {
     S = g->SH;
     return g->groups == 1 && (S == 2 || S == 4) && g->SW == S && g->KH == 2 * S && g->KW == 2 * S &&
@@ -725,6 +966,8 @@ bool down_src_ok(const isg_vtensor* v) {
 }
 
 }  // namespace
+
+ISG_STAMP_ACCESSOR(isg_dbg_stamps_down)
 
 // Returns 1 if launched, 0 if the shape is not for these kernels, <0 on error.
 int32_t isg_down_conv_fwd(const isg_conv_geom* g, const isg_vtensor* src, const float* w,
@@ -828,5 +1071,60 @@ int32_t isg_s2k5_fwd(const isg_conv_geom* g, const isg_vtensor* x, const float* 
     hipLaunchKernelGGL(s2k5_fwd_kernel, grid, dim3(kThreads), 0, st, a);
     if (out->fin_counter) isg_fin_note_handled();
     const int32_t e = isg_check_launch("s2k5_fwd_kernel");
+    return e ? e : 1;
+}
+
+// 5x5 stride 2 pad 2 weight gradient with <= 16 input / output channels (s2k5_wgrad_kernel).
+// Returns 1 if launched, 0 if the shape is not for this kernel, <0 on error.
+int32_t isg_s2k5_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x,
+                       float* dw, float* dbias, int64_t rep_stride, int32_t nrep, hipStream_t st) {
+    static const bool off = getenv("ISG_NO_S2K5_WGRAD") != nullptr;
+    if (off || g->groups != 1 || g->SH != 2 || g->SW != 2 || g->KH != 5 || g->KW != 5 ||
+        g->PH != 2 || g->PW != 2 || g->DH != 1 || g->DW != 1 || g->H != 2 * g->OH ||
+        g->W != 2 * g->OW || g->OW % 4 || g->Co > kMaxM || g->Ci > kMaxM ||
+        (g->w_ci && g->w_ci != g->Ci) || !down_src_ok(x) || !down_src_ok(dy))
+        return 0;
+    // the kernel's branch-free transforms: x PLAIN / BN_FWD with any activation, dy PLAIN /
+    // BN_BWD without one
+    for (int i = 0; i < x->nseg; ++i)
+        if (x->s[i].xform == ISG_XF_BN_BWD) return 0;
+    for (int i = 0; i < dy->nseg; ++i)
+        if (dy->s[i].xform == ISG_XF_BN_FWD || dy->s[i].act != ISG_ACT_NONE) return 0;
+    if ((int64_t)g->H * g->W >= (1ll << 31)) return 0;
+    S2wArgs a{};
+    a.dy = *dy; a.x = *x; a.dw = dw; a.dbias = dbias;
+    a.rep_stride = nrep > 1 ? rep_stride : 0;
+    a.nrep = nrep < 1 ? 1 : nrep;
+    a.N = g->N; a.M = g->Co; a.C = g->Ci; a.OH = g->OH; a.OW = g->OW;
+    static const int dbg = getenv("ISG_S2W_DBG") ? atoi(getenv("ISG_S2W_DBG")) : 0;
+    a.dbg = dbg;
+    a.tiles_x = (a.OW + kWgX - 1) / kWgX;
+    a.tiles_y = (a.OH + kWgRows - 1) / kWgRows;
+    const int64_t nt = (int64_t)a.N * a.tiles_x * a.tiles_y;
+    if (nt >= (1ll << 31)) return 0;
+    a.ntiles = (int)nt;
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+            cus = 256;
+    }
+    static const int env_wg = getenv("ISG_S2W_WGS") ? atoi(getenv("ISG_S2W_WGS")) : 0;
+    const int target = env_wg > 0 ? env_wg : 2 * cus;  // two workgroups per CU (LDS 60 KB each)
+    a.tpw = (int)std::max<int64_t>(1, (nt + target - 1) / target);
+    const int grid = (int)((nt + a.tpw - 1) / a.tpw);
+    bool yb = false;
+    for (int i = 0; i < dy->nseg; ++i) yb |= dy->s[i].xform == ISG_XF_BN_BWD && dy->s[i].y != dy->s[i].p;
+    const size_t lds = (size_t)kWgLds * sizeof(float);
+    auto k = yb ? s2k5_wgrad_kernel<true> : s2k5_wgrad_kernel<false>;
+    static bool attr[2] = {false, false};
+    if (!attr[yb]) {
+        if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+            return isg_check_launch("s2k5_wgrad_kernel: dynamic LDS");
+        attr[yb] = true;
+    }
+    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(kThreads), lds, st, a);
+    const int32_t e = isg_check_launch("s2k5_wgrad_kernel");
     return e ? e : 1;
 }

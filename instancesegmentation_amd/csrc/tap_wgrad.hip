@@ -674,7 +674,8 @@ int32_t twa_try(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor
     const int KK = g->KH * g->KW;
     // measured (kbench): the stem layer1 (20 x 25 columns) 433 -> 308 us; the 16-channel
     // layer2 (400 columns, a 4x smaller map) is faster on the chunked kernel (71 vs ~100 us)
-    if (g->Ci * KK > 16 * kTwaTiles || g->Ci * KK < 448) return 0;
+    static const bool force = getenv("ISG_TWA_FORCE") != nullptr;
+    if (g->Ci * KK > 16 * kTwaTiles || (g->Ci * KK < 448 && !force)) return 0;
     TwaArgs a{};
     a.N = g->N; a.C = g->Ci; a.Co = g->Co; a.H = g->H; a.W = g->W; a.OH = g->OH; a.OW = g->OW;
     a.WC = g->w_ci > 0 ? g->w_ci : g->Ci;

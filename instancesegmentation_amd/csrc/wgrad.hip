@@ -604,6 +604,8 @@ int32_t isg_thin_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_
 int32_t isg_down_conv_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x,
                             float* dw, float* dbias, int64_t rep_stride, int32_t nrep,
                             hipStream_t st);
+int32_t isg_s2k5_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x,
+                       float* dw, float* dbias, int64_t rep_stride, int32_t nrep, hipStream_t st);
 
 int32_t isg_dense_conv_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x,
                              float* dw, float* dbias, int64_t rep_stride, int32_t nrep,
@@ -615,6 +617,8 @@ int32_t isg_dense_conv_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, cons
         int32_t t = isg_thin_wgrad(g, dy, x, dw, dbias, rep_stride, nrep, st);
         if (t != 0) return t < 0 ? t : 0;
         t = isg_down_conv_wgrad(g, dy, x, dw, dbias, rep_stride, nrep, st);  // convT weights
+        if (t != 0) return t < 0 ? t : 0;
+        t = isg_s2k5_wgrad(g, dy, x, dw, dbias, rep_stride, nrep, st);  // the stem's layer 2
         if (t != 0) return t < 0 ? t : 0;
         t = isg_tap_wgrad(g, dy, x, dw, dbias, rep_stride, nrep, st);
         if (t != 0) return t < 0 ? t : 0;

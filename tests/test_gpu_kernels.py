@@ -185,6 +185,49 @@ def test_s2k5_fwd(cfg, monkeypatch):
     close(stats[Co:2 * Co], (ref * ref).sum((0, 2, 3)), tol=4e-6, what="sumsq")
 
 
+@pytest.mark.parametrize("cfg", [(16, 16, 512, 512), (16, 16, 134, 200), (12, 10, 72, 200),
+                                 (3, 16, 64, 48)],
+                         ids=["stem_bench", "ragged", "narrow_partial_rows", "three_channels"])
+def test_s2k5_wgrad(cfg):
+    """The LDS-staged 5x5 s2 weight gradient (down_conv.hip s2k5_wgrad_kernel, the stem's
+    layer 2 on the bench step) through the replicated entry point, against fp64: dy with
+    training-mode BatchNorm backward rebuilt on load, x with BatchNorm + PReLU on load, the
+    dbias, at the bench geometry (2x512^2 -> 256^2, 1024 tiles over persistent workgroups),
+    a partial last column tile, a partial last row tile with fewer than 16 channels on both
+    sides, and 3 input channels."""
+    Ci, Co, H, W = cfg
+    N = 2
+    ge, OH, OW = _geom(N, Ci, Co, H, W, 5, 2, 2, 1)
+    x = rnd(N, Ci, H, W, seed=51)
+    gamma, beta, rm, rv, slope = bn_eval_params(Ci, 52)
+    xt = fwd_xform_ref(x, gamma, beta, rm, rv, slope, "prelu")
+    yraw = rnd(N, Co, OH, OW, seed=53) + 0.3
+    gbn = rnd(N, Co, OH, OW, seed=54)
+    og, ob, st, _ = _bn_train_state(yraw, gbn, 55)
+    dy = _bn_bwd_ref(yraw, gbn, og)
+    ref = torch.nn.grad.conv2d_weight(xt, (Co, Ci, 5, 5), dy, stride=2, padding=2)
+    X, G = cuda32(x), [cuda32(t) for t in (gamma, beta, rm, rv, slope)]
+    xseg = {"p": ptr(X), "n_stride": Ci * H * W, "C": Ci, "xform": L.XF_BN_FWD,
+            "act": L.ACT["prelu"], "slope": ptr(G[4]), "bn": bn_spec_eval(*G[:4])}
+    Yr, Gb, GA, BE, ST = cuda32(yraw), cuda32(gbn), cuda32(og), cuda32(ob), rep_from(st)
+    dyseg = {"p": ptr(Gb), "y": ptr(Yr), "n_stride": Co * OH * OW, "y_n_stride": Co * OH * OW,
+             "C": Co, "xform": L.XF_BN_BWD, "bn": bn_spec_train(GA, BE, ST, N * OH * OW)}
+    nw = Co * Ci * 25
+    stride_ = nw + Co + 5
+    REP = torch.zeros(L.WREP * stride_, device=DEV)
+    call("isg_conv_wgrad_rep", geom(**ge), vt([dyseg], N, OH, OW), vt([xseg], N, H, W),
+         ptr(REP), ptr(REP[nw:]), stride_, L.WREP, stream())
+    OUT = torch.full((stride_,), float("nan"), device=DEV)
+    call("isg_sum_replicas", ptr(OUT), ptr(REP), stride_, L.WREP, stride_, stream())
+    torch.cuda.synchronize()
+    close(OUT[:nw].view(Co, Ci, 5, 5), ref, what="s2k5 wgrad")
+    # the BatchNorm-backward dy sums to ~0 per channel: the dbias bar is relative to the
+    # summed magnitudes (one fp32 rounding per partial over 2 x 256^2 terms)
+    derr = (OUT[nw:nw + Co].double().cpu() - dy.sum((0, 2, 3))).abs().max().item()
+    assert derr <= 1e-6 * dy.abs().sum((0, 2, 3)).max().item(), derr
+    assert torch.all(OUT[nw + Co:] == 0)
+
+
 def _bn_train_state(y, g, seed):
     """stats [sum, sumsq, gsum, gxsum] for raw y and BN-output grad g (gxsum centred)."""
     C = y.shape[1]

@@ -14,6 +14,7 @@
 
 extern "C" void* isg_dbg_stamps_wgrad(void);
 extern "C" void* isg_dbg_stamps_pw(void);
+extern "C" void* isg_dbg_stamps_down(void);
 
 #define CK(x)                                                                   \
     do {                                                                        \
@@ -158,7 +159,8 @@ int main(int argc, char** argv) {
     float ms;
     CK(hipEventElapsedTime(&ms, e0, e1));
     // stamped single launch
-    unsigned long long* sp = (unsigned long long*)(strcmp(op, "wgrad") ? isg_dbg_stamps_pw() : isg_dbg_stamps_wgrad());
+    unsigned long long* sp = (unsigned long long*)(getenv("KB_STAMPS_DOWN") ? isg_dbg_stamps_down()
+                                                   : strcmp(op, "wgrad") ? isg_dbg_stamps_pw() : isg_dbg_stamps_wgrad());
     CK(hipMemset(sp, 0, 65536 * 8 * sizeof(unsigned long long)));
     run();
     CK(hipStreamSynchronize(st));
