@@ -780,17 +780,19 @@ ISG_DEV f32x4 s2_coef_dy(const isg_vtensor& vt, int c, int hw) {
 }
 
 template <bool YB>
-__global__ __launch_bounds__(kThreads, 2) void s2k5_wgrad_kernel(S2wArgs a) {
-    extern __shared__ __attribute__((aligned(16))) float s2w_lds[];
-    float* const Xs = s2w_lds;                 // [16][kWgPL]
-    float* const Ds = s2w_lds + kMaxM * kWgPL;  // [16][kWgDQ]
+__global__ __launch_bounds__(2 * kThreads, 1) void s2k5_wgrad_kernel(S2wArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float s2w_lds[];  // 2 x [Xs | Ds]
     __shared__ S2Ch tabx[kMaxM];
     __shared__ S2Ch taby[kMaxM];
     __shared__ float bred[4][64];
     typedef float f32x2 __attribute__((ext_vector_type(2)));
 
+    // waves 0-3 consume (MFMA, wave w = tile row w), waves 4-7 produce (stage the next
+    // tile into the other buffer while the consumers' MFMAs run on the same SIMDs)
     const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
     const int kq = lane >> 4, pl = lane & 15;
+    const bool producer = wave >= 4;
+    const int ptid = tid - kThreads;
     const int G = gridDim.x, b = blockIdx.x;
     const int L = (G % 8 == 0) ? (b % 8) * (G / 8) + b / 8 : b;  // XCD-grouped runs
     const int t0 = L * a.tpw, t1 = min(t0 + a.tpw, a.ntiles);
@@ -811,19 +813,17 @@ __global__ __launch_bounds__(kThreads, 2) void s2k5_wgrad_kernel(S2wArgs a) {
     constexpr int ND = kMaxM * kWgRows * (kWgX / 4);
     constexpr int UD = (ND + kThreads - 1) / kThreads;
     f32x4 xv[UX], dv[UD], yv[UD];
-    int n = 0, oy0 = 0, ox0 = 0;
-    auto tile_geo = [&](int t) {
+    int n = 0, oy0 = 0, ox0 = 0;  // the tile held in xv / dv / yv
+    auto load = [&](int t) {
         const int tpi = a.tiles_x * a.tiles_y;
         n = t / tpi;
         const int r = t - n * tpi, ty = r / a.tiles_x;
         oy0 = ty * kWgRows;
         ox0 = (r - ty * a.tiles_x) * kWgX;
-    };
-    auto load = [&](int t) {
-        tile_geo(t);
+        if (a.dbg & 2) return;
 #pragma unroll
         for (int u = 0; u < UX; ++u) {
-            const int e = min(tid + u * kThreads, NE - 1);
+            const int e = min(ptid + u * kThreads, NE - 1);
             const int c = e / (kWgNR * kWgQ), rq = e - c * (kWgNR * kWgQ);
             const int rr = rq / kWgQ, q = rq - rr * kWgQ;
             const int iy = 2 * oy0 - 2 + rr, ix = 2 * ox0 - 4 + 4 * q;
@@ -833,7 +833,7 @@ __global__ __launch_bounds__(kThreads, 2) void s2k5_wgrad_kernel(S2wArgs a) {
         }
 #pragma unroll
         for (int u = 0; u < UD; ++u) {
-            const int e = min(tid + u * kThreads, ND - 1);
+            const int e = min(ptid + u * kThreads, ND - 1);
             const int m = e / (kWgRows * kWgX / 4), rem = e - m * (kWgRows * kWgX / 4);
             const int r = rem / (kWgX / 4), qx = rem - r * (kWgX / 4);
             const int oy = oy0 + r, ox = ox0 + 4 * qx;
@@ -844,10 +844,13 @@ __global__ __launch_bounds__(kThreads, 2) void s2k5_wgrad_kernel(S2wArgs a) {
             if constexpr (YB) yv[u] = gld4(t.y + (int64_t)n * t.yns, o);
         }
     };
-    auto store = [&]() {
+    auto store = [&](int buf) {
+        if (a.dbg & 4) return;
+        float* const Xs = s2w_lds + buf * kWgLds;
+        float* const Ds = Xs + kMaxM * kWgPL;
 #pragma unroll
         for (int u = 0; u < UX; ++u) {
-            const int e = tid + u * kThreads;
+            const int e = ptid + u * kThreads;
             if (e >= NE) continue;
             const int c = e / (kWgNR * kWgQ), rq = e - c * (kWgNR * kWgQ);
             const int rr = rq / kWgQ, q = rq - rr * kWgQ;
@@ -866,7 +869,7 @@ __global__ __launch_bounds__(kThreads, 2) void s2k5_wgrad_kernel(S2wArgs a) {
         }
 #pragma unroll
         for (int u = 0; u < UD; ++u) {
-            const int e = tid + u * kThreads;
+            const int e = ptid + u * kThreads;
             if (e >= ND) continue;
             const int m = e / (kWgRows * kWgX / 4), rem = e - m * (kWgRows * kWgX / 4);
             const int r = rem / (kWgX / 4), qx = rem - r * (kWgX / 4);
@@ -882,59 +885,78 @@ __global__ __launch_bounds__(kThreads, 2) void s2k5_wgrad_kernel(S2wArgs a) {
         }
     };
 
-    f32x4 acc[25];
-#pragma unroll
-    for (int t = 0; t < 25; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float bsum = 0.f;
-    const float* const ab = Ds + pl * kWgDQ + wave * kWgX + kq;
-    const float* const bb = Xs + pl * kWgPL + 2 * wave * kWgRS + kq + 1;
-    if (!(a.dbg & 2)) load(t0);
-    if (tid < kMaxM) {
-        tabx[tid].k = s2_coef_x(a.x, min(tid, a.C - 1), Hi * Wi);
-    } else if (tid >= 64 && tid < 64 + kMaxM) {
-        taby[tid - 64].k = s2_coef_dy(a.dy, min(tid - 64, a.M - 1), Ho * Wo);
-    }
-    const int nq = (a.dbg & 1) ? 0 : kWgX / 4;
-    for (int t = t0; t < t1; ++t) {
-        __syncthreads();  // the previous tile's operand reads are done
-        if (!(a.dbg & 4)) store();
-        __syncthreads();
-        if (t == t0) STAMP(2);
-        if (t + 1 < t1 && !(a.dbg & 2)) load(t + 1);
-#pragma unroll 1
-        for (int q = 0; q < nq; ++q) {
-            const float av = ab[4 * q];
-            bsum += av;
-#pragma unroll
-            for (int kh = 0; kh < 5; ++kh)
-#pragma unroll
-                for (int kw = 0; kw < 5; ++kw)
-                    acc[kh * 5 + kw] = __builtin_amdgcn_mfma_f32_16x16x4f32(
-                        av, bb[kh * kWgRS + (kw & 1) * kWgEW + (kw >> 1) + 4 * q], acc[kh * 5 + kw], 0, 0, 0);
+    // the two roles run separate loops with the same barrier sequence (A, B, one per tile,
+    // E1, E2), so neither role's registers are live in the other's code
+    float* const R = s2w_lds;  // epilogue: two regions of [16][16][25]
+    if (producer) {
+        load(t0);
+        __syncthreads();  // A: coefficients
+        store(0);
+        if (t0 + 1 < t1) load(t0 + 1);
+        __syncthreads();  // B: tile t0 staged
+        for (int t = t0; t < t1; ++t) {
+            if (t + 1 < t1) {
+                store(((t - t0) & 1) ^ 1);  // registers hold tile t + 1
+                if (t + 2 < t1) load(t + 2);
+            }
+            __syncthreads();
         }
+        __syncthreads();  // E1
+        __syncthreads();  // E2
+    } else {
+        if (tid < kMaxM) {
+            tabx[tid].k = s2_coef_x(a.x, min(tid, a.C - 1), Hi * Wi);
+        } else if (tid >= 64 && tid < 64 + kMaxM) {
+            taby[tid - 64].k = s2_coef_dy(a.dy, min(tid - 64, a.M - 1), Ho * Wo);
+        }
+        f32x4 acc[25];
+#pragma unroll
+        for (int t = 0; t < 25; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        float bsum = 0.f;
+        __syncthreads();  // A
+        __syncthreads();  // B
+        STAMP(2);
+        const int nq = (a.dbg & 1) ? 0 : kWgX / 4;
+        for (int t = t0; t < t1; ++t) {
+            const float* const Xs = s2w_lds + ((t - t0) & 1) * kWgLds;
+            const float* const ab = Xs + kMaxM * kWgPL + pl * kWgDQ + wave * kWgX + kq;
+            const float* const bb = Xs + pl * kWgPL + 2 * wave * kWgRS + kq + 1;
+            // fully unrolled: every operand read is the lane's base address plus an immediate
+            // offset, and the scheduler runs the reads ahead of the MFMAs (a rolled loop
+            // re-derived 25 addresses per step and waited out each read)
+            if (nq) {
+#pragma unroll
+                for (int q = 0; q < kWgX / 4; ++q) {
+                    const float av = ab[4 * q];
+                    bsum += av;
+#pragma unroll
+                    for (int j = 0; j < 25; ++j)
+                        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                            av, bb[(j / 5) * kWgRS + ((j % 5) & 1) * kWgEW + ((j % 5) >> 1) + 4 * q], acc[j], 0, 0, 0);
+                }
+            }
+            __syncthreads();
+        }
+        // ---- epilogue: lane holds D[m = 4kq + i][c = pl] of every tap
+        STAMP(3);
+        if (wave < 2) {
+#pragma unroll
+            for (int t = 0; t < 25; ++t)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) R[wave * kWgNW + ((4 * kq + i) * kMaxM + pl) * 25 + t] = acc[t][i];
+        }
+        bred[wave][lane] = bsum;
+        __syncthreads();  // E1
+        if (wave >= 2) {
+#pragma unroll
+            for (int t = 0; t < 25; ++t)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) R[(wave - 2) * kWgNW + ((4 * kq + i) * kMaxM + pl) * 25 + t] += acc[t][i];
+        }
+        __syncthreads();  // E2
     }
-
-    // ---- epilogue: lane holds D[m = 4kq + i][c = pl] of every tap
-    STAMP(3);
-    __syncthreads();
-    float* const R = s2w_lds;  // two regions of [16][16][25]
-    if (wave < 2) {
-#pragma unroll
-        for (int t = 0; t < 25; ++t)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) R[wave * kWgNW + ((4 * kq + i) * kMaxM + pl) * 25 + t] = acc[t][i];
-    }
-    bred[wave][lane] = bsum;
-    __syncthreads();
-    if (wave >= 2) {
-#pragma unroll
-        for (int t = 0; t < 25; ++t)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) R[(wave - 2) * kWgNW + ((4 * kq + i) * kMaxM + pl) * 25 + t] += acc[t][i];
-    }
-    __syncthreads();
     float* const dwr = a.dw + (int64_t)(blockIdx.x % a.nrep) * a.rep_stride;
-    for (int e = tid; e < kWgNW; e += kThreads) {
+    for (int e = tid; e < kWgNW; e += 2 * kThreads) {
         const int m = e / (kMaxM * 25), rem = e - m * (kMaxM * 25);
         const int c = rem / 25, tap = rem - c * 25;
         if (m < a.M && c < a.C) atomicAdd(&dwr[(m * a.C + c) * 25 + tap], R[e] + R[kWgNW + e]);
@@ -1111,12 +1133,12 @@ int32_t isg_s2k5_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_
             cus = 256;
     }
     static const int env_wg = getenv("ISG_S2W_WGS") ? atoi(getenv("ISG_S2W_WGS")) : 0;
-    const int target = env_wg > 0 ? env_wg : 2 * cus;  // two workgroups per CU (LDS 60 KB each)
+    const int target = env_wg > 0 ? env_wg : cus;  // one 8-wave workgroup per CU (LDS 2 x 60 KB)
     a.tpw = (int)std::max<int64_t>(1, (nt + target - 1) / target);
     const int grid = (int)((nt + a.tpw - 1) / a.tpw);
     bool yb = false;
     for (int i = 0; i < dy->nseg; ++i) yb |= dy->s[i].xform == ISG_XF_BN_BWD && dy->s[i].y != dy->s[i].p;
-    const size_t lds = (size_t)kWgLds * sizeof(float);
+    const size_t lds = (size_t)2 * kWgLds * sizeof(float);
     auto k = yb ? s2k5_wgrad_kernel<true> : s2k5_wgrad_kernel<false>;
     static bool attr[2] = {false, false};
     if (!attr[yb]) {
@@ -1124,7 +1146,7 @@ int32_t isg_s2k5_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_
             return isg_check_launch("s2k5_wgrad_kernel: dynamic LDS");
         attr[yb] = true;
     }
-    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(kThreads), lds, st, a);
+    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(2 * kThreads), lds, st, a);
     const int32_t e = isg_check_launch("s2k5_wgrad_kernel");
     return e ? e : 1;
 }
