@@ -425,13 +425,18 @@ __global__ __launch_bounds__(kThreads) void sub2_dgrad_lds_kernel(DownArgs a) {
     __shared__ float wl[kMaxM * kMaxM * K * K];  // [c][m][kh][kw] (the weight's own layout)
     __shared__ __attribute__((aligned(16))) float Ls[kMaxM * kSubPL];  // [c][row][col] dy band
     __shared__ ChT tab[kMaxM];
+    __shared__ XfLin lin[kMaxM];
     __shared__ SinkRow ri[kMaxM];
     __shared__ float red[4][3][kMaxM];
     const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
     const int kq = lane >> 4, pl = lane & 15;
     const int Hs = a.H, Ws = a.W, Wd = 2 * Ws;
     const int n = blockIdx.z, j0 = blockIdx.x * 64, i0 = blockIdx.y * kRowsPB;
-    if (tid < a.C) tab[tid] = ch_table_entry(a.dy, tid, (int64_t)Hs * Ws);
+    if (tid < a.C) {
+        const ChT t = ch_table_entry(a.dy, tid, (int64_t)Hs * Ws);
+        tab[tid] = t;
+        lin[tid] = xf_lin(t.xf, t.act, t.k);
+    }
     if (tid < a.M) ri[tid] = sink_row(a.out, tid, (int64_t)2 * Hs * Wd);
     for (int e = tid; e < kMaxM * kMaxM * K * K; e += kThreads) {
         const int c = e / (kMaxM * K * K), r = e - c * kMaxM * K * K;
@@ -457,7 +462,7 @@ __global__ __launch_bounds__(kThreads) void sub2_dgrad_lds_kernel(DownArgs a) {
             const ChT t = tab[c < a.C ? c : 0];
             const int64_t o = ok ? (int64_t)yy * Ws + xx : 0;
             xv[u] = gld4(t.p + (int64_t)n * t.ns, o);
-            yv[u] = t.xf == ISG_XF_BN_BWD ? gld4(t.y + (int64_t)n * t.yns, o) : xv[u];
+            yv[u] = gld4(t.y + (int64_t)n * t.yns, o);  // == p unless BN_BWD (an L1 hit)
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -466,14 +471,9 @@ __global__ __launch_bounds__(kThreads) void sub2_dgrad_lds_kernel(DownArgs a) {
             const int c = e / ((kRowsPB + 2) * 16), rq = e - c * (kRowsPB + 2) * 16;
             const int rr = rq >> 4, q = rq & 15;
             float* d = Ls + c * kSubPL + rr * kSubRS + 4 + 4 * q;
-            if (ok) {
-                const ChT t = tab[c];
+            const XfLin l = lin[c < a.C ? c : 0];
 #pragma unroll
-                for (int k = 0; k < 4; ++k) d[k] = ch_xform(t.xf, t.act, t.k, xv[u][k], yv[u][k]);
-            } else {
-#pragma unroll
-                for (int k = 0; k < 4; ++k) d[k] = 0.f;
-            }
+            for (int k = 0; k < 4; ++k) d[k] = ok ? xf_lin_apply(l, xv[u][k], yv[u][k]) : 0.f;
         }
         for (int e = tid; e < kMaxM * (kRowsPB + 2) * 2; e += kThreads) {
             const int c = e / ((kRowsPB + 2) * 2), rs = e - c * (kRowsPB + 2) * 2;

@@ -142,7 +142,7 @@ __global__ __launch_bounds__(kThreads) void pw_kernel(PwArgs a) {
             for (int u = 0; u < kKC / 4; ++u) {
                 const int k = wave + 4 * u;
                 const ChT c = tab[kc + min(k, kn - 1)];
-                const float t = ch_xform(c.xf, c.act, c.k, v[u], yv[u]);
+                const float t = ch_xform_u(c.xf, c.act, c.k, v[u], yv[u]);  // k is wave-uniform
                 Xs[k * kXst + lane] = (k < kn && pv_l) ? t : 0.f;
             }
         }
@@ -452,13 +452,15 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
     for (int u = 0; u < XU; ++u) {
         const int c = cr + u * CPP;
         if (c < Kp) {
-            f32x4 o = {0.f, 0.f, 0.f, 0.f};
-            if (c < K && pv) {
-                const ChSrc t = tabA[c];
-                const ChanCoef k = tabK[c];
+            // the channel differs between lanes: branch-free transform (XfLin)
+            const bool live = c < K && pv;
+            const ChSrc t = tabA[c];
+            const XfLin l = xf_lin(t.xf, t.act, tabK[c]);
+            f32x4 o;
 #pragma unroll
-                for (int e = 0; e < 4; ++e) o[e] = ch_xform(t.xf, t.act, k, xv[u][e], HY ? yv[u][e] : xv[u][e]);
-            }
+            for (int e = 0; e < 4; ++e) o[e] = xf_lin_apply(l, xv[u][e], HY ? yv[u][e] : xv[u][e]);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = live ? o[e] : 0.f;
             *reinterpret_cast<f32x4*>(&Xs[c * XS + 4 * q]) = o;
         }
     }

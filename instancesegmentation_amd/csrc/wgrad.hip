@@ -357,6 +357,9 @@ __global__ __launch_bounds__(kThreads) void pwg_kernel(PwgArgs a) {
     char* const smem = reinterpret_cast<char*>(pwg_smem);
     ChSrc* const tabA = reinterpret_cast<ChSrc*>(smem);  // kThreads entries: BR dy rows, BC x rows
     ChanCoef* const tabK = reinterpret_cast<ChanCoef*>(smem + a.off_k);
+    // per row: (negative-side slope, 1 if BatchNorm backward) — the staging transform runs
+    // branch-free (rows of one wave can differ in transform kind and activation)
+    float2* const tabN = reinterpret_cast<float2*>(smem + a.off_k + kGMaxRows * (int)sizeof(ChanCoef));
     float* const S = reinterpret_cast<float*>(smem + a.off_x);  // [BR + BC][kGS]
 
     const int tid = threadIdx.x, lane = tid & 63;
@@ -383,13 +386,21 @@ __global__ __launch_bounds__(kThreads) void pwg_kernel(PwgArgs a) {
         e.p = is_dy ? ad.p : ax.p; e.y = is_dy ? ad.y : ax.y;
         e.ns = is_dy ? ad.ns : ax.ns; e.yns = is_dy ? ad.yns : ax.yns;
         e.xf = is_dy ? ad.xf : ax.xf; e.act = is_dy ? ad.act : ax.act;
+        ChanCoef kk;
         if (a.fast) {
             const ChanCoef kd = coef_finish(vd, cdy, ld), kx = coef_finish(vx, cx, lx);
-            if (tid < NR)
-                tabK[tid] = ChanCoef{is_dy ? kd.c0 : kx.c0, is_dy ? kd.c1 : kx.c1, is_dy ? kd.c2 : kx.c2,
-                                     is_dy ? kd.c3 : kx.c3};
-        } else if (tid < NR) {
-            tabK[tid] = is_dy ? vt_coef(a.dy, cdy) : vt_coef(a.x, cx);
+            kk = ChanCoef{is_dy ? kd.c0 : kx.c0, is_dy ? kd.c1 : kx.c1, is_dy ? kd.c2 : kx.c2,
+                          is_dy ? kd.c3 : kx.c3};
+        } else {
+            kk = tid < NR ? (is_dy ? vt_coef(a.dy, cdy) : vt_coef(a.x, cx)) : ChanCoef{0.f, 1.f, 0.f, 0.f};
+        }
+        if (tid < NR) {
+            const int xf = e.xf, act = e.act;
+            if (xf == ISG_XF_PLAIN) kk = ChanCoef{0.f, 1.f, 0.f, 0.f};
+            tabK[tid] = kk;
+            const float neg = (xf != ISG_XF_BN_FWD || act == ISG_ACT_NONE) ? 1.f
+                              : act == ISG_ACT_RELU ? 0.f : kk.c3;
+            tabN[tid] = float2{neg, xf == ISG_XF_BN_BWD ? 1.f : 0.f};
         }
     }
     __syncthreads();
@@ -423,12 +434,17 @@ __global__ __launch_bounds__(kThreads) void pwg_kernel(PwgArgs a) {
             const int j = cr + 16 * u;
             if (j < NR) {
                 const bool live = pv && (j < BR ? j < Rb : j - BR < Cb);
-                f32x4 o = {0.f, 0.f, 0.f, 0.f};
-                if (live) {
-                    const ChSrc t = tabA[j];
-                    const ChanCoef k = tabK[j];
+                const ChanCoef k = tabK[j];
+                const float2 nb = tabN[j];
+                f32x4 o;
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) o[e] = ch_xform(t.xf, t.act, k, v[u][e], HY ? yv[u][e] : v[u][e]);
+                for (int e = 0; e < 4; ++e) {
+                    // ch_xform's three forms, evaluated unconditionally and selected
+                    const float x = v[u][e], y = HY ? yv[u][e] : x;
+                    float zf = (x - k.c0) * k.c1 + k.c2;
+                    zf = zf > 0.f ? zf : zf * nb.x;
+                    const float zb = k.c0 * x + k.c1 * (y - k.c2) + k.c3;
+                    o[e] = live ? (nb.y != 0.f ? zb : zf) : 0.f;
                 }
                 *reinterpret_cast<f32x4*>(&S[j * kGS + 4 * q]) = o;
             }
@@ -574,7 +590,7 @@ int32_t pwg_try(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor
     if (env_tpb > a.tiles_per_block) a.tiles_per_block = env_tpb;
     gx = (a.ntiles + a.tiles_per_block - 1) / a.tiles_per_block;
     a.off_k = (kThreads * (int)sizeof(ChSrc) + 15) & ~15;
-    a.off_x = (a.off_k + kGMaxRows * (int)sizeof(ChanCoef) + 15) & ~15;
+    a.off_x = (a.off_k + kGMaxRows * (int)(sizeof(ChanCoef) + 2 * sizeof(float)) + 15) & ~15;
     const size_t lds = (size_t)a.off_x + (size_t)(br + bc) * kGS * sizeof(float);
     const int tpw = ((br / 16) * (bc / 16) + 3) / 4;
     const dim3 grid((unsigned)gx, (unsigned)gy);
