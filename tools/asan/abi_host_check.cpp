@@ -2,7 +2,7 @@
 // is not available on this pool, so the host half runs instrumented on the CPU).
 //
 // Built by tools/asan/build.sh from every libisg source compiled host-only
-// (--offload-host-only -fsanitize=address): no device code, no GPU needed. It drives the
+// (-Xarch_host -fsanitize=address, host half only): no device code, no GPU needed. It drives the
 // paths whose memory handling is host code — argument validation, the error plumbing,
 // the executor's record parsing and pointer fix-ups, the chunking of host item arrays —
 // with valid and malformed inputs; kernel launches fail cleanly without a device.

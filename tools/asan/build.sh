@@ -25,4 +25,4 @@ for s in "$ROOT"/instancesegmentation_amd/csrc/*.hip "$ROOT"/instancesegmentatio
   pids+=($!)
 done
 for p in "${pids[@]}"; do wait "$p"; done
-$HIPCC --offload-arch=gfx950 -fsanitize=address -g "${objs[@]}" -o "$OUT/abi_host_check"
+$HIPCC --offload-arch=gfx950 -Xarch_host -fsanitize=address -fno-gpu-sanitize -g "${objs[@]}" -o "$OUT/abi_host_check"

@@ -1,5 +1,5 @@
 #!/bin/bash
-# GPU session: parity tests -> bench (+ per-op table) -> rocprofv3 kernel-trace stats of the bench.
+# GPU session: parity tests -> smoke -> bench (+ per-op table) -> rocprofv3 kernel-trace stats of the bench.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export PYTHONDONTWRITEBYTECODE=1
@@ -9,6 +9,9 @@ STEPS=${STEPS:-20}
 timeout -k 10 600 python -u -m pytest tests -v -m gpu -x -rf --timeout 120 --timeout-method thread \
     > gpurun_out/tests_$TAG.log 2>&1 || { tail -30 gpurun_out/tests_$TAG.log; exit 1; }
 tail -3 gpurun_out/tests_$TAG.log
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 \
+    || { tail -30 gpurun_out/smoke_$TAG.log; exit 1; }
+tail -2 gpurun_out/smoke_$TAG.log
 timeout -k 10 400 python -u bench.py --steps $STEPS --warmup 5 --cpu-seconds 15 \
     --profile-ops gpurun_out/ops_$TAG.txt > gpurun_out/bench_$TAG.log 2>&1 \
     || { tail -30 gpurun_out/bench_$TAG.log; exit 1; }
