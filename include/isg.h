@@ -370,13 +370,18 @@ int32_t isg_kp_pool(const isg_kp_stem* a, isg_stream_t stream);
 
 /* bottle6_1 = ConvTranspose2d(16 -> 4, k8, s4, p2) followed by bottle6_2 = Conv2d(4 -> 1,
  * 3x3, p1) (no nonlinearity between them), with the 4-channel full-resolution
- * intermediate kept on chip (recomputed in the backward).
- *   fwd: out = logits [N,1,4Hi,4Wi]
+ * intermediate kept on chip (never recomputed in the backward).
+ *   fwd: out = logits [N,1,4Hi,4Wi]; when `ring` is non-NULL also the UN-cropped
+ *        intermediate (bias included) on the one-pixel ring just outside the 4Hi x 4Wi
+ *        image, per image [4 channels][ISG_HEAD_RING(Hi, Wi)]: row -1 (columns -1 .. 4Wi),
+ *        row 4Hi (same), column -1 (rows 0 .. 4Hi-1), column 4Wi (same). The backward
+ *        needs it (the 3x3's weight gradient border term).
  *   bwd: dx (sinks: STORE / ACCUM without statistics) = dL/dx; dw1/db1/dw2/db2 += the
  *        parameter gradients, added into replica (workgroup % nrep) of each (replica r at
- *        + r*rep_stride floats; NULL skips one). Replaces the unfused isg_convT_fwd +
- *        isg_conv_fwd (+ their dgrad / wgrad) pair, which round-trips the intermediate
- *        through HBM. */
+ *        + r*rep_stride floats; NULL skips one); `ring` as written by the forward
+ *        (required). Replaces the unfused isg_convT_fwd + isg_conv_fwd (+ their dgrad /
+ *        wgrad) pair, which round-trips the intermediate through HBM. */
+#define ISG_HEAD_RING(Hi, Wi) (2 * (4 * (int64_t)(Wi) + 2) + 2 * 4 * (int64_t)(Hi))
 typedef struct {
     isg_vtensor x;               /* [N,16,Hi,Wi] */
     const float* w1;             /* ConvTranspose2d weight [16][4][8][8] */
@@ -395,6 +400,8 @@ typedef struct {
     int64_t rep_stride;
     int32_t nrep;
     int32_t N, Hi, Wi;
+    int32_t pad_;
+    float* ring;                 /* [N][4][ISG_HEAD_RING(Hi, Wi)] (fwd: written if non-NULL; bwd: read) */
 } isg_mask_head;
 
 int32_t isg_mask_head_fwd(const isg_mask_head* a, isg_stream_t stream);

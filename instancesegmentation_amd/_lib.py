@@ -20,7 +20,7 @@ SINK_STORE, SINK_ACCUM, SINK_ACTBWD, SINK_NONE = 0, 1, 2, 3
 MAX_SEGS = 3
 LIST_CHUNK = 32
 STAT_REP = int(os.environ.get("ISG_STAT_REP", "4"))  # accumulator replicas (isg.h ISG_STAT_REP)
-ABI_VERSION = 7
+ABI_VERSION = 8
 WREP = 16         # ISG_WREP: weight-gradient replicas (isg.h)
 
 
@@ -99,7 +99,12 @@ class MaskHead(Structure):
                 ("b2", c_void_p), ("out", c_void_p), ("out_n_stride", c_int64), ("dout", c_void_p),
                 ("dout_n_stride", c_int64), ("dx", Sinks), ("dw1", c_void_p), ("db1", c_void_p),
                 ("dw2", c_void_p), ("db2", c_void_p), ("rep_stride", c_int64), ("nrep", c_int32),
-                ("N", c_int32), ("Hi", c_int32), ("Wi", c_int32)]
+                ("N", c_int32), ("Hi", c_int32), ("Wi", c_int32), ("pad_", c_int32), ("ring", c_void_p)]
+
+
+def head_ring_floats(Hi, Wi):
+    """Floats per image of the mask head's ring buffer (isg.h ISG_HEAD_RING x 4 channels)."""
+    return 4 * (2 * (4 * Wi + 2) + 2 * 4 * Hi)
 
 
 # executor records (api.cpp)

@@ -79,7 +79,7 @@ static bool partial_w(const isg_conv_geom* g) { return g->w_ci > 0 && g->w_ci !=
 extern "C" {
 
 const char* isg_last_error(void) { return g_last_error.c_str(); }
-int32_t isg_abi_version(void) { return 7; }
+int32_t isg_abi_version(void) { return 8; }
 int32_t isg_stat_replicas(void) { return ISG_STAT_REP; }
 
 int32_t isg_conv_fwd(const isg_conv_geom* g, const isg_vtensor* x, const float* w,
@@ -371,6 +371,14 @@ int32_t isg_exec_ms2(const void* ops, int32_t nops, void* const* table, isg_stre
         if (hipEventRecord(ev_fork, main_st) != hipSuccess || hipStreamWaitEvent(side, ev_fork, 0) != hipSuccess ||
             (spread && hipStreamWaitEvent(side2, ev_fork, 0) != hipSuccess))
             return isg_check_launch("exec: fork side stream");
+        if (!spread && forked2) {
+            // a non-weight-gradient batch (e.g. the replica fold / gradient finalisation at
+            // ISG_SIDE_CLOSE=1) runs on `side` only: order it after side2's outstanding
+            // weight-gradient accumulations, which it may read
+            forked2 = false;
+            if (hipEventRecord(ev_join2, side2) != hipSuccess || hipStreamWaitEvent(side, ev_join2, 0) != hipSuccess)
+                return isg_check_launch("exec: order side stream after side stream 2");
+        }
         forked = true;
         forked2 = forked2 || spread;
         alignas(16) char pb[8192];

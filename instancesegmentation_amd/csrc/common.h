@@ -28,6 +28,9 @@ ISG_DEV void gst(float* p, int64_t i, float v) { ((gfloat_p)p)[i] = v; }
 typedef const f32x4 __attribute__((address_space(1)))* gcf32x4_p;
 // 16-B global load of 4 consecutive floats at p[i..i+3] (p + i 16-B aligned)
 ISG_DEV f32x4 gld4(const float* p, int64_t i) { return *(gcf32x4_p)((gcfloat_p)p + i); }
+typedef f32x4 __attribute__((address_space(1)))* gf32x4_p;
+// 16-B global store of 4 consecutive floats at p[i..i+3] (p + i 16-B aligned)
+ISG_DEV void gst4(float* p, int64_t i, f32x4 v) { *(gf32x4_p)((gfloat_p)p + i) = v; }
 
 // ---- per-channel coefficient table (LDS) -------------------------------------
 // BN_FWD : v = act((x - c0) * c1 + c2)          c0=mean  c1=gamma*rstd  c2=beta, c3=slope

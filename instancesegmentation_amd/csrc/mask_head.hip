@@ -36,7 +36,6 @@ constexpr int GY = TY + 4, GX = TX + 4;   // intermediate-gradient region       
 constexpr int GJY = GY / 4, GJX = GX / 4; // per phase: 9 x 17
 constexpr int GPL = 16 * GJY * GJX;       // one channel, phase-split             2448
 constexpr int IPL = IY * IXS;             // one channel of the intermediate      2278
-constexpr int XPL = GPL > IPL ? GPL : IPL;
 constexpr int kW1 = kCi * kCm * 64;       // convT weights [16][4][8][8]
 
 // the input region of the tile whose top-left intermediate pixel is (Y0, X0), transformed,
@@ -90,9 +89,11 @@ ISG_DEV void cell_afrag(const float* w1s, float (&wf)[kCm][kCi]) {
 
 // The intermediate over the cells of the tile region (rows Y0 - 2 .. Y0 + 34, columns
 // X0 - 2 .. X0 + 66) into Ic[co][row][col] (origin (Y0 - 2, X0 - 2)), + bias, zero outside
-// the image.
+// the image. ring (this image's [4][ISG_HEAD_RING] block, NULL off the image border): the
+// un-cropped values on the one-pixel ring outside the image are stored there as well
+// (isg.h isg_mask_head); a ring pixel two tiles both cover gets the same bits from each.
 ISG_DEV void intermediate_mfma(const isg_mask_head& a, int Y0, int X0, const float (*Ts)[RY][RXS],
-                               const float (&wf)[kCm][kCi], float* Ic) {
+                               const float (&wf)[kCm][kCi], float* Ic, float* ring = nullptr) {
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int kq = lane >> 4, aa = kq >> 1, bb = kq & 1;
@@ -124,6 +125,20 @@ ISG_DEV void intermediate_mfma(const isg_mask_head& a, int Y0, int X0, const flo
             for (int i = 0; i < 4; ++i) v[i] = (rok && ox + i >= 0 && ox + i < OW) ? acc[co][i] + b1[co] : 0.f;
             if (cell < NCELL) *reinterpret_cast<f32x4*>(&Ic[co * IRP + (4 * cy + kq) * IRS + 4 * cx]) = v;
         }
+        if (ring && cell < NCELL) {
+            const int64_t rn = ISG_HEAD_RING(a.Hi, a.Wi);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int px = ox + i;
+                int idx = -1;
+                if ((oy == -1 || oy == OH) && px >= -1 && px <= OW) idx = (oy == OH ? OW + 2 : 0) + px + 1;
+                else if ((px == -1 || px == OW) && oy >= 0 && oy < OH) idx = 2 * (OW + 2) + (px == OW ? OH : 0) + oy;
+                if (idx >= 0) {
+#pragma unroll
+                    for (int co = 0; co < kCm; ++co) ring[co * rn + idx] = acc[co][i] + b1[co];
+                }
+            }
+        }
     }
 }
 
@@ -141,7 +156,9 @@ __global__ __launch_bounds__(kThreads, 2) void head_fwd_kernel(isg_mask_head a) 
     __syncthreads();
     load_input(a, coef, n, Y0, X0, Ts);
     __syncthreads();
-    intermediate_mfma(a, Y0, X0, Ts, wf, Ic);
+    const bool border = Y0 == 0 || Y0 + TY >= OH || X0 == 0 || X0 + TX >= OW;
+    intermediate_mfma(a, Y0, X0, Ts, wf, Ic,
+                      a.ring && border ? a.ring + (int64_t)n * kCm * ISG_HEAD_RING(a.Hi, a.Wi) : nullptr);
     __syncthreads();
     // 3x3 (4 -> 1): lane = column, 8 rows per thread (10 x 3 reads per channel); the
     // intermediate's origin is (Y0 - 2, X0 - 2)
@@ -186,8 +203,8 @@ ISG_DEV void stage_wd(const float* w1s, float* Wd) {
 constexpr int XPP = NCELL;        // phase-split intermediate gradient: one (co, r, s) plane
 constexpr int XCF = kCm * 16 * XPP > kCm * IRP ? kCm * 16 * XPP : kCm * IRP;
 
-__global__ __launch_bounds__(kThreads, 2) void head_bwd_kernel(isg_mask_head a, int ntx, int nty,
-                                                               int ntiles) {
+__global__ __launch_bounds__(kThreads, 2) void head_bwd_v1_kernel(isg_mask_head a, int ntx, int nty,
+                                                                  int ntiles) {
     __shared__ float Ts[kCi][RY][RXS];
     __shared__ float Ds[DY * DXS];
     __shared__ __attribute__((aligned(16))) float Xc[XCF];  // intermediate, then its gradient
@@ -377,6 +394,470 @@ __global__ __launch_bounds__(kThreads, 2) void head_bwd_kernel(isg_mask_head a, 
     }
 }
 
+// ---- backward, round 4 (head_bwd_kernel) ----------------------------------------------
+// Per 32 x 64 logit tile (8 x 16 own input pixels), on a persistent grid:
+//   staging  : dlogits rows Y0-3 .. Y0+34, cols X0-4 .. X0+67 and the input rows iy0-1 ..
+//              iy0+8, cols ix0-4 .. ix0+19 (transformed) -> LDS, 16-B loads;
+//   VALU     : the intermediate gradient dI = 3x3^T(dlogits) over the 9 x 17 cells
+//              (phase-split, as head_bwd_v1) and its per-channel sums (convT bias);
+//   MFMA     : dx = convT^T(dI) (A operands = the convT weights, kept in 64 registers per
+//              lane for the whole launch), dW1 = x (x) dI (this wave's output channel), and
+//              Z'[ci][d] = sum_i x[ci][i] * dl[4i + d - 2], d in [-1, 8]^2 (100 offsets);
+//   epilogue : dx staged in LDS and written with 16-B stores at the next tile's top.
+// The intermediate itself is never recomputed (head_bwd_v1 spent 640 of its 1664 MFMAs
+// per tile and ~40 % of its VALU on that, for the 3x3 weight gradient only): with
+// I_full = b1 + convT(x) WITHOUT the output crop,
+//     dW2[co][t] = sum_{p in image} dl[p] * I[co][p + t - 1]
+//                = b1[co] * sum(dl) + sum_{ci,k} W1[ci][co][k] * Z'[ci][k - t + 1] - C[co][t]
+// where C removes the (p, t) pairs whose intermediate pixel q = p + t - 1 lies just
+// outside the cropped image (q row -1 / OH, column -1 / OW: I there is zero in the
+// reference, segment.py:435-438 with padding 2). C needs I_full only on that one-pixel
+// ring, computed by the tiles on the image border. Z' and C are reduced once per
+// workgroup, then dW2 = W1 . Z' (1024 MACs per output) — the same sum as the reference's
+// sum_q I(q) dl(q - t'), reassociated.
+namespace hb {
+constexpr int IH = TY / 4, IW = TX / 4;     // own input pixels per tile: 8 x 16
+constexpr int TSH = IH + 2, TSW = IW + 8;   // staged input: rows iy0-1.., cols ix0-4.. (16-B quads)
+constexpr int TSP = TSH * TSW;              // one channel: 240
+constexpr int DSH = TY + 6, DSW = TX + 8;   // staged dlogits: rows Y0-3.., cols X0-4..
+constexpr int DNQ = DSW / 4;                // 18 quads per dlogits row
+constexpr int ZD = 10, ZN = 112;            // Z' offsets per axis (d = -1 .. 8); columns padded
+constexpr int RT = TX + 2, RL = TY + 2;     // ring lengths: top/bottom (cols X0-1 .. X0+TX), left/right
+constexpr int RING = 2 * RT + 2 * RL;       // per output channel
+constexpr int NDI = GY * CX;                // dI items: one intermediate row x one cell column (4 px)
+static_assert(IW == 16 && IH == 8, "lane mappings below assume 8 x 16 own input pixels");
+static_assert(TX == 64, "the ring correction maps one lane per tile column");
+}  // namespace hb
+
+// the dx of one finished tile (LDS [16 ci][IH][IW]) through the caller's STORE / ACCUM sinks
+template <bool VX>
+ISG_DEV void hb_store_dx(const isg_mask_head& a, const SinkRow* sk, const float* dxs, int n, int iy0,
+                         int ix0) {
+    using namespace hb;
+    if (VX) {
+        for (int i = threadIdx.x; i < kCi * IH * IW / 4; i += kThreads) {
+            const int ci = i >> 5, r = (i >> 2) & 7, qd = i & 3;
+            const int iy = iy0 + r, ix = ix0 + 4 * qd;
+            const SinkRow& q = sk[ci];
+            if (iy >= a.Hi || ix >= a.Wi || (q.mode != ISG_SINK_STORE && q.mode != ISG_SINK_ACCUM)) continue;
+            const f32x4 v = *reinterpret_cast<const f32x4*>(&dxs[(ci * IH + r) * IW + 4 * qd]);
+            const int64_t off = (int64_t)n * q.ns + (int64_t)iy * a.Wi + ix;
+            gst4(q.p, off, q.mode == ISG_SINK_ACCUM ? gld4(q.p, off) + v : v);
+        }
+    } else {
+        for (int i = threadIdx.x; i < kCi * IH * IW; i += kThreads) {
+            const int ci = i >> 7, r = (i >> 4) & 7, c = i & 15;
+            const int iy = iy0 + r, ix = ix0 + c;
+            const SinkRow& q = sk[ci];
+            if (iy >= a.Hi || ix >= a.Wi || (q.mode != ISG_SINK_STORE && q.mode != ISG_SINK_ACCUM)) continue;
+            const float v = dxs[(ci * IH + r) * IW + c];
+            const int64_t off = (int64_t)n * q.ns + (int64_t)iy * a.Wi + ix;
+            gst(q.p, off, q.mode == ISG_SINK_ACCUM ? gld(q.p, off) + v : v);
+        }
+    }
+}
+
+// Staging of one tile into registers (16-B loads, issued together so their latencies
+// overlap) and from registers into LDS. Lane items: 3 dlogits quads and 4 input quads
+// (channel, row, quad) per thread; the input transform is the branch-free per-lane form
+// (stage.h XfLin: PLAIN / BN_FWD + activation).
+struct HbPrefetch {
+    f32x4 dl[3], x[4];
+};
+
+ISG_DEV void hb_issue(const isg_mask_head& a, const VtLite& vl, int n, int Y0, int X0, HbPrefetch& f) {
+    using namespace hb;
+    const int OH = 4 * a.Hi, OW = 4 * a.Wi, iy0 = Y0 / 4, ix0 = X0 / 4;
+    const float* dout = a.dout + (int64_t)n * a.dout_n_stride;
+    const int hw = a.Hi * a.Wi;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const int i = threadIdx.x + k * kThreads;
+        const int r = i / DNQ, qd = i - r * DNQ;
+        const int oy = Y0 - 3 + r, ox = X0 - 4 + 4 * qd;
+        f.dl[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (i < DSH * DNQ && oy >= 0 && oy < OH && ox >= 0 && ox < OW)
+            f.dl[k] = gld4(dout, (int64_t)oy * OW + ox);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        // opaque: recompute the per-lane channel addressing per tile instead of keeping 4
+        // hoisted 64-bit pointers live across the whole tile loop (they spilled)
+        const int i = opaque(threadIdx.x + k * kThreads);
+        const int ci = i / (TSH * TSW / 4), rem = i - ci * (TSH * TSW / 4);
+        const int r = rem / (TSW / 4), qd = rem - r * (TSW / 4);
+        const int iy = iy0 - 1 + r, ix = ix0 - 4 + 4 * qd;
+        f.x[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (i < kCi * TSH * TSW / 4 && iy >= 0 && iy < a.Hi && ix >= 0 && ix < a.Wi) {
+            const float* p = ci >= vl.c2 ? vl.p2 + (int64_t)(ci - vl.c2) * hw + (int64_t)n * vl.ns2
+                           : ci >= vl.c1 ? vl.p1 + (int64_t)(ci - vl.c1) * hw + (int64_t)n * vl.ns1
+                                         : vl.p0 + (int64_t)ci * hw + (int64_t)n * vl.ns0;
+            f.x[k] = gld4(p, (int64_t)iy * a.Wi + ix);
+        }
+    }
+}
+
+ISG_DEV void hb_commit(const HbPrefetch& f, const XfLin* xl, int Hi, int Wi, int iy0, int ix0,
+                       float* Ts, float* Ds, float& db2) {
+    using namespace hb;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const int i = threadIdx.x + k * kThreads;
+        if (i < DSH * DNQ) {
+            const int r = i / DNQ, qd = i - r * DNQ;
+            *reinterpret_cast<f32x4*>(&Ds[r * DSW + 4 * qd]) = f.dl[k];
+            if (r >= 3 && r < 3 + TY && qd >= 1 && qd <= TX / 4)
+                db2 += (f.dl[k][0] + f.dl[k][1]) + (f.dl[k][2] + f.dl[k][3]);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int i = threadIdx.x + k * kThreads;
+        if (i < kCi * TSH * TSW / 4) {
+            const int ci = i / (TSH * TSW / 4), rem = i - ci * (TSH * TSW / 4);
+            const int r = rem / (TSW / 4), qd = rem - r * (TSW / 4);
+            const int iy = iy0 - 1 + r, ix = ix0 - 4 + 4 * qd;
+            // outside the image the convT input is zero padding, not transform(0)
+            const bool in = iy >= 0 && iy < Hi && ix >= 0 && ix < Wi;
+            const XfLin l = xl[ci];
+            f32x4 v;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = in ? xf_lin_apply(l, f.x[k][e], 0.f) : 0.f;
+            *reinterpret_cast<f32x4*>(&Ts[ci * TSP + 4 * rem]) = v;
+        }
+    }
+}
+
+template <bool VX>
+__global__ __launch_bounds__(kThreads, 2) void head_bwd_kernel(isg_mask_head a, int ntx, int nty,
+                                                               int ntiles) {
+    using namespace hb;
+    __shared__ __attribute__((aligned(16))) float Ts[kCi * TSP];
+    __shared__ __attribute__((aligned(16))) float Ds[DSH * DSW];
+    __shared__ __attribute__((aligned(16))) float Xc[kCm * 16 * NCELL];  // dI, phase-split
+    __shared__ __attribute__((aligned(16))) float dxs[kCi * IH * IW];
+    __shared__ float ring[kCm * RING];
+    __shared__ __attribute__((aligned(16))) float w2s[kCm * 9];
+    __shared__ ChanCoef coef[kCi];
+    __shared__ XfLin xl[kCi];
+    __shared__ SinkRow sk[kCi];
+    __shared__ float Cs[kCm * 9];
+    __shared__ float red[kCm * 4 + 4];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(tid >> 6));
+    const int kq = lane >> 4, nl = lane & 15, aa = kq >> 1, bb = kq & 1;
+    const int OH = 4 * a.Hi, OW = 4 * a.Wi;
+    const int64_t hw = (int64_t)a.Hi * a.Wi;
+    const int64_t rn = ISG_HEAD_RING(a.Hi, a.Wi);
+    STAMP(0);
+    const VtLite vl = vt_lite(a.x);
+    HbPrefetch pf;
+    if (VX && (int)blockIdx.x < ntiles) {  // the first tile's loads overlap the setup below
+        const int t2 = blockIdx.x % (ntx * nty);
+        hb_issue(a, vl, blockIdx.x / (ntx * nty), (t2 / ntx) * TY, (t2 % ntx) * TX, pf);
+    }
+    load_vt_coefs(a.x, coef, tid, kThreads);
+    copy_w1(a.w1, Xc);
+    if (tid < kCi) {
+        SinkRow q = {};
+        q.mode = ISG_SINK_NONE;
+        if (a.dx.nsink > 0) q = sink_row(a.dx, tid, hw);
+        sk[tid] = q;
+    }
+    if (tid < kCm * 9) {
+        Cs[tid] = 0.f;
+        w2s[tid] = a.w2[tid];
+    }
+    __syncthreads();
+    if (tid < kCi) {
+        const int c1 = vl.c1, c2 = vl.c2;
+        const int xf = tid >= c2 ? vl.xf2 : tid >= c1 ? vl.xf1 : vl.xf0;
+        const int act = tid >= c2 ? vl.act2 : tid >= c1 ? vl.act1 : vl.act0;
+        xl[tid] = xf_lin(xf, act, coef[tid]);
+    }
+    // dx GEMM A operands, constant for the launch: A[m = ci][k = (a, b)] of plane o = (co, r, s)
+    // = W1[ci][co][r + 4(1 - a)][s + 4(1 - b)]
+    float wdA[64];
+#pragma unroll
+    for (int o = 0; o < 64; ++o) {
+        const int co = o >> 4, r = (o >> 2) & 3, s = o & 3;
+        wdA[o] = Xc[((nl * kCm + co) * 8 + r + 4 * (1 - aa)) * 8 + s + 4 * (1 - bb)];
+    }
+    // Z' N-tiles of this wave: 2 wave, 2 wave + 1 (of 7); column d = (dy, dx) of this lane
+    // as a Ds offset
+    int zoff[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const int j = 16 * (2 * wave + t) + nl;
+        zoff[t] = j < ZD * ZD ? (j / ZD - 1) * DSW + (j % ZD - 1) : 0;
+    }
+    const bool z2 = 2 * wave + 1 < ZN / 16;  // wave 3 has one N-tile
+    // dW1 N-tiles of this wave's output channel co = wave: column (ky, kx) = 16t + nl
+    int w1off[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const int ky = 2 * t + (nl >> 3), kx = nl & 7;
+        w1off[t] = ((wave * 4 + (ky & 3)) * 4 + (kx & 3)) * NCELL + (ky >> 2) * CX + (kx >> 2);
+    }
+    f32x4 dw1[4], zp[2];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) dw1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    zp[0] = zp[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float db1[kCm] = {0.f, 0.f, 0.f, 0.f}, db2 = 0.f;
+    int pn = -1, piy0 = 0, pix0 = 0;  // the tile whose dx sits in dxs
+    STAMP(1);
+
+    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int n = tile / (ntx * nty), t2 = tile - n * ntx * nty;
+        const int Y0 = (t2 / ntx) * TY, X0 = (t2 % ntx) * TX;
+        const int iy0 = Y0 / 4, ix0 = X0 / 4;
+        const bool top = Y0 == 0, bot = Y0 + TY >= OH, lft = X0 == 0, rgt = X0 + TX >= OW;
+        const bool border = top || bot || lft || rgt;
+        __syncthreads();  // the previous tile's LDS reads are done (tables and wdA ready)
+        if (pn >= 0) hb_store_dx<VX>(a, sk, dxs, pn, piy0, pix0);
+        // ---- staging: dlogits (+ own sum), input region, the ring (border tiles)
+        if (VX) {
+            hb_commit(pf, xl, a.Hi, a.Wi, iy0, ix0, Ts, Ds, db2);
+        } else {
+            const float* dout = a.dout + (int64_t)n * a.dout_n_stride;
+            for (int i = tid; i < DSH * DSW; i += kThreads) {
+                const int r = i / DSW, c = i - r * DSW;
+                const int oy = Y0 - 3 + r, ox = X0 - 4 + c;
+                float v = 0.f;
+                if (oy >= 0 && oy < OH && ox >= 0 && ox < OW) v = dout[(int64_t)oy * OW + ox];
+                Ds[i] = v;
+                if (r >= 3 && r < 3 + TY && c >= 4 && c < 4 + TX) db2 += v;
+            }
+            for (int i = tid; i < kCi * TSP; i += kThreads) {
+                const int ci = i / TSP, r = (i / TSW) % TSH, c = i % TSW;
+                const int iy = iy0 - 1 + r, ix = ix0 - 4 + c;
+                float v = 0.f;
+                if (iy >= 0 && iy < a.Hi && ix >= 0 && ix < a.Wi)
+                    v = vt_load(a.x, coef, n, ci, hw, (int64_t)iy * a.Wi + ix);
+                Ts[i] = v;
+            }
+        }
+        if (border) {
+            const float* rg = a.ring + (int64_t)n * kCm * rn;
+            for (int it = tid; it < kCm * RING; it += kThreads) {
+                const int co = it / RING, e = it - co * RING;
+                float v = 0.f;
+                if (e < 2 * RT) {  // top / bottom rows, corners included
+                    const bool b = e >= RT;
+                    const int qx = X0 - 1 + (e - (b ? RT : 0));
+                    if ((b ? bot : top) && qx <= OW) v = rg[co * rn + (b ? OW + 2 : 0) + qx + 1];
+                } else {  // left / right columns, rows inside the image only
+                    const bool rr = e >= 2 * RT + RL;
+                    const int qy = Y0 - 1 + (e - 2 * RT - (rr ? RL : 0));
+                    if ((rr ? rgt : lft) && qy >= 0 && qy < OH) v = rg[co * rn + 2 * (OW + 2) + (rr ? OH : 0) + qy];
+                }
+                ring[it] = v;
+            }
+        }
+        __syncthreads();
+        if (pn < 0) STAMP(2);
+        // ---- the next tile's loads, in flight during this tile's compute
+        if (VX && tile + (int)gridDim.x < ntiles) {
+            const int nt = tile + gridDim.x, nn = nt / (ntx * nty), nt2 = nt - nn * ntx * nty;
+            hb_issue(a, vl, nn, (nt2 / ntx) * TY, (nt2 % ntx) * TX, pf);
+        }
+        // ---- intermediate gradient over the cell region (origin (Y0 - 2, X0 - 2)):
+        //      dI[co][q] = sum_{ty,tx} w2[co][ty][tx] dl[q + 1 - ty][q + 1 - tx], zero outside
+        //      the image, stored phase-split Xc[((co * 4 + r) * 4 + s) * NCELL + cy * CX + cx]
+        for (int it = tid; it < NDI; it += kThreads) {
+            const int ql = it / CX, cx = it - ql * CX;
+            const int cy = ql >> 2, r = ql & 3;
+            const int qy = Y0 - 2 + ql;
+            float d[3][8];  // Ds rows ql .. ql + 2, columns 4cx .. 4cx + 7
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const f32x4 lo = *reinterpret_cast<const f32x4*>(&Ds[(ql + k) * DSW + 4 * cx]);
+                const f32x4 hi = *reinterpret_cast<const f32x4*>(&Ds[(ql + k) * DSW + 4 * cx + 4]);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    d[k][e] = lo[e];
+                    d[k][4 + e] = hi[e];
+                }
+            }
+            const bool rin = qy >= 0 && qy < OH;
+            const bool rown = ql >= 2 && ql < 2 + TY;
+#pragma unroll
+            for (int co = 0; co < kCm; ++co) {
+                float w[9];
+#pragma unroll
+                for (int k = 0; k < 9; ++k) w[k] = w2s[co * 9 + k];
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    const int qxl = 4 * cx + s, qx = X0 - 2 + qxl;
+                    const bool in = rin && qx >= 0 && qx < OW;
+                    const bool own = rown && qxl >= 2 && qxl < 2 + TX;
+                    float v = 0.f;
+#pragma unroll
+                    for (int ty = 0; ty < 3; ++ty)
+#pragma unroll
+                        for (int tx = 0; tx < 3; ++tx) v += w[ty * 3 + tx] * d[2 - ty][s + 3 - tx];
+                    v = in ? v : 0.f;
+                    db1[co] += own ? v : 0.f;
+                    Xc[((co * 4 + r) * 4 + s) * NCELL + cy * CX + cx] = v;
+                }
+            }
+        }
+        __syncthreads();
+        if (pn < 0) STAMP(3);
+        // ---- border tiles: C[co][t] += dl[p] * I_full[p + t - 1] over the pairs whose
+        //      intermediate pixel is outside the image (wave = co, lane = tile column / row)
+        if (border) {
+            const int co = wave;
+            const float* rg = ring + co * RING;
+            float c[9];
+#pragma unroll
+            for (int t = 0; t < 9; ++t) c[t] = 0.f;
+            if (top && X0 + lane < OW) {
+                const float dv = Ds[3 * DSW + lane + 4];
+#pragma unroll
+                for (int tx = 0; tx < 3; ++tx) c[tx] += dv * rg[lane + tx];
+            }
+            if (bot && X0 + lane < OW) {
+                const float dv = Ds[(OH - 1 - Y0 + 3) * DSW + lane + 4];
+#pragma unroll
+                for (int tx = 0; tx < 3; ++tx) c[6 + tx] += dv * rg[RT + lane + tx];
+            }
+            if (lane < TY && Y0 + lane < OH) {
+                if (lft) {
+                    const float dv = Ds[(lane + 3) * DSW + 4];
+#pragma unroll
+                    for (int ty = 0; ty < 3; ++ty) c[ty * 3] += dv * rg[2 * RT + lane + ty];
+                }
+                if (rgt) {
+                    const float dv = Ds[(lane + 3) * DSW + OW - 1 - X0 + 4];
+#pragma unroll
+                    for (int ty = 0; ty < 3; ++ty) c[ty * 3 + 2] += dv * rg[2 * RT + RL + lane + ty];
+                }
+            }
+#pragma unroll
+            for (int t = 0; t < 9; ++t) {
+                const float v = wave_sum(c[t]);
+                if (lane == 0) Cs[co * 9 + t] += v;
+            }
+        }
+        // ---- input gradient: rows ly = wave, wave + 4 of the tile; D lane: ci = 4kq + i, px nl
+        {
+            const int ly0 = wave, ly1 = wave + 4;
+            const float* b0 = Xc + (ly0 + 1 - aa) * CX + (nl + 1 - bb);
+            const float* b1p = Xc + (ly1 + 1 - aa) * CX + (nl + 1 - bb);
+            f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int o = 0; o < 64; ++o) {
+                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(wdA[o], b0[o * NCELL], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(wdA[o], b1p[o * NCELL], acc1, 0, 0, 0);
+                // bound how far the scheduler hoists the B reads (each a live register)
+                if ((o & 15) == 15) asm volatile("" ::: "memory");
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                dxs[((4 * kq + i) * IH + ly0) * IW + nl] = acc0[i];
+                dxs[((4 * kq + i) * IH + ly1) * IW + nl] = acc1[i];
+            }
+        }
+        // ---- convT weight gradient of output channel co = wave and this wave's Z' N-tiles:
+        //      K = the 128 own pixels, 4 per step (A = the input, shared by both GEMMs)
+        {
+            const float* ap = Ts + nl * TSP + TSW + 4 + kq;
+            const float* zb = Ds + DSW + 4 * kq + 2;
+#pragma unroll
+            for (int st = 0; st < IH * IW / 4; ++st) {
+                const int ly = st >> 2, lx4 = 4 * (st & 3);
+                const float av = ap[ly * TSW + lx4];
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+                    dw1[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, Xc[w1off[t] + ly * CX + lx4 + kq],
+                                                                  dw1[t], 0, 0, 0);
+                // Z' B[px][d] = dl[4 px + d - 2]: Ds row 4 ly + 1 + dy, column 4 lx + 2 + dx
+                const float* zr = zb + 4 * ly * DSW + 4 * lx4;
+                zp[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, zr[zoff[0]], zp[0], 0, 0, 0);
+                if (z2) zp[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, zr[zoff[1]], zp[1], 0, 0, 0);
+                if ((st & 3) == 3) asm volatile("" ::: "memory");
+            }
+        }
+        if (pn < 0) STAMP(4);
+        pn = n; piy0 = iy0; pix0 = ix0;
+    }
+    __syncthreads();
+    STAMP(5);
+    if (pn >= 0) hb_store_dx<VX>(a, sk, dxs, pn, piy0, pix0);
+    // ---- once per workgroup: dW1, Z' -> dW2, bias gradients, into replica rep
+    const int rep = blockIdx.x % a.nrep;
+    const int64_t ro = (int64_t)rep * a.rep_stride;
+    if (a.dw1) {
+        float* d = a.dw1 + ro;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                atomicAdd(&d[(4 * kq + i) * (kCm * 64) + wave * 64 + t * 16 + nl], dw1[t][i]);
+    }
+    float* Zs = Xc;                      // [16 ci][ZN]
+    float* W1s = Xc + kCi * ZN;          // [16][4][8][8]
+    for (int e = tid; e < kW1 / 4; e += kThreads)
+        reinterpret_cast<f32x4*>(W1s)[e] = gld4(a.w1, 4 * e);
+    float v1[kCm];
+#pragma unroll
+    for (int co = 0; co < kCm; ++co) v1[co] = wave_sum(db1[co]);
+    const float v2 = wave_sum(db2);
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+        if (t == 0 || z2)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) Zs[(4 * kq + i) * ZN + 16 * (2 * wave + t) + nl] = zp[t][i];
+    if (lane == 0) {
+#pragma unroll
+        for (int co = 0; co < kCm; ++co) red[co * 4 + wave] = v1[co];
+        red[kCm * 4 + wave] = v2;
+    }
+    __syncthreads();
+    STAMP(6);
+    const float sdl = (red[kCm * 4] + red[kCm * 4 + 1]) + (red[kCm * 4 + 2] + red[kCm * 4 + 3]);
+    // dW2[co][t] = sum_{ci, ky, kx} W1[ci][co][ky][kx] Z'[ci][(ky - ty + 1, kx - tx + 1)]:
+    // wave = co, lane = (ci, two kernel rows); the 9 taps summed over the wave
+    {
+        const int co = wave, ci = lane >> 2, kyg = lane & 3;
+        const float* w = W1s + (ci * kCm + co) * 64 + 2 * kyg * 8;
+        const float* z = Zs + ci * ZN + 2 * kyg * ZD;  // rows 2kyg .. 2kyg + 3 of the 10 x 10 offsets
+        float zr[4][ZD];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int c = 0; c < ZD; ++c) zr[r][c] = z[r * ZD + c];
+        float c9[9];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) c9[t] = 0.f;
+#pragma unroll
+        for (int ky = 0; ky < 2; ++ky)
+#pragma unroll
+            for (int kx = 0; kx < 8; ++kx) {
+                const float wv = w[ky * 8 + kx];
+#pragma unroll
+                for (int ty = 0; ty < 3; ++ty)
+#pragma unroll
+                    for (int tx = 0; tx < 3; ++tx) c9[ty * 3 + tx] += wv * zr[ky + 2 - ty][kx + 2 - tx];
+            }
+        const float b1 = a.b1 ? a.b1[co] : 0.f;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            const float v = wave_sum(c9[t]);
+            if (lane == 0 && a.dw2) atomicAdd(a.dw2 + ro + co * 9 + t, v + b1 * sdl - Cs[co * 9 + t]);
+        }
+        if (lane == 1 && a.db1) {
+            const float s = (red[co * 4] + red[co * 4 + 1]) + (red[co * 4 + 2] + red[co * 4 + 3]);
+            atomicAdd(a.db1 + ro + co, s);
+        }
+        if (tid == 2 && a.db2) atomicAdd(a.db2 + ro, sdl);
+    }
+    __syncthreads();
+    STAMP(7);
+}
+
 int32_t check_head(const isg_mask_head* a, bool bwd) {
     if (!a || !a->w1 || !a->w2 || a->N < 1 || a->Hi < 1 || a->Wi < 1)
         return isg_set_error(ISG_ERR_INVALID, "mask head: NULL weights or bad size");
@@ -397,10 +878,30 @@ int32_t check_head(const isg_mask_head* a, bool bwd) {
     }
     if (a->nrep < 1 || (a->nrep > 1 && a->rep_stride <= 0))
         return isg_set_error(ISG_ERR_INVALID, "mask head bwd: bad replicas");
+    if (!a->ring)
+        return isg_set_error(ISG_ERR_INVALID, "mask head bwd: NULL ring (the forward writes it)");
     return ISG_OK;
 }
 
+// 16-B staging and dx stores: the input width a multiple of 4 and every base pointer and
+// image stride 16-B aligned (the network's H, W = 0 mod 16 always give that)
+bool head_bwd_vec(const isg_mask_head* a) {
+    auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    if (a->Wi % 4 || !al(a->dout) || a->dout_n_stride % 4) return false;
+    for (int s = 0; s < a->x.nseg; ++s) {
+        const isg_vseg& g = a->x.s[s];
+        if (!al(g.p) || g.n_stride % 4 || g.xform == ISG_XF_BN_BWD) return false;
+    }
+    for (int s = 0; s < a->dx.nsink; ++s) {
+        const isg_sink& k = a->dx.s[s];
+        if (k.mode != ISG_SINK_NONE && (!al(k.p) || k.n_stride % 4)) return false;
+    }
+    return true;
+}
+
 }  // namespace
+
+ISG_STAMP_ACCESSOR(isg_dbg_stamps_head)
 
 extern "C" int32_t isg_mask_head_fwd(const isg_mask_head* a, isg_stream_t st) {
     if (int32_t e = check_head(a, false)) return e;
@@ -417,6 +918,14 @@ extern "C" int32_t isg_mask_head_bwd(const isg_mask_head* a, isg_stream_t st) {
     const int ntiles = ntx * nty * a->N;
     static const int env = getenv("ISG_HEAD_BWD_GRID") ? atoi(getenv("ISG_HEAD_BWD_GRID")) : 0;
     const int grid = std::min(ntiles, env > 0 ? env : 512);  // 2 workgroups per CU
-    hipLaunchKernelGGL(head_bwd_kernel, dim3(grid), dim3(kThreads), 0, st, *a, ntx, nty, ntiles);
+    static const bool v1 = getenv("ISG_HEAD_BWD_V1") && atoi(getenv("ISG_HEAD_BWD_V1"));
+    if (v1) {
+        hipLaunchKernelGGL(head_bwd_v1_kernel, dim3(grid), dim3(kThreads), 0, st, *a, ntx, nty, ntiles);
+        return isg_check_launch("head_bwd_v1_kernel");
+    }
+    if (head_bwd_vec(a))
+        hipLaunchKernelGGL(head_bwd_kernel<true>, dim3(grid), dim3(kThreads), 0, st, *a, ntx, nty, ntiles);
+    else
+        hipLaunchKernelGGL(head_bwd_kernel<false>, dim3(grid), dim3(kThreads), 0, st, *a, ntx, nty, ntiles);
     return isg_check_launch("head_bwd_kernel");
 }

@@ -703,7 +703,7 @@ struct ThinPwArgs {
     int64_t Q;  // pixel quads
 };
 
-typedef f32x4 __attribute__((address_space(1)))* gf32x4_p;
+// gf32x4_p: common.h
 
 ISG_DEV void sink_row_apply4(const SinkRow& q, int n, int64_t pix, f32x4 v, float& s0, float& s1,
                              float& s2) {

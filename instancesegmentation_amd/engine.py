@@ -427,7 +427,11 @@ class Graph:
                 and x.C == 16 and all(not s.virtual for s in x.segs)):
             return None
         out = self.act_buf(1, 4 * x.H, 4 * x.W, name)
-        op = HeadOp(self, ct, conv, x, out)
+        # the un-cropped intermediate on the ring outside the image, written by the forward
+        # for the backward's 3x3 weight-gradient border term (isg.h isg_mask_head)
+        ring = self.act_buf(1, 1, L.head_ring_floats(x.H, x.W), name + ".ring") \
+            if self.need_grad else None
+        op = HeadOp(self, ct, conv, x, out, ring)
         self.ops.append(op)
         return Value([Val(out, 0, 1, grad=self.need_grad)])
 
@@ -827,14 +831,16 @@ class ConvOp:
 class HeadOp:
     """Fused mask head (Graph.head): one forward and one backward record."""
 
-    def __init__(self, g, ct, conv, x, out):
-        self.g, self.ct, self.conv, self.x, self.out = g, ct, conv, x, out
+    def __init__(self, g, ct, conv, x, out, ring=None):
+        self.g, self.ct, self.conv, self.x, self.out, self.ring = g, ct, conv, x, out, ring
 
     def _spec(self):
         g = self.g
         segs = [fwd_seg(v, g.train) for v in self.x.segs]
         s = {"x": vtensor(segs, g.N, self.x.H, self.x.W), "w1": g.tptr(self.ct, "weight"),
              "w2": g.tptr(self.conv, "weight"), "N": g.N, "Hi": self.x.H, "Wi": self.x.W}
+        if self.ring is not None:
+            s["ring"] = self.ring.ptr()
         if self.ct.bias is not None:
             s["b1"] = g.tptr(self.ct, "bias")
         if self.conv.bias is not None:
@@ -876,9 +882,11 @@ class HeadOp:
         if self.conv.bias is not None:
             s["db2"] = g.wrep_ptr(self.conv, "bias")
         fl, nb = self._cost()
-        # input gradient + both weight gradients (+ the intermediate recomputed)
+        # algorithmic: input gradient + both weight gradients = 2x the forward (SURVEY
+        # §8d). The kernel also recomputes the intermediate (another 1x the forward) —
+        # implementation overhead, not counted as work in the roofline.
         ops.add(Record(L.OP_HEAD_BWD, L.MaskHead, s, label="d_" + self.out.name,
-                       flops=3 * fl, nbytes=nb + 4 * 16 * g.N * self.x.H * self.x.W))
+                       flops=2 * fl, nbytes=nb + 4 * 16 * g.N * self.x.H * self.x.W))
 
 
 class KpPoolOp:

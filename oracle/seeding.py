@@ -19,8 +19,15 @@ def _rng(seed, salt=0):
     return np.random.Generator(np.random.PCG64([seed, salt]))
 
 
-def synth_params(shapes, seed):
+def synth_params(shapes, seed, head_scale=1.0):
     """shapes: ordered list of (key, shape). Returns {key: float64 ndarray}.
+
+    head_scale multiplies the last conv's weight (`bottle6_2.weight`, segment.py:438).
+    The CPU-fp32 reference's own logits error scales linearly with it (it is the upstream
+    fp32 noise carried through that conv): at 1.0 (|logit| 6-16) the CPU-fp32 path is
+    1.1-2.7e-4 from fp64 at every size tried, at 0.35 (|logit| 2-6) 3.8-5.4e-5 — the
+    well-conditioned regime where `north_star`'s "fp32 logits within 1e-4 of the CPU path"
+    is a meaningful assertion rather than a measure of the CPU path's own rounding.
 
     Distributions are chosen to exercise every code path (non-zero biases,
     non-trivial BN affine, PReLU slopes != 0.25) while staying in the
@@ -46,6 +53,8 @@ def synth_params(shapes, seed):
             out[key] = r.uniform(-0.1, 0.1, shape)
         else:
             raise KeyError(key)
+    if head_scale != 1.0 and "bottle6_2.weight" in out:
+        out["bottle6_2.weight"] = out["bottle6_2.weight"] * head_scale
     return out
 
 

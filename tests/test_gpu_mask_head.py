@@ -48,14 +48,25 @@ def test_mask_head_fwd_bwd(N, Hi, Wi):
     # two input segments (channels 0-9, 10-15) exercise the vtensor segment split
     xa, xb = d["x"][:, :10].contiguous(), d["x"][:, 10:].contiguous()
     seg = lambda t, C: {"p": t.data_ptr(), "n_stride": C * Hi * Wi, "C": C, "xform": L.XF_PLAIN}
+    ring = torch.full((N, L.head_ring_floats(Hi, Wi)), float("nan"), device=DEV)
     base = {"x": {"s": [seg(xa, 10), seg(xb, 6)], "nseg": 2, "N": N, "H": Hi, "W": Wi},
             "w1": d["w1"].data_ptr(), "b1": d["b1"].data_ptr(), "w2": d["w2"].data_ptr(),
-            "b2": d["b2"].data_ptr(), "N": N, "Hi": Hi, "Wi": Wi}
+            "b2": d["b2"].data_ptr(), "N": N, "Hi": Hi, "Wi": Wi, "ring": ring.data_ptr()}
     a = struct(L.MaskHead, dict(base, out=out.data_ptr(), out_n_stride=OH * OW))
     call("isg_mask_head_fwd", a, L.stream_ptr())
     e = _rel(out, ref_y)
     print(f"{N}x16x{Hi}x{Wi}: logits rel err {e:.2e}")
     assert e < 2e-6
+    # the ring: the un-cropped intermediate one pixel outside the image (isg.h)
+    full = F.conv_transpose2d(x.double(), w1.double(), b1.double(), stride=4)  # no crop: p = -2
+    OHf = full.shape[2]
+    rg = ring.view(N, 4, -1).double().cpu()
+    exp = torch.cat([full[:, :, 1, 1:OW + 3], full[:, :, OH + 2, 1:OW + 3],
+                     full[:, :, 2:OH + 2, 1], full[:, :, 2:OH + 2, OW + 2]], 2)
+    assert OHf == OH + 4 and rg.shape == exp.shape
+    er = (rg - exp).abs().max().item() / max(exp.abs().max().item(), 1e-12)
+    print(f"ring rel err {er:.2e}")
+    assert er < 2e-6
     # backward: dx of channels 0-9 STOREd, 10-15 ACCUMulated onto a preset value
     dxa = torch.full((N, 10, Hi, Wi), 5.0, device=DEV)
     pre = torch.randn(N, 6, Hi, Wi, device=DEV)

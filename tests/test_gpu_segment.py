@@ -11,7 +11,7 @@ import pytest
 import torch
 
 from instancesegmentation_amd.model.segment import Segment
-from tests.golden_util import SEGMENT_FIXTURES, SegmentFixture
+from tests.golden_util import SEGMENT_FIXTURES, WELL_CONDITIONED_FIXTURES, SegmentFixture
 from tests.grad_check import check_grads, check_logits, reference_grads
 
 pytestmark = pytest.mark.gpu
@@ -45,7 +45,8 @@ def test_segment_train_step_matches_reference(name):
     fx = SegmentFixture(name)
     m = load_model(fx)
     logits, loss = run_step(m, fx)
-    check_logits(logits.cpu(), fx.z["logits64"], fx.z["logits32"], name)
+    check_logits(logits.cpu(), fx.z["logits64"], fx.z["logits32"], name,
+                 strict=name in WELL_CONDITIONED_FIXTURES)
     assert abs(loss.item() - float(fx.z["loss64"])) < 1e-5
     got = {k: p.grad for k, p in m.named_parameters()}
     ref, flo = reference_grads(fx.params, fx.x, fx.mask, got, fixture=fx, tag=name)

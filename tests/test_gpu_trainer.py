@@ -188,3 +188,39 @@ def test_loaded_adam_hyperparameters_reach_the_captured_step():
     tr.step(xs, y)
     torch.cuda.synchronize()
     assert not torch.equal(tr.flat, before)
+
+
+def test_side_close_orders_after_second_side_stream(monkeypatch):
+    """ADVICE r03 (api.cpp flush): with two gradient buckets and bucket 1's replica fold +
+    gradient finalisation on the side stream (ISG_SIDE_CLOSE=1), that fold must run after
+    the weight gradients dealt onto the second side stream. The gradients must equal those
+    of the same plan with the second side stream off (ISG_NO_SIDE2=1) and of the default
+    plan; a dropped weight-gradient contribution would show up as an O(1) relative error."""
+    fx = SegmentFixture("segment20_n2_128.npz")
+    xs, y = _inputs(fx.x), torch.from_numpy(fx.mask).to(DEV)
+
+    def grads(env):
+        for k in ("ISG_BUCKETS", "ISG_SIDE_CLOSE", "ISG_NO_SIDE2"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        tr = Trainer(_model(fx), fx.n, [(fx.n, 3, fx.h, fx.w), (fx.n, 17, fx.h, fx.w)],
+                     device=DEV).capture()
+        sd = tr.optimizer_state_dict()
+        sd["param_groups"][0]["lr"] = 0.0  # parameters fixed: every replay has one answer
+        tr.load_optimizer_state_dict(sd)
+        out = []
+        for _ in range(3):  # replays: a race would not show on every one
+            tr.step(xs, y)
+            torch.cuda.synchronize()
+            out.append(tr.grad_flat.detach().double().cpu().clone())
+        return out
+
+    base = grads({})[0]
+    scale = base.abs().max().item()
+    for env in ({"ISG_BUCKETS": "2", "ISG_SIDE_CLOSE": "1"},
+                {"ISG_BUCKETS": "2", "ISG_SIDE_CLOSE": "1", "ISG_NO_SIDE2": "1"}, {}):
+        for i, g in enumerate(grads(env)):
+            err = (g - base).abs().max().item()
+            print(env, i, f"max abs diff {err:.2e} (scale {scale:.2e})")
+            assert err <= 1e-5 * scale, (env, i, err)
