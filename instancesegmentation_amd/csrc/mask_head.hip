@@ -21,6 +21,8 @@
 // row ly (origin Y0 - 1) has phase r = (1 + ly) & 3 and local input row (1 + ly) >> 2.
 #include "stage.h"
 
+#include <type_traits>
+
 namespace {
 
 constexpr int kThreads = 256;
@@ -463,51 +465,82 @@ ISG_DEV void hb_store_dx(const isg_mask_head& a, const SinkRow* sk, const float*
 // (stage.h XfLin: PLAIN / BN_FWD + activation).
 struct HbPrefetch {
     f32x4 dl[3], x[4];
+    int ok;  // bit k: dl[k] in range, bit 3 + k: x[k] in range (else the load read a dummy)
 };
 
-ISG_DEV void hb_issue(const isg_mask_head& a, const VtLite& vl, int n, int Y0, int X0, HbPrefetch& f) {
+// Branch-free: every lane issues its 7 loads unconditionally (an out-of-range item reads
+// the first element of its tensor instead and its bit in `ok` is clear). A load under a
+// branch makes the compiler drain the whole memory queue (s_waitcnt vmcnt(0)) at the join,
+// which turned the prefetch into a synchronous load.
+struct HbSrc {  // the input's segments as element offsets from segment 0 (opaque scalars)
+    const float* p0;
+    int64_t d1, d2;
+    int ns0, ns1, ns2, c1, c2, Hi, Wi;
+};
+
+ISG_DEV HbSrc hb_src(const VtLite& l, int Hi, int Wi) {
+    HbSrc r;
+    r.p0 = sgpr_p(l.p0);
+    // per-lane segment selection as integer selects: a select between pointers was
+    // lowered to an indexed load from a stack copy of the candidates
+    const int64_t d1 = l.p1 ? l.p1 - l.p0 : 0, d2 = l.p2 ? l.p2 - l.p0 : 0;
+    r.d1 = ((int64_t)sgpr_i((int)(d1 >> 32)) << 32) | (uint32_t)sgpr_i((int)d1);
+    r.d2 = ((int64_t)sgpr_i((int)(d2 >> 32)) << 32) | (uint32_t)sgpr_i((int)d2);
+    r.ns0 = sgpr_i(l.ns0); r.ns1 = sgpr_i(l.ns1); r.ns2 = sgpr_i(l.ns2);
+    r.c1 = sgpr_i(l.c1); r.c2 = sgpr_i(l.c2);
+    r.Hi = sgpr_i(Hi); r.Wi = sgpr_i(Wi);
+    return r;
+}
+
+ISG_DEV void hb_issue(const HbSrc& hs, const float* dout0, int64_t dns, int n, int Y0, int X0,
+                      HbPrefetch& f) {
     using namespace hb;
-    const int OH = 4 * a.Hi, OW = 4 * a.Wi, iy0 = Y0 / 4, ix0 = X0 / 4;
-    const float* dout = a.dout + (int64_t)n * a.dout_n_stride;
-    const int hw = a.Hi * a.Wi;
+    const int OH = 4 * hs.Hi, OW = 4 * hs.Wi, iy0 = Y0 / 4, ix0 = X0 / 4;
+    const int hw = hs.Hi * hs.Wi;
+    const float* dout = dout0 + (int64_t)n * dns;
+    int ok = 0;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         const int i = threadIdx.x + k * kThreads;
         const int r = i / DNQ, qd = i - r * DNQ;
         const int oy = Y0 - 3 + r, ox = X0 - 4 + 4 * qd;
-        f.dl[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (i < DSH * DNQ && oy >= 0 && oy < OH && ox >= 0 && ox < OW)
-            f.dl[k] = gld4(dout, (int64_t)oy * OW + ox);
+        const bool in = (i < DSH * DNQ) & (oy >= 0) & (oy < OH) & (ox >= 0) & (ox < OW);
+        f.dl[k] = gld4(dout, in ? oy * OW + ox : 0);
+        ok |= in ? 1 << k : 0;
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         // opaque: recompute the per-lane channel addressing per tile instead of keeping 4
-        // hoisted 64-bit pointers live across the whole tile loop (they spilled)
+        // 64-bit offsets live across the whole tile loop (they spilled)
         const int i = opaque(threadIdx.x + k * kThreads);
         const int ci = i / (TSH * TSW / 4), rem = i - ci * (TSH * TSW / 4);
         const int r = rem / (TSW / 4), qd = rem - r * (TSW / 4);
         const int iy = iy0 - 1 + r, ix = ix0 - 4 + 4 * qd;
-        f.x[k] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (i < kCi * TSH * TSW / 4 && iy >= 0 && iy < a.Hi && ix >= 0 && ix < a.Wi) {
-            const float* p = ci >= vl.c2 ? vl.p2 + (int64_t)(ci - vl.c2) * hw + (int64_t)n * vl.ns2
-                           : ci >= vl.c1 ? vl.p1 + (int64_t)(ci - vl.c1) * hw + (int64_t)n * vl.ns1
-                                         : vl.p0 + (int64_t)ci * hw + (int64_t)n * vl.ns0;
-            f.x[k] = gld4(p, (int64_t)iy * a.Wi + ix);
-        }
+        const bool in = (i < kCi * TSH * TSW / 4) & (iy >= 0) & (iy < hs.Hi) & (ix >= 0) & (ix < hs.Wi);
+        // segment by masks, not selects: a select chain over the three candidates was
+        // turned into a lookup table in scratch memory
+        const int m2 = -(int)(ci >= hs.c2), m1 = -(int)(ci >= hs.c1) & ~m2;
+        const int cl = ci - (hs.c1 & m1) - (hs.c2 & m2);
+        const int ns = hs.ns0 + ((hs.ns1 - hs.ns0) & m1) + ((hs.ns2 - hs.ns0) & m2);
+        const int64_t off = (hs.d1 & (int64_t)m1) + (hs.d2 & (int64_t)m2) + (int64_t)n * ns +
+                            (int64_t)cl * hw + iy * hs.Wi + ix;
+        f.x[k] = gld4(hs.p0, in ? off : 0);
+        ok |= in ? 1 << (3 + k) : 0;
     }
+    f.ok = ok;
 }
 
-ISG_DEV void hb_commit(const HbPrefetch& f, const XfLin* xl, int Hi, int Wi, int iy0, int ix0,
-                       float* Ts, float* Ds, float& db2) {
+ISG_DEV void hb_commit(const HbPrefetch& f, const XfLin* xl, float* Ts, float* Ds, float& db2) {
     using namespace hb;
+    const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         const int i = threadIdx.x + k * kThreads;
         if (i < DSH * DNQ) {
             const int r = i / DNQ, qd = i - r * DNQ;
-            *reinterpret_cast<f32x4*>(&Ds[r * DSW + 4 * qd]) = f.dl[k];
-            if (r >= 3 && r < 3 + TY && qd >= 1 && qd <= TX / 4)
-                db2 += (f.dl[k][0] + f.dl[k][1]) + (f.dl[k][2] + f.dl[k][3]);
+            const f32x4 v = (f.ok >> k) & 1 ? f.dl[k] : zero;
+            *reinterpret_cast<f32x4*>(&Ds[r * DSW + 4 * qd]) = v;
+            if (r >= 3 && r < 3 + TY && qd >= 1 && qd <= TX / 4) db2 += (v[0] + v[1]) + (v[2] + v[3]);
         }
     }
 #pragma unroll
@@ -515,10 +548,8 @@ ISG_DEV void hb_commit(const HbPrefetch& f, const XfLin* xl, int Hi, int Wi, int
         const int i = threadIdx.x + k * kThreads;
         if (i < kCi * TSH * TSW / 4) {
             const int ci = i / (TSH * TSW / 4), rem = i - ci * (TSH * TSW / 4);
-            const int r = rem / (TSW / 4), qd = rem - r * (TSW / 4);
-            const int iy = iy0 - 1 + r, ix = ix0 - 4 + 4 * qd;
             // outside the image the convT input is zero padding, not transform(0)
-            const bool in = iy >= 0 && iy < Hi && ix >= 0 && ix < Wi;
+            const bool in = (f.ok >> (3 + k)) & 1;
             const XfLin l = xl[ci];
             f32x4 v;
 #pragma unroll
@@ -551,13 +582,20 @@ __global__ __launch_bounds__(kThreads, 2) void head_bwd_kernel(isg_mask_head a, 
     const int64_t rn = ISG_HEAD_RING(a.Hi, a.Wi);
     STAMP(0);
     const VtLite vl = vt_lite(a.x);
+    const HbSrc hs = hb_src(vl, a.Hi, a.Wi);
+    const float* dout0 = sgpr_p(a.dout);
+    const int64_t dns = a.dout_n_stride;
+    f32x4 w1r[kW1 / 4 / kThreads];  // the convT weight, issued first: its LDS copy below
+#pragma unroll                       // then waits for these loads only
+    for (int k = 0; k < kW1 / 4 / kThreads; ++k) w1r[k] = gld4(a.w1, 4 * (tid + k * kThreads));
     HbPrefetch pf;
     if (VX && (int)blockIdx.x < ntiles) {  // the first tile's loads overlap the setup below
         const int t2 = blockIdx.x % (ntx * nty);
-        hb_issue(a, vl, blockIdx.x / (ntx * nty), (t2 / ntx) * TY, (t2 % ntx) * TX, pf);
+        hb_issue(hs, dout0, dns, blockIdx.x / (ntx * nty), (t2 / ntx) * TY, (t2 % ntx) * TX, pf);
     }
     load_vt_coefs(a.x, coef, tid, kThreads);
-    copy_w1(a.w1, Xc);
+#pragma unroll
+    for (int k = 0; k < kW1 / 4 / kThreads; ++k) reinterpret_cast<f32x4*>(Xc)[tid + k * kThreads] = w1r[k];
     if (tid < kCi) {
         SinkRow q = {};
         q.mode = ISG_SINK_NONE;
@@ -617,7 +655,7 @@ __global__ __launch_bounds__(kThreads, 2) void head_bwd_kernel(isg_mask_head a, 
         if (pn >= 0) hb_store_dx<VX>(a, sk, dxs, pn, piy0, pix0);
         // ---- staging: dlogits (+ own sum), input region, the ring (border tiles)
         if (VX) {
-            hb_commit(pf, xl, a.Hi, a.Wi, iy0, ix0, Ts, Ds, db2);
+            hb_commit(pf, xl, Ts, Ds, db2);
         } else {
             const float* dout = a.dout + (int64_t)n * a.dout_n_stride;
             for (int i = tid; i < DSH * DSW; i += kThreads) {
@@ -659,8 +697,9 @@ __global__ __launch_bounds__(kThreads, 2) void head_bwd_kernel(isg_mask_head a, 
         // ---- the next tile's loads, in flight during this tile's compute
         if (VX && tile + (int)gridDim.x < ntiles) {
             const int nt = tile + gridDim.x, nn = nt / (ntx * nty), nt2 = nt - nn * ntx * nty;
-            hb_issue(a, vl, nn, (nt2 / ntx) * TY, (nt2 % ntx) * TX, pf);
+            hb_issue(hs, dout0, dns, nn, (nt2 / ntx) * TY, (nt2 % ntx) * TX, pf);
         }
+        if (pn < 0) STAMP(3);
         // ---- intermediate gradient over the cell region (origin (Y0 - 2, X0 - 2)):
         //      dI[co][q] = sum_{ty,tx} w2[co][ty][tx] dl[q + 1 - ty][q + 1 - tx], zero outside
         //      the image, stored phase-split Xc[((co * 4 + r) * 4 + s) * NCELL + cy * CX + cx]
@@ -703,7 +742,7 @@ __global__ __launch_bounds__(kThreads, 2) void head_bwd_kernel(isg_mask_head a, 
             }
         }
         __syncthreads();
-        if (pn < 0) STAMP(3);
+        if (pn < 0) STAMP(4);
         // ---- border tiles: C[co][t] += dl[p] * I_full[p + t - 1] over the pairs whose
         //      intermediate pixel is outside the image (wave = co, lane = tile column / row)
         if (border) {
@@ -779,11 +818,11 @@ __global__ __launch_bounds__(kThreads, 2) void head_bwd_kernel(isg_mask_head a, 
                 if ((st & 3) == 3) asm volatile("" ::: "memory");
             }
         }
-        if (pn < 0) STAMP(4);
+        if (pn < 0) STAMP(5);
         pn = n; piy0 = iy0; pix0 = ix0;
     }
     __syncthreads();
-    STAMP(5);
+    STAMP(6);
     if (pn >= 0) hb_store_dx<VX>(a, sk, dxs, pn, piy0, pix0);
     // ---- once per workgroup: dW1, Z' -> dW2, bias gradients, into replica rep
     const int rep = blockIdx.x % a.nrep;
@@ -796,15 +835,11 @@ __global__ __launch_bounds__(kThreads, 2) void head_bwd_kernel(isg_mask_head a, 
             for (int i = 0; i < 4; ++i)
                 atomicAdd(&d[(4 * kq + i) * (kCm * 64) + wave * 64 + t * 16 + nl], dw1[t][i]);
     }
-    float* Zs = Xc;                      // [16 ci][ZN]
-    float* W1s = Xc + kCi * ZN;          // [16][4][8][8]
-    for (int e = tid; e < kW1 / 4; e += kThreads)
-        reinterpret_cast<f32x4*>(W1s)[e] = gld4(a.w1, 4 * e);
+    float* Zs = Xc;  // [16 ci][ZN]
     float v1[kCm];
 #pragma unroll
     for (int co = 0; co < kCm; ++co) v1[co] = wave_sum(db1[co]);
     const float v2 = wave_sum(db2);
-    __syncthreads();
 #pragma unroll
     for (int t = 0; t < 2; ++t)
         if (t == 0 || z2)
@@ -816,32 +851,37 @@ __global__ __launch_bounds__(kThreads, 2) void head_bwd_kernel(isg_mask_head a, 
         red[kCm * 4 + wave] = v2;
     }
     __syncthreads();
-    STAMP(6);
     const float sdl = (red[kCm * 4] + red[kCm * 4 + 1]) + (red[kCm * 4 + 2] + red[kCm * 4 + 3]);
-    // dW2[co][t] = sum_{ci, ky, kx} W1[ci][co][ky][kx] Z'[ci][(ky - ty + 1, kx - tx + 1)]:
-    // wave = co, lane = (ci, two kernel rows); the 9 taps summed over the wave
+    // dW2[co][t] = sum_{ci, ky, kx} W1[ci][co][ky][kx] Z'[ci][(ky - ty + 1, kx - tx + 1)] from
+    // the W1 values already in wdA: lane (ci = nl, (a, b) = kq) holds, for plane o = (co, r,
+    // s), W1[ci][co][r + 4(1 - a)][s + 4(1 - b)]; wave = co, the 9 taps summed over the wave
     {
-        const int co = wave, ci = lane >> 2, kyg = lane & 3;
-        const float* w = W1s + (ci * kCm + co) * 64 + 2 * kyg * 8;
-        const float* z = Zs + ci * ZN + 2 * kyg * ZD;  // rows 2kyg .. 2kyg + 3 of the 10 x 10 offsets
-        float zr[4][ZD];
+        float zr[6][6];  // Z' rows / columns 4(1-a) .. 4(1-a) + 5 of this lane's input channel
+        const float* z = Zs + nl * ZN + 4 * (1 - aa) * ZD + 4 * (1 - bb);
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
+        for (int r = 0; r < 6; ++r)
 #pragma unroll
-            for (int c = 0; c < ZD; ++c) zr[r][c] = z[r * ZD + c];
+            for (int c = 0; c < 6; ++c) zr[r][c] = z[r * ZD + c];
         float c9[9];
 #pragma unroll
         for (int t = 0; t < 9; ++t) c9[t] = 0.f;
+        auto dw2_co = [&](auto cot) {
+            constexpr int co = decltype(cot)::value;
 #pragma unroll
-        for (int ky = 0; ky < 2; ++ky)
-#pragma unroll
-            for (int kx = 0; kx < 8; ++kx) {
-                const float wv = w[ky * 8 + kx];
+            for (int j = 0; j < 16; ++j) {
+                const int r = j >> 2, s2 = j & 3;
+                const float wv = wdA[co * 16 + j];
 #pragma unroll
                 for (int ty = 0; ty < 3; ++ty)
 #pragma unroll
-                    for (int tx = 0; tx < 3; ++tx) c9[ty * 3 + tx] += wv * zr[ky + 2 - ty][kx + 2 - tx];
+                    for (int tx = 0; tx < 3; ++tx) c9[ty * 3 + tx] += wv * zr[r + 2 - ty][s2 + 2 - tx];
             }
+        };
+        if (wave == 0) dw2_co(std::integral_constant<int, 0>{});
+        else if (wave == 1) dw2_co(std::integral_constant<int, 1>{});
+        else if (wave == 2) dw2_co(std::integral_constant<int, 2>{});
+        else dw2_co(std::integral_constant<int, 3>{});
+        const int co = wave;
         const float b1 = a.b1 ? a.b1[co] : 0.f;
 #pragma unroll
         for (int t = 0; t < 9; ++t) {
