@@ -69,6 +69,8 @@ static int32_t check_geom(const isg_conv_geom* g) {
 
 int32_t isg_tap_conv(const isg_conv_geom*, const isg_vtensor*, const float*, const isg_sinks*,
                      bool, hipStream_t);
+int32_t isg_s2k5_fwd(const isg_conv_geom*, const isg_vtensor*, const float*, const isg_sinks*,
+                     hipStream_t);
 int32_t isg_tap_wgrad(const isg_conv_geom*, const isg_vtensor*, const isg_vtensor*, float*, float*,
                       int64_t, int32_t, hipStream_t);
 
@@ -86,6 +88,9 @@ int32_t isg_conv_fwd(const isg_conv_geom* g, const isg_vtensor* x, const float* 
                      const isg_sinks* out, isg_stream_t st) {
     if (int32_t e = check_geom(g)) return e;
     if (partial_w(g)) {
+        // the stem's RGB layer 1 (5x5 s2, weight over w_ci = 20 channels): s2k5_fwd_kernel
+        const int32_t s = isg_s2k5_fwd(g, x, w, out, st);
+        if (s != 0) return s < 0 ? s : ISG_OK;
         const int32_t t = isg_tap_conv(g, x, w, out, false, st);
         if (t < 0) return t;
         return t ? ISG_OK : isg_set_error(ISG_ERR_UNSUPPORTED, "conv fwd: w_ci %d != Ci %d off tap_conv", g->w_ci, g->Ci);

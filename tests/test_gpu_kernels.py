@@ -149,19 +149,26 @@ def test_conv_fwd_dense(cfg):
     close(stats[Co:2 * Co], (ref * ref).sum((0, 2, 3)), what="sumsq")
 
 
-@pytest.mark.parametrize("cfg", [(16, 16, 134, 200), (12, 8, 40, 36), (16, 16, 400, 672)],
-                         ids=["ragged", "narrow", "stem_1344x800"])
-def test_s2k5_fwd(cfg, monkeypatch):
-    """The opt-in LDS-staged 5x5 s2 forward (ISG_S2K5=1, down_conv.hip s2k5_fwd_kernel)
-    against fp64 at a bar of 4e-6 of scale — one fp32 rounding chain over 400 taps — at
-    the stem's layer-2 geometry of BASELINE config 3 (2x400x672 -> 200x336: a partial
-    64-column block) as well as ragged shapes; training-mode BN + PReLU on load."""
-    monkeypatch.setenv("ISG_S2K5", "1")
-    Ci, Co, H, W = cfg
+@pytest.mark.parametrize("cfg", [(16, 16, 512, 512), (16, 16, 134, 200), (12, 8, 40, 36),
+                                 (16, 16, 400, 672), (3, 16, 64, 48), (3, 16, 1024, 1024, 20)],
+                         ids=["stem_bench", "ragged", "narrow", "stem_1344x800", "three_channels",
+                              "stem_rgb_layer1_wci20"])
+def test_s2k5_fwd(cfg):
+    """The persistent producer/consumer 5x5 s2 forward (down_conv.hip s2k5_fwd_kernel, the
+    stem's layer 2) against fp64 at a bar of 4e-6 of scale — one fp32 rounding chain over
+    400 taps — at the bench geometry (2x512^2 -> 256^2, 1024 tiles over persistent
+    workgroups), BASELINE config 3's (2x400x672 -> 200x336: partial column and row tiles),
+    ragged shapes and 3 input channels; training-mode BN + PReLU on load, bias and BN
+    statistics through the STORE sink."""
+    Ci, Co, H, W = cfg[:4]
+    wci = cfg[4] if len(cfg) > 4 else Ci  # the keypoint stem's RGB part: weight over 20 channels
     N = 2
     ge, OH, OW = _geom(N, Ci, Co, H, W, 5, 2, 2, 1)
+    if wci != Ci:
+        ge["w_ci"] = wci
     x = rnd(N, Ci, H, W, seed=11) * 0.7 + 0.2
-    w = rnd(Co, Ci, 5, 5, seed=12, scale=(2.0 / (Ci * 25)) ** 0.5)
+    wfull = rnd(Co, wci, 5, 5, seed=12, scale=(2.0 / (wci * 25)) ** 0.5)
+    w = wfull[:, :Ci].contiguous()
     b = rnd(Co, seed=13, scale=0.1)
     gamma, beta, _, _, slope = bn_eval_params(Ci, 5)
     mean = x.mean((0, 2, 3))
@@ -174,7 +181,7 @@ def test_s2k5_fwd(cfg, monkeypatch):
              "act": L.ACT["prelu"], "slope": ptr(G[4]), "bn": bn_spec_eval(*G[:4])}]
     Y = torch.full((N, Co, OH, OW), float("nan"), device=DEV)
     stats = rep_zeros(4 * Co)
-    B, Wt = cuda32(b), cuda32(w)  # held: the kernel reads them after this frame's temporaries die
+    B, Wt = cuda32(b), cuda32(wfull)  # held: the kernel reads them after this frame's temporaries die
     sk = sinks([{"p": ptr(Y), "n_stride": Co * OH * OW, "c0": 0, "C": Co,
                  "mode": L.SINK_STORE, "bias": ptr(B), "stats": ptr(stats)}])
     call("isg_conv_fwd", geom(**ge), vt(segs, N, H, W), ptr(Wt), sk, stream())
