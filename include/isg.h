@@ -310,6 +310,14 @@ int32_t isg_mask_nms(const uint8_t* masks, int32_t K, int32_t H, int32_t W, floa
                      void* work, float* scores_out, int32_t* keep, int32_t* nkeep,
                      isg_stream_t stream);
 
+/* A13 + A14 in one pass (the infer product path): isg_mask_paste's canvases written and
+ * bit-packed for the NMS in the same kernel (no memset, no re-read of the canvases),
+ * then isg_mask_nms's intersections and greedy suppression. Same outputs, bit-exact to
+ * isg_mask_paste followed by isg_mask_nms; work: isg_mask_nms_workspace(K,H,W) bytes. */
+int32_t isg_mask_paste_nms(const float* prob, int32_t K, int32_t S, const int32_t* boxes,
+                           int32_t H, int32_t W, float iou_thr, uint8_t* masks, void* work,
+                           float* scores_out, int32_t* keep, int32_t* nkeep, isg_stream_t stream);
+
 /* ---- infer pre-process ----------------------------- */
 
 /* Per-instance crop: window k = (x0,y0,x1,y1) of an HxWx3 uint8 RGB image (instance box

@@ -182,6 +182,8 @@ SIGNATURES = {
     "isg_mask_nms_workspace": (c_int64, [c_int32, c_int32, c_int32]),
     "isg_mask_nms": (c_int32, [c_void_p, c_int32, c_int32, c_int32, c_float, c_void_p, c_void_p,
                                c_void_p, c_void_p, c_void_p]),
+    "isg_mask_paste_nms": (c_int32, [c_void_p, c_int32, c_int32, c_void_p, c_int32, c_int32, c_float,
+                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "isg_instance_crop": (c_int32, [c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_int32,
                                     c_int32, c_void_p, c_void_p]),
     "isg_keypoint_heatmaps": (c_int32, [c_void_p, c_int32, c_int32, c_int32, c_int32, c_double,

@@ -71,6 +71,8 @@ int32_t isg_tap_conv(const isg_conv_geom*, const isg_vtensor*, const float*, con
                      bool, hipStream_t);
 int32_t isg_s2k5_fwd(const isg_conv_geom*, const isg_vtensor*, const float*, const isg_sinks*,
                      hipStream_t);
+int32_t isg_s2k5_wgrad(const isg_conv_geom*, const isg_vtensor*, const isg_vtensor*, float*, float*,
+                       int64_t, int32_t, hipStream_t);
 int32_t isg_tap_wgrad(const isg_conv_geom*, const isg_vtensor*, const isg_vtensor*, float*, float*,
                       int64_t, int32_t, hipStream_t);
 
@@ -115,6 +117,9 @@ int32_t isg_conv_wgrad_rep(const isg_conv_geom* g, const isg_vtensor* dy, const 
         return isg_set_error(ISG_ERR_INVALID, "conv wgrad: bad replicas %d / stride %lld", nrep,
                              (long long)rep_stride);
     if (partial_w(g)) {
+        // the stem's RGB layer 1 (weight over w_ci = 20 channels): s2k5_wgrad_kernel
+        const int32_t s = isg_s2k5_wgrad(g, dy, x, dw, dbias, rep_stride, nrep, st);
+        if (s != 0) return s < 0 ? s : ISG_OK;
         const int32_t t = isg_tap_wgrad(g, dy, x, dw, dbias, rep_stride, nrep, st);
         if (t < 0) return t;
         return t ? ISG_OK : isg_set_error(ISG_ERR_UNSUPPORTED, "conv wgrad: w_ci %d != Ci %d off tap_wgrad", g->w_ci, g->Ci);

@@ -32,6 +32,31 @@ typedef f32x4 __attribute__((address_space(1)))* gf32x4_p;
 // 16-B global store of 4 consecutive floats at p[i..i+3] (p + i 16-B aligned)
 ISG_DEV void gst4(float* p, int64_t i, f32x4 v) { *(gf32x4_p)((gfloat_p)p + i) = v; }
 
+// Cooperative global -> LDS copy of n floats, dst[i] = src[off(i)] (off(i) < 0: 0), with U
+// loads of each thread in flight together. A rolled `for (i = tid; i < n; i += nthreads)`
+// loop around a predicated load pays one full memory round trip per iteration (the
+// compiler waits for each load before the next iteration's branch): 9-34 serial L2 round
+// trips in the weight staging of tap_conv / kp_stem / sub2_dgrad.
+template <int U, class F>
+ISG_DEV void coop_gather(float* dst, int n, int tid, int nthreads, const float* src, F off) {
+    for (int i0 = tid; i0 < n; i0 += U * nthreads) {
+        float v[U];
+        bool z[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = i0 + u * nthreads;
+            const int o = i < n ? off(i) : -1;
+            z[u] = o < 0;
+            v[u] = ((gcfloat_p)src)[o < 0 ? 0 : o];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = i0 + u * nthreads;
+            if (i < n) dst[i] = z[u] ? 0.f : v[u];
+        }
+    }
+}
+
 // ---- per-channel coefficient table (LDS) -------------------------------------
 // BN_FWD : v = act((x - c0) * c1 + c2)          c0=mean  c1=gamma*rstd  c2=beta, c3=slope
 // BN_BWD : v = c0*g + c1*(y - c2) + c3          (BatchNorm2d backward)

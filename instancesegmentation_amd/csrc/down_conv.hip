@@ -302,10 +302,23 @@ __global__ __launch_bounds__(kThreads) void sub2_dgrad_mfma_kernel(DownArgs a) {
     const int Hs = a.H, Ws = a.W, Wd = 2 * Ws;
     if (tid < a.C) tab[tid] = ch_table_entry(a.dy, tid, (int64_t)Hs * Ws);
     if (tid < a.M) ri[tid] = sink_row(a.out, tid, (int64_t)2 * Hs * Wd);
-    for (int e = tid; e < kMaxM * kMaxM * K * K; e += kThreads) {
-        const int c = e / (kMaxM * K * K), r = e - c * kMaxM * K * K;
-        const int m = r / (K * K), tap = r - m * K * K;
-        wl[e] = (c < a.C && m < a.M) ? gld(a.w, ((int64_t)c * a.M + m) * K * K + tap) : 0.f;
+    {   // the weight: every load of the thread issued before the first store (a rolled loop
+        // of predicated loads paid one L2 round trip per element: 25 in a row)
+        constexpr int NW = kMaxM * kMaxM * K * K, UW = NW / kThreads;
+        static_assert(NW % kThreads == 0, "weight copy split");
+        const int nw = a.C * a.M * K * K;
+        float wv[UW];
+#pragma unroll
+        for (int u = 0; u < UW; ++u) {
+            const int e = tid + u * kThreads;
+            const int c = e / (kMaxM * K * K), r = e - c * kMaxM * K * K;
+            const int m = r / (K * K), tap = r - m * K * K;
+            const int src = (c * a.M + m) * K * K + tap;
+            wv[u] = gld(a.w, (c < a.C && m < a.M) ? src : 0);
+            wv[u] = (c < a.C && m < a.M && src < nw) ? wv[u] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < UW; ++u) wl[tid + u * kThreads] = wv[u];
     }
     __syncthreads();
     // block: 64 cells (4 waves x 16) of kRowsPB consecutive rows, one row at a time (the
@@ -436,10 +449,23 @@ __global__ __launch_bounds__(kThreads) void sub2_dgrad_lds_kernel(DownArgs a) {
         lin[tid] = xf_lin(t.xf, t.act, t.k);
     }
     if (tid < a.M) ri[tid] = sink_row(a.out, tid, (int64_t)2 * Hs * Wd);
-    for (int e = tid; e < kMaxM * kMaxM * K * K; e += kThreads) {
-        const int c = e / (kMaxM * K * K), r = e - c * kMaxM * K * K;
-        const int m = r / (K * K), tap = r - m * K * K;
-        wl[e] = (c < a.C && m < a.M) ? gld(a.w, ((int64_t)c * a.M + m) * K * K + tap) : 0.f;
+    {   // the weight: every load of the thread issued before the first store (a rolled loop
+        // of predicated loads paid one L2 round trip per element: 25 in a row)
+        constexpr int NW = kMaxM * kMaxM * K * K, UW = NW / kThreads;
+        static_assert(NW % kThreads == 0, "weight copy split");
+        const int nw = a.C * a.M * K * K;
+        float wv[UW];
+#pragma unroll
+        for (int u = 0; u < UW; ++u) {
+            const int e = tid + u * kThreads;
+            const int c = e / (kMaxM * K * K), r = e - c * kMaxM * K * K;
+            const int m = r / (K * K), tap = r - m * K * K;
+            const int src = (c * a.M + m) * K * K + tap;
+            wv[u] = gld(a.w, (c < a.C && m < a.M) ? src : 0);
+            wv[u] = (c < a.C && m < a.M && src < nw) ? wv[u] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < UW; ++u) wl[tid + u * kThreads] = wv[u];
     }
     __syncthreads();
     // ---- stage the band: interior quads (16-B loads), then the two halo columns
@@ -584,11 +610,11 @@ static_assert(2 * kWgNW <= kWgLds, "s2k5 wgrad epilogue regions");
 struct S2wArgs {
     isg_vtensor dy;  // the conv's output gradient: M channels, OH x OW
     isg_vtensor x;   // its input: C channels, 2 OH x 2 OW
-    float* dw;
+    float* dw;       // [M][wc][5][5] (the first C input channels written)
     float* dbias;
     int64_t rep_stride;
     int nrep;
-    int N, M, C, OH, OW;
+    int N, M, C, wc, OH, OW;
     int tiles_x, tiles_y, ntiles, tpw;
     int dbg;  // ablation bits (ISG_S2W_DBG, experiments only): 1 no MFMA loop, 2 no global loads, 4 no LDS staging
 };
@@ -625,7 +651,12 @@ ISG_DEV f32x4 s2_coef_dy(const isg_vtensor& vt, int c, int hw) {
     return f32x4{q.c0, q.c1, q.c2, q.c3};
 }
 
-template <bool YB>
+// NARROW (C <= 4, the RGB layer 1): the 25 taps x C channels go into the MFMA's N dimension
+// instead — B[px][n = (c, tap)], 5 N-tiles of 16 (75 used) — so a pixel quad costs 5 MFMAs,
+// not 25 with 13 of every 16 columns zero.
+constexpr int kNarN = 5;                  // N-tiles of the narrow form
+constexpr int kNarNW = kMaxM * 16 * kNarN;  // its per-workgroup partial
+template <bool YB, bool NARROW>
 __global__ __launch_bounds__(2 * kThreads, 1) void s2k5_wgrad_kernel(S2wArgs a) {
     extern __shared__ __attribute__((aligned(16))) float s2w_lds[];  // 2 x [Xs | Ds]
     __shared__ S2Ch tabx[kMaxM];
@@ -654,7 +685,7 @@ __global__ __launch_bounds__(2 * kThreads, 1) void s2k5_wgrad_kernel(S2wArgs a) 
     __syncthreads();
     STAMP(1);
 
-    constexpr int NE = kMaxM * kWgNR * kWgQ;
+    constexpr int NE = (NARROW ? 4 : kMaxM) * kWgNR * kWgQ;
     constexpr int UX = (NE + kThreads - 1) / kThreads;
     constexpr int ND = kMaxM * kWgRows * (kWgX / 4);
     constexpr int UD = (ND + kThreads - 1) / kThreads;
@@ -755,10 +786,18 @@ __global__ __launch_bounds__(2 * kThreads, 1) void s2k5_wgrad_kernel(S2wArgs a) 
         } else if (tid >= 64 && tid < 64 + kMaxM) {
             taby[tid - 64].k = s2_coef_dy(a.dy, min(tid - 64, a.M - 1), Ho * Wo);
         }
-        f32x4 acc[25];
+        constexpr int NACC = NARROW ? kNarN : 25;
+        f32x4 acc[NACC];
 #pragma unroll
-        for (int t = 0; t < 25; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int t = 0; t < NACC; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
         float bsum = 0.f;
+        // NARROW: this lane's column n = 16t + pl -> (channel, tap) as a band offset
+        int noff[kNarN];
+#pragma unroll
+        for (int t = 0; t < kNarN; ++t) {
+            const int n = 16 * t + pl, c = n / 25, tap = n - c * 25, kh = tap / 5, kw = tap - kh * 5;
+            noff[t] = n < 4 * 25 ? c * kWgPL + kh * kWgRS + (kw & 1) * kWgEW + (kw >> 1) : 0;
+        }
         __syncthreads();  // A
         __syncthreads();  // B
         STAMP(2);
@@ -770,13 +809,23 @@ __global__ __launch_bounds__(2 * kThreads, 1) void s2k5_wgrad_kernel(S2wArgs a) 
             // fully unrolled: every operand read is the lane's base address plus an immediate
             // offset, and the scheduler runs the reads ahead of the MFMAs (a rolled loop
             // re-derived 25 addresses per step and waited out each read)
-            if (nq) {
+            if (nq && NARROW) {
+                const float* const nb = Xs + 2 * wave * kWgRS + kq + 1;
 #pragma unroll
                 for (int q = 0; q < kWgX / 4; ++q) {
                     const float av = ab[4 * q];
                     bsum += av;
 #pragma unroll
-                    for (int j = 0; j < 25; ++j)
+                    for (int t = 0; t < kNarN; ++t)
+                        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, nb[noff[t] + 4 * q], acc[t], 0, 0, 0);
+                }
+            } else if (nq) {
+#pragma unroll
+                for (int q = 0; q < kWgX / 4; ++q) {
+                    const float av = ab[4 * q];
+                    bsum += av;
+#pragma unroll
+                    for (int j = 0; j < NACC; ++j)
                         acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(
                             av, bb[(j / 5) * kWgRS + ((j % 5) & 1) * kWgEW + ((j % 5) >> 1) + 4 * q], acc[j], 0, 0, 0);
                 }
@@ -785,27 +834,39 @@ __global__ __launch_bounds__(2 * kThreads, 1) void s2k5_wgrad_kernel(S2wArgs a) 
         }
         // ---- epilogue: lane holds D[m = 4kq + i][c = pl] of every tap
         STAMP(3);
+        // NARROW: R[(m * kNarN + t) * 16 + pl] = D[m][n = 16t + pl]
+        auto ridx = [&](int t, int i) {
+            return NARROW ? ((4 * kq + i) * kNarN + t) * 16 + pl : ((4 * kq + i) * kMaxM + pl) * 25 + t;
+        };
+        constexpr int NW = NARROW ? kNarNW : kWgNW;
         if (wave < 2) {
 #pragma unroll
-            for (int t = 0; t < 25; ++t)
+            for (int t = 0; t < NACC; ++t)
 #pragma unroll
-                for (int i = 0; i < 4; ++i) R[wave * kWgNW + ((4 * kq + i) * kMaxM + pl) * 25 + t] = acc[t][i];
+                for (int i = 0; i < 4; ++i) R[wave * NW + ridx(t, i)] = acc[t][i];
         }
         bred[wave][lane] = bsum;
         __syncthreads();  // E1
         if (wave >= 2) {
 #pragma unroll
-            for (int t = 0; t < 25; ++t)
+            for (int t = 0; t < NACC; ++t)
 #pragma unroll
-                for (int i = 0; i < 4; ++i) R[(wave - 2) * kWgNW + ((4 * kq + i) * kMaxM + pl) * 25 + t] += acc[t][i];
+                for (int i = 0; i < 4; ++i) R[(wave - 2) * NW + ridx(t, i)] += acc[t][i];
         }
         __syncthreads();  // E2
     }
     float* const dwr = a.dw + (int64_t)(blockIdx.x % a.nrep) * a.rep_stride;
-    for (int e = tid; e < kWgNW; e += 2 * kThreads) {
-        const int m = e / (kMaxM * 25), rem = e - m * (kMaxM * 25);
-        const int c = rem / 25, tap = rem - c * 25;
-        if (m < a.M && c < a.C) atomicAdd(&dwr[(m * a.C + c) * 25 + tap], R[e] + R[kWgNW + e]);
+    if (NARROW) {
+        for (int e = tid; e < kNarNW; e += 2 * kThreads) {
+            const int m = e / (kNarN * 16), n = e - m * (kNarN * 16), c = n / 25, tap = n - c * 25;
+            if (m < a.M && c < a.C) atomicAdd(&dwr[(m * a.wc + c) * 25 + tap], R[e] + R[kNarNW + e]);
+        }
+    } else {
+        for (int e = tid; e < kWgNW; e += 2 * kThreads) {
+            const int m = e / (kMaxM * 25), rem = e - m * (kMaxM * 25);
+            const int c = rem / 25, tap = rem - c * 25;
+            if (m < a.M && c < a.C) atomicAdd(&dwr[(m * a.wc + c) * 25 + tap], R[e] + R[kWgNW + e]);
+        }
     }
     if (a.dbias && tid < a.M) {
         float s = 0.f;
@@ -831,12 +892,17 @@ __global__ __launch_bounds__(2 * kThreads, 1) void s2k5_wgrad_kernel(S2wArgs a) 
 // (bias, BN statistics accumulated in registers across tiles, flushed once per workgroup).
 // The previous form (one tile per workgroup, weights re-staged per tile, no overlap of
 // staging and MFMA) ran 62 us against tap_conv's 65.
+constexpr int kFwPL = 816;  // channel plane (>= 11 * 72; 16 mod 32: lanes k = 0 / 1 of a B read hit disjoint banks)
+static_assert(kFwPL >= kWgNR * kWgRS && kFwPL % 32 == 16, "s2k5 fwd plane");
+constexpr int kFwOut = kMaxM * kWgX + 4;  // one wave's output row in LDS: [16 channels][32 columns] (+4: bank shift)
+
 struct S2fArgs {
     isg_vtensor x;  // C channels, 2 OH x 2 OW
     const float* w;  // [M][wc][5][5], the first C input channels used (wc >= C)
     isg_sinks out;   // M channels, OH x OW
     int N, M, C, wc, OH, OW;
     int tiles_x, tiles_y, ntiles, tpw;
+    int st16;  // one STORE sink over all M channels and OW % 4 == 0: 16-B epilogue stores
 };
 
 // G: channel groups of 4 (1 for the stem's RGB layer 1 with w_ci = 20, 4 for layer 2)
@@ -847,7 +913,7 @@ __global__ __launch_bounds__(2 * kThreads, 1) void s2k5_fwd_kernel(S2fArgs a) {
     __shared__ SinkRow ri[kMaxM];
     __shared__ float red[4][3][kMaxM];
     typedef float f32x2 __attribute__((ext_vector_type(2)));
-    constexpr int BAND = kMaxM * kWgPL;
+    constexpr int BAND = kMaxM * kFwPL;
     const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
     const int kq = lane >> 4, pl = lane & 15;
     const bool producer = wave >= 4;
@@ -858,13 +924,21 @@ __global__ __launch_bounds__(2 * kThreads, 1) void s2k5_fwd_kernel(S2fArgs a) {
     const int Ho = a.OH, Wo = a.OW, Hi = 2 * Ho, Wi = 2 * Wo;
     STAMP(0);
     if (tid < kMaxM) tabx[tid] = s2_ch_addr(a.x, min(tid, a.C - 1), Hi * Wi);
-    {  // the weight into buffer 1 (first written by the producers after barrier B)
+    {  // the weight into buffer 1 (first written by the producers after barrier B): every
+       // load of the thread in flight at once (a rolled loop paid one round trip per element)
         float* wl = s2f_lds + BAND;
         const int nw = a.M * a.C * 25;
-        for (int e = tid; e < nw; e += 2 * kThreads) {
+        constexpr int UW = (kMaxM * 4 * G * 25 + 2 * kThreads - 1) / (2 * kThreads);
+        float wv[UW];
+#pragma unroll
+        for (int u = 0; u < UW; ++u) {
+            const int e = min(tid + u * 2 * kThreads, nw - 1);
             const int mc = e / 25, t = e - mc * 25, m = mc / a.C, c = mc - m * a.C;
-            wl[e] = gld(a.w, ((int64_t)m * a.wc + c) * 25 + t);
+            wv[u] = gld(a.w, ((int64_t)m * a.wc + c) * 25 + t);
         }
+#pragma unroll
+        for (int u = 0; u < UW; ++u)
+            if (tid + u * 2 * kThreads < nw) wl[tid + u * 2 * kThreads] = wv[u];
     }
     __syncthreads();  // S0: channel addresses, weight copy
 
@@ -909,7 +983,7 @@ __global__ __launch_bounds__(2 * kThreads, 1) void s2k5_fwd_kernel(S2fArgs a) {
                 const float z = (xv[u][k] - kk[0]) * kk[1] + kk[2];
                 v[k] = ok ? (z > 0.f ? z : z * kk[3]) : 0.f;
             }
-            float* row = Xs + c * kWgPL + rr * kWgRS + 2 * q;
+            float* row = Xs + c * kFwPL + rr * kWgRS + 2 * q;
             *reinterpret_cast<f32x2*>(row) = f32x2{v[0], v[2]};
             *reinterpret_cast<f32x2*>(row + kWgEW) = f32x2{v[1], v[3]};
         }
@@ -946,13 +1020,22 @@ __global__ __launch_bounds__(2 * kThreads, 1) void s2k5_fwd_kernel(S2fArgs a) {
             }
         }
         float bs0[4] = {0.f, 0.f, 0.f, 0.f}, bs1[4] = {0.f, 0.f, 0.f, 0.f}, bs2[4] = {0.f, 0.f, 0.f, 0.f};
+        // st16: the STORE sink's base, image stride and this lane's 4 channel biases
+        float* const obase = uniform_ptr(a.out.s[0].p);
+        const int64_t ons = a.out.s[0].n_stride;
+        float bias[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int m = min(4 * kq + i, a.M - 1);
+            bias[i] = a.st16 && a.out.s[0].bias ? a.out.s[0].bias[m] : 0.f;
+        }
         __syncthreads();  // A
         __syncthreads();  // B
         STAMP(1);
         for (int t = t0; t < t1; ++t) {
             int tn, ty0, tx0;
             tile_of(t, tn, ty0, tx0);
-            const float* const bb = s2f_lds + ((t - t0) & 1) * BAND + kq * kWgPL + 2 * wave * kWgRS + pl + 1;
+            const float* const bb = s2f_lds + ((t - t0) & 1) * BAND + kq * kFwPL + 2 * wave * kWgRS + pl + 1;
             f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
             for (int g = 0; g < G; ++g)
@@ -960,31 +1043,65 @@ __global__ __launch_bounds__(2 * kThreads, 1) void s2k5_fwd_kernel(S2fArgs a) {
                 for (int kh = 0; kh < 5; ++kh)
 #pragma unroll
                     for (int kw = 0; kw < 5; ++kw) {
-                        const float* bp = bb + 4 * g * kWgPL + kh * kWgRS + (kw & 1) * kWgEW + (kw >> 1);
+                        const float* bp = bb + 4 * g * kFwPL + kh * kWgRS + (kw & 1) * kWgEW + (kw >> 1);
 #pragma unroll
                         for (int h = 0; h < 2; ++h)
                             acc[h] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[g][kh * 5 + kw], bp[16 * h], acc[h], 0, 0, 0);
                     }
+            if (t == t0) STAMP(2);
             // epilogue: lane holds D[m = 4kq + i][px = pl] of pixel group h, row ty0 + wave
             const int oy = ty0 + wave;
+            if (a.st16) {
+                // bias + statistics from the registers; the row [16 channels][32 columns] goes
+                // through this wave's LDS slot and leaves as 16-B stores (8 lanes = one 128-B
+                // channel row) — 4-B stores of 16-lane runs made the epilogue store-issue bound
+                float* ob = s2f_lds + 2 * BAND + wave * kFwOut;
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int ox = tx0 + 16 * h + pl;
-                if (oy >= Ho || ox >= Wo) continue;
+                for (int h = 0; h < 2; ++h) {
+                    const bool in = oy < Ho && tx0 + 16 * h + pl < Wo;
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int m = 4 * kq + i;
-                    if (m >= a.M) continue;
-                    float s0 = 0.f, s1 = 0.f, s2 = 0.f;
-                    sink_row_apply(ri[m], tn, (int64_t)oy * Wo + ox, acc[h][i], s0, s1, s2);
-                    bs0[i] += s0;
-                    bs1[i] += s1;
-                    bs2[i] += s2;
+                    for (int i = 0; i < 4; ++i) {
+                        const int m = 4 * kq + i;
+                        const float v = acc[h][i] + bias[i];
+                        ob[m * kWgX + 16 * h + pl] = v;
+                        bs0[i] += in ? v : 0.f;
+                        bs1[i] += in ? v * v : 0.f;
+                    }
+                }
+                // the row is read back as f32x4 by other lanes of this wave: a compiler barrier
+                // keeps those reads after the float stores (different types: no alias assumed)
+                asm volatile("" ::: "memory");
+                if (oy < Ho) {
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+                        const int m = (lane >> 3) + 8 * u, q = lane & 7, ox = tx0 + 4 * q;
+                        if (m < a.M && ox < Wo)
+                            gst4(obase, (int64_t)tn * ons + (int64_t)m * Ho * Wo + (int64_t)oy * Wo + ox,
+                                 *reinterpret_cast<const f32x4*>(&ob[m * kWgX + 4 * q]));
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int ox = tx0 + 16 * h + pl;
+                    if (oy >= Ho || ox >= Wo) continue;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int m = 4 * kq + i;
+                        if (m >= a.M) continue;
+                        float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+                        sink_row_apply(ri[m], tn, (int64_t)oy * Wo + ox, acc[h][i], s0, s1, s2);
+                        bs0[i] += s0;
+                        bs1[i] += s1;
+                        bs2[i] += s2;
+                    }
                 }
             }
+            if (t == t0) STAMP(3);
             __syncthreads();
+            if (t == t0) STAMP(4);
         }
-        STAMP(2);
+        STAMP(5);
         if (sinks_need_red(a.out)) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -1005,7 +1122,7 @@ __global__ __launch_bounds__(2 * kThreads, 1) void s2k5_fwd_kernel(S2fArgs a) {
             sink_row_flush(a.out, tid, r3[0], r3[1], r3[2]);
         }
     }
-    STAMP(3);
+    STAMP(6);
 }
 
 bool down_geom(const isg_conv_geom* g, int& S) {
@@ -1124,6 +1241,10 @@ int32_t isg_s2k5_fwd(const isg_conv_geom* g, const isg_vtensor* x, const float* 
     if ((int64_t)g->H * g->W >= (1ll << 31)) return 0;
     S2fArgs a{};
     a.x = *x; a.w = w; a.out = *out;
+    static const bool no16 = getenv("ISG_S2F_NO16") != nullptr;  // A/B: per-element sink epilogue
+    a.st16 = !no16 && out->nsink == 1 && out->s[0].mode == ISG_SINK_STORE && out->s[0].c0 == 0 &&
+             out->s[0].C == g->Co && g->OW % 4 == 0 && (uintptr_t)out->s[0].p % 16 == 0 &&
+             out->s[0].n_stride % 4 == 0;
     a.N = g->N; a.M = g->Co; a.C = g->Ci; a.wc = g->w_ci ? g->w_ci : g->Ci; a.OH = g->OH; a.OW = g->OW;
     a.tiles_x = (a.OW + kWgX - 1) / kWgX;
     a.tiles_y = (a.OH + kWgRows - 1) / kWgRows;
@@ -1164,7 +1285,7 @@ int32_t isg_s2k5_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_
     if (off || g->groups != 1 || g->SH != 2 || g->SW != 2 || g->KH != 5 || g->KW != 5 ||
         g->PH != 2 || g->PW != 2 || g->DH != 1 || g->DW != 1 || g->H != 2 * g->OH ||
         g->W != 2 * g->OW || g->OW % 4 || g->Co > kMaxM || g->Ci > kMaxM ||
-        (g->w_ci && g->w_ci != g->Ci) || !down_src_ok(x) || !down_src_ok(dy))
+        (g->w_ci && g->w_ci < g->Ci) || !down_src_ok(x) || !down_src_ok(dy))
         return 0;
     // the kernel's branch-free transforms: x PLAIN / BN_FWD with any activation, dy PLAIN /
     // BN_BWD without one
@@ -1177,7 +1298,7 @@ int32_t isg_s2k5_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_
     a.dy = *dy; a.x = *x; a.dw = dw; a.dbias = dbias;
     a.rep_stride = nrep > 1 ? rep_stride : 0;
     a.nrep = nrep < 1 ? 1 : nrep;
-    a.N = g->N; a.M = g->Co; a.C = g->Ci; a.OH = g->OH; a.OW = g->OW;
+    a.N = g->N; a.M = g->Co; a.C = g->Ci; a.wc = g->w_ci ? g->w_ci : g->Ci; a.OH = g->OH; a.OW = g->OW;
     static const int dbg = getenv("ISG_S2W_DBG") ? atoi(getenv("ISG_S2W_DBG")) : 0;
     a.dbg = dbg;
     a.tiles_x = (a.OW + kWgX - 1) / kWgX;
@@ -1199,12 +1320,16 @@ int32_t isg_s2k5_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_
     bool yb = false;
     for (int i = 0; i < dy->nseg; ++i) yb |= dy->s[i].xform == ISG_XF_BN_BWD && dy->s[i].y != dy->s[i].p;
     const size_t lds = (size_t)2 * kWgLds * sizeof(float);
-    auto k = yb ? s2k5_wgrad_kernel<true> : s2k5_wgrad_kernel<false>;
-    static bool attr[2] = {false, false};
-    if (!attr[yb]) {
+    static const bool no_narrow = getenv("ISG_NO_S2W_NARROW") != nullptr;  // A/B
+    const bool nar = a.C <= 4 && !no_narrow;
+    auto k = yb ? (nar ? s2k5_wgrad_kernel<true, true> : s2k5_wgrad_kernel<true, false>)
+                : (nar ? s2k5_wgrad_kernel<false, true> : s2k5_wgrad_kernel<false, false>);
+    const int ki = 2 * yb + nar;
+    static bool attr[4] = {false, false, false, false};
+    if (!attr[ki]) {
         if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
             return isg_check_launch("s2k5_wgrad_kernel: dynamic LDS");
-        attr[yb] = true;
+        attr[ki] = true;
     }
     hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(2 * kThreads), lds, st, a);
     const int32_t e = isg_check_launch("s2k5_wgrad_kernel");

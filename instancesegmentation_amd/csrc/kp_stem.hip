@@ -96,6 +96,7 @@ __global__ __launch_bounds__(kThreads) void kp_fwd_kernel(KpArgs a) {
     __shared__ int toff[kMaxKK];
     __shared__ Win wins[kMaxParts];
     __shared__ uint32_t act_mask;
+    __shared__ int jofs[32];
     __shared__ float red[2][4][kMaxCo];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int n = blockIdx.y;
@@ -120,14 +121,16 @@ __global__ __launch_bounds__(kThreads) void kp_fwd_kernel(KpArgs a) {
     {
         float* const wf = reinterpret_cast<float*>(wl);
         int s = 0;
-        for (uint32_t m = mask; m; m &= m - 1, ++s) {
-            const int j = __ffs(m) - 1;
-            for (int i = tid; i < kMaxCo * KK; i += kThreads) {
-                const int co = i / KK, tap = i - co * KK;
-                wf[(s * KK + tap) * kMaxCo + co] =
-                    co < a.Co ? gld(a.w, ((int64_t)co * a.Ci + a.c_kp0 + j) * KK + tap) : 0.f;
-            }
-        }
+        // every part's weights in one gather (their loads in flight together); slot s =
+        // the s-th set bit j of the visible-part mask (table in LDS: a register array with
+        // a runtime index lives in scratch memory)
+        if (tid < 32 && ((mask >> tid) & 1u)) jofs[__popc(mask & ((1u << tid) - 1u))] = tid;
+        __syncthreads();
+        s = __popc(mask);
+        coop_gather<8>(wf, s * KK * kMaxCo, tid, kThreads, a.w, [&](int i) {
+            const int co = i % kMaxCo, r = i / kMaxCo, tap = r % KK, sl = r / KK;
+            return co < a.Co ? (co * a.Ci + a.c_kp0 + jofs[sl]) * KK + tap : -1;
+        });
         for (int t = tid; t < KK; t += kThreads) {
             const int kh = t / a.KW, kw = t - kh * a.KW;
             toff[t] = kh * a.DH * a.FW + kw * a.DW;
@@ -239,14 +242,28 @@ __global__ __launch_bounds__(kThreads) void kp_wgrad_kernel(KpArgs a) {
             const int r = i / fw, c = i - r * fw;
             hl[i] = heat(a, w, iy0 + r, ix0 + c);
         }
-        for (int i = tid; i < a.Co * np; i += kThreads) {
-            const int co = i / np, p = i - co * np;
-            const int pr = p / ncol, pc = p - pr * ncol;
-            const int64_t pix = (int64_t)(r0 + pr) * a.OW + ox_lo + pc;
-            const ChT& t = taby[co];
-            const float g = gld(t.p, (int64_t)n * t.ns + pix);
-            const float yv = t.xf == ISG_XF_BN_BWD ? gld(t.y, (int64_t)n * t.yns + pix) : g;
-            dyl[co * kMaxWgPix + p] = ch_xform(t.xf, t.act, t.k, g, yv);
+        // 4 items per thread with their loads in flight together (ChT.y == p unless
+        // BatchNorm backward, so the second load needs no branch)
+        for (int i0 = tid; i0 < a.Co * np; i0 += 4 * kThreads) {
+            float g[4], yv[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int i = min(i0 + u * kThreads, a.Co * np - 1);
+                const int co = i / np, p = i - co * np;
+                const int pr = p / ncol, pc = p - pr * ncol;
+                const int64_t pix = (int64_t)(r0 + pr) * a.OW + ox_lo + pc;
+                const ChT& t = taby[co];
+                g[u] = gld(t.p, (int64_t)n * t.ns + pix);
+                yv[u] = gld(t.y, (int64_t)n * t.yns + pix);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int i = i0 + u * kThreads;
+                if (i >= a.Co * np) continue;
+                const int co = i / np, p = i - co * np;
+                const ChT& t = taby[co];
+                dyl[co * kMaxWgPix + p] = ch_xform(t.xf, t.act, t.k, g[u], yv[u]);
+            }
         }
         __syncthreads();
 #pragma unroll

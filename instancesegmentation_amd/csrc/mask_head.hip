@@ -36,8 +36,6 @@ constexpr int DY = TY + 6, DX = TX + 6;   // dlogits region (backward)         3
 constexpr int DXS = DX;
 constexpr int GY = TY + 4, GX = TX + 4;   // intermediate-gradient region       36 x 68
 constexpr int GJY = GY / 4, GJX = GX / 4; // per phase: 9 x 17
-constexpr int GPL = 16 * GJY * GJX;       // one channel, phase-split             2448
-constexpr int IPL = IY * IXS;             // one channel of the intermediate      2278
 constexpr int kW1 = kCi * kCm * 64;       // convT weights [16][4][8][8]
 
 // the input region of the tile whose top-left intermediate pixel is (Y0, X0), transformed,

@@ -150,13 +150,11 @@ __global__ __launch_bounds__(kThreads) void tap_conv_kernel(TapArgs a) {
         if (r < a.M) q = sink_row(a.out, r, (int64_t)a.DstH * a.DstW);
         ri[r] = q;
     }
-    for (int f = tid; f < a.ws_floats; f += kThreads) {
+    coop_gather<8>(Ws, a.ws_floats, tid, kThreads, a.w, [&](int f) {
         const int c = f / a.WCS, rem = f - c * a.WCS;
         const int k = rem / MP, m = rem - k * MP;
-        float x = 0.f;
-        if (m < a.M && c < a.C && k < a.KK) x = gld(a.w, (int64_t)m * a.wm + (int64_t)c * a.wc + k);
-        Ws[f] = x;
-    }
+        return (m < a.M && c < a.C && k < a.KK) ? m * a.wm + c * a.wc + k : -1;
+    });
     __syncthreads();
 
     // per-group pixel (16 consecutive pixels of the tile in row-major order) and LDS base

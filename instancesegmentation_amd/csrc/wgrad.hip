@@ -577,10 +577,16 @@ int32_t pwg_try(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor
     };
     // narrower column blocks while the grid would not cover the CUs
     while (bc > 32 && a.ntiles * gy_of(bc) < 256) bc = (bc / 2 + 15) / 16 * 16;
+    // experiments (tools/kbench): block shape overrides
+    static const int env_br = getenv("ISG_PWG_BR") ? atoi(getenv("ISG_PWG_BR")) : 0;
+    static const int env_bc = getenv("ISG_PWG_BC") ? atoi(getenv("ISG_PWG_BC")) : 0;
+    if (env_br >= 16 && env_br % 16 == 0 && env_br <= 64) br = std::min(env_br, (a.R + 15) / 16 * 16);
+    if (env_bc >= 16 && env_bc % 16 == 0) bc = std::min(std::min(env_bc, kGMaxRows - br), (a.C + 15) / 16 * 16);
     a.BR = br; a.BC = bc;
     a.ncb = (a.C + bc - 1) / bc;
     const int64_t gy = gy_of(bc);
-    int64_t gx = std::max<int64_t>(1, 512 / gy);
+    static const int env_wgs = getenv("ISG_PWG_WGS") ? atoi(getenv("ISG_PWG_WGS")) : 512;
+    int64_t gx = std::max<int64_t>(1, env_wgs / gy);
     if (gx > a.ntiles) gx = a.ntiles;
     a.tiles_per_block = (a.ntiles + gx - 1) / gx;
     // at least 2 tiles per workgroup: half the dW atomics, and — these kernels run on the

@@ -121,11 +121,12 @@ class InstanceSegmenter:
         self.plan.fwd.run(self.table, st)
         L.check(lib.isg_sigmoid_fwd(self.logits.data_ptr(), self.prob.data_ptr(),
                                     self.prob.numel(), st), "sigmoid")
-        L.check(lib.isg_mask_paste(self.prob.data_ptr(), K, S, self.windows.data_ptr(),
-                                   self.H, self.W, self.masks.data_ptr(), st), "mask_paste")
-        L.check(lib.isg_mask_nms(self.masks.data_ptr(), K, self.H, self.W, self.iou_thr,
-                                 self.work.data_ptr(), self.scores.data_ptr(),
-                                 self.keep.data_ptr(), self.nkeep.data_ptr(), st), "mask_nms")
+        # paste-back and the NMS bit-packing in one pass over the canvases (A13 + A14)
+        L.check(lib.isg_mask_paste_nms(self.prob.data_ptr(), K, S, self.windows.data_ptr(),
+                                       self.H, self.W, self.iou_thr, self.masks.data_ptr(),
+                                       self.work.data_ptr(), self.scores.data_ptr(),
+                                       self.keep.data_ptr(), self.nkeep.data_ptr(), st),
+                "mask_paste_nms")
 
     def load(self, image, boxes, keypoints):
         """Copy one image's inputs into the static buffers (no launch).

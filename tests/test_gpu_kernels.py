@@ -193,18 +193,23 @@ def test_s2k5_fwd(cfg):
 
 
 @pytest.mark.parametrize("cfg", [(16, 16, 512, 512), (16, 16, 134, 200), (12, 10, 72, 200),
-                                 (3, 16, 64, 48)],
-                         ids=["stem_bench", "ragged", "narrow_partial_rows", "three_channels"])
+                                 (3, 16, 64, 48), (3, 16, 1024, 1024, 20), (4, 12, 40, 72)],
+                         ids=["stem_bench", "ragged", "narrow_partial_rows", "three_channels",
+                              "stem_rgb_layer1_wci20", "four_channels_ragged"])
 def test_s2k5_wgrad(cfg):
     """The LDS-staged 5x5 s2 weight gradient (down_conv.hip s2k5_wgrad_kernel, the stem's
     layer 2 on the bench step) through the replicated entry point, against fp64: dy with
     training-mode BatchNorm backward rebuilt on load, x with BatchNorm + PReLU on load, the
     dbias, at the bench geometry (2x512^2 -> 256^2, 1024 tiles over persistent workgroups),
     a partial last column tile, a partial last row tile with fewer than 16 channels on both
-    sides, and 3 input channels."""
-    Ci, Co, H, W = cfg
+    sides, and 3-4 input channels (the narrow form: channels x taps in the MFMA's N), incl.
+    the keypoint stem's RGB layer 1 whose weight spans w_ci = 20 channels."""
+    Ci, Co, H, W = cfg[:4]
+    wci = cfg[4] if len(cfg) > 4 else Ci
     N = 2
     ge, OH, OW = _geom(N, Ci, Co, H, W, 5, 2, 2, 1)
+    if wci != Ci:
+        ge["w_ci"] = wci
     x = rnd(N, Ci, H, W, seed=51)
     gamma, beta, rm, rv, slope = bn_eval_params(Ci, 52)
     xt = fwd_xform_ref(x, gamma, beta, rm, rv, slope, "prelu")
@@ -219,15 +224,20 @@ def test_s2k5_wgrad(cfg):
     Yr, Gb, GA, BE, ST = cuda32(yraw), cuda32(gbn), cuda32(og), cuda32(ob), rep_from(st)
     dyseg = {"p": ptr(Gb), "y": ptr(Yr), "n_stride": Co * OH * OW, "y_n_stride": Co * OH * OW,
              "C": Co, "xform": L.XF_BN_BWD, "bn": bn_spec_train(GA, BE, ST, N * OH * OW)}
-    nw = Co * Ci * 25
+    nw = Co * wci * 25
     stride_ = nw + Co + 5
     REP = torch.zeros(L.WREP * stride_, device=DEV)
+    dbias_p = ptr(REP[nw:]) if wci == Ci else 0  # the partial-weight entry takes no bias
     call("isg_conv_wgrad_rep", geom(**ge), vt([dyseg], N, OH, OW), vt([xseg], N, H, W),
-         ptr(REP), ptr(REP[nw:]), stride_, L.WREP, stream())
+         ptr(REP), dbias_p, stride_, L.WREP, stream())
     OUT = torch.full((stride_,), float("nan"), device=DEV)
     call("isg_sum_replicas", ptr(OUT), ptr(REP), stride_, L.WREP, stride_, stream())
     torch.cuda.synchronize()
-    close(OUT[:nw].view(Co, Ci, 5, 5), ref, what="s2k5 wgrad")
+    full = OUT[:nw].view(Co, wci, 5, 5)
+    close(full[:, :Ci], ref, what="s2k5 wgrad")
+    if wci != Ci:
+        assert torch.all(full[:, Ci:] == 0)  # the other weight channels are not touched
+        return
     # the BatchNorm-backward dy sums to ~0 per channel: the dbias bar is relative to the
     # summed magnitudes (one fp32 rounding per partial over 2 x 256^2 terms)
     derr = (OUT[nw:nw + Co].double().cpu() - dy.sum((0, 2, 3))).abs().max().item()
@@ -601,6 +611,17 @@ def _paste_nms_gpu(prob, boxes, H, W, thr):
     keep = torch.full((K,), -1, dtype=torch.int32, device=DEV)
     nk = torch.zeros(1, dtype=torch.int32, device=DEV)
     call("isg_mask_nms", ptr(O), K, H, W, thr, ptr(work), ptr(sc), ptr(keep), ptr(nk), stream())
+    # the product path's fused form (paste + NMS bit-packing in one pass) must agree bit
+    # for bit with the two-call form
+    O2 = torch.full((K, H, W), 77, dtype=torch.uint8, device=DEV)
+    work2 = torch.full((max(ws, 1),), 0xAB, dtype=torch.uint8, device=DEV)
+    sc2 = torch.empty(K, dtype=torch.float32, device=DEV)
+    keep2 = torch.full((K,), -1, dtype=torch.int32, device=DEV)
+    nk2 = torch.zeros(1, dtype=torch.int32, device=DEV)
+    call("isg_mask_paste_nms", ptr(P), K, S, ptr(B), H, W, thr, ptr(O2), ptr(work2), ptr(sc2),
+         ptr(keep2), ptr(nk2), stream())
+    assert torch.equal(O2, O) and torch.equal(sc2, sc) and nk2.item() == nk.item()
+    assert torch.equal(keep2[:nk.item()], keep[:nk.item()])
     return O.cpu().numpy(), sc.cpu().numpy(), keep.cpu().numpy()[:nk.item()]
 
 
