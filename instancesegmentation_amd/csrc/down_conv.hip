@@ -654,9 +654,8 @@ ISG_DEV f32x4 s2_coef_dy(const isg_vtensor& vt, int c, int hw) {
 // NARROW (C <= 4, the RGB layer 1): the 25 taps x C channels go into the MFMA's N dimension
 // instead — B[px][n = (c, tap)], 5 N-tiles of 16 (75 used) — so a pixel quad costs 5 MFMAs,
 // not 25 with 13 of every 16 columns zero.
-constexpr int kNarN = 5;                  // N-tiles of the narrow form
-constexpr int kNarNW = kMaxM * 16 * kNarN;  // its per-workgroup partial
-template <bool YB, bool NARROW>
+// NT: N-tiles of the narrow form (5 for C <= 3, 7 for C = 4; 0 = the wide form)
+template <bool YB, int NT>
 __global__ __launch_bounds__(2 * kThreads, 1) void s2k5_wgrad_kernel(S2wArgs a) {
     extern __shared__ __attribute__((aligned(16))) float s2w_lds[];  // 2 x [Xs | Ds]
     __shared__ S2Ch tabx[kMaxM];
@@ -670,6 +669,9 @@ __global__ __launch_bounds__(2 * kThreads, 1) void s2k5_wgrad_kernel(S2wArgs a) 
     const int kq = lane >> 4, pl = lane & 15;
     const bool producer = wave >= 4;
     const int ptid = tid - kThreads;
+    constexpr bool NARROW = NT > 0;
+    constexpr int kNarN = NARROW ? NT : 1;
+    constexpr int kNarNW = kMaxM * 16 * kNarN;  // the narrow form's per-workgroup partial
     const int G = gridDim.x, b = blockIdx.x;
     const int L = (G % 8 == 0) ? (b % 8) * (G / 8) + b / 8 : b;  // XCD-grouped runs
     const int t0 = L * a.tpw, t1 = min(t0 + a.tpw, a.ntiles);
@@ -1259,10 +1261,11 @@ int32_t isg_s2k5_fwd(const isg_conv_geom* g, const isg_vtensor* x, const float* 
             cus = 256;
     }
     static const int env_wg = getenv("ISG_S2F_WGS") ? atoi(getenv("ISG_S2F_WGS")) : 0;
-    const int target = env_wg > 0 ? env_wg : cus;  // one 8-wave workgroup per CU (LDS 2 x 51 KB)
+    const int target = env_wg > 0 ? env_wg : cus;  // one 8-wave workgroup per CU (LDS 2 x 52 KB + 8 KB)
     a.tpw = (int)std::max<int64_t>(1, (nt + target - 1) / target);
     const int grid = (int)((nt + a.tpw - 1) / a.tpw);
-    const size_t lds = (size_t)2 * kMaxM * kWgPL * sizeof(float);
+    // two bands + the four consumer waves' output rows (st16 epilogue)
+    const size_t lds = ((size_t)2 * kMaxM * kFwPL + 4 * kFwOut) * sizeof(float);
     const int G = (a.C + 3) / 4;
     auto k = G == 1 ? s2k5_fwd_kernel<1> : G == 2 ? s2k5_fwd_kernel<2> : G == 3 ? s2k5_fwd_kernel<3>
                                                                                 : s2k5_fwd_kernel<4>;
@@ -1321,11 +1324,11 @@ int32_t isg_s2k5_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_
     for (int i = 0; i < dy->nseg; ++i) yb |= dy->s[i].xform == ISG_XF_BN_BWD && dy->s[i].y != dy->s[i].p;
     const size_t lds = (size_t)2 * kWgLds * sizeof(float);
     static const bool no_narrow = getenv("ISG_NO_S2W_NARROW") != nullptr;  // A/B
-    const bool nar = a.C <= 4 && !no_narrow;
-    auto k = yb ? (nar ? s2k5_wgrad_kernel<true, true> : s2k5_wgrad_kernel<true, false>)
-                : (nar ? s2k5_wgrad_kernel<false, true> : s2k5_wgrad_kernel<false, false>);
-    const int ki = 2 * yb + nar;
-    static bool attr[4] = {false, false, false, false};
+    const int nar = no_narrow || a.C > 4 ? 0 : a.C <= 3 ? 1 : 2;
+    auto k = yb ? (nar == 1 ? s2k5_wgrad_kernel<true, 5> : nar == 2 ? s2k5_wgrad_kernel<true, 7> : s2k5_wgrad_kernel<true, 0>)
+                : (nar == 1 ? s2k5_wgrad_kernel<false, 5> : nar == 2 ? s2k5_wgrad_kernel<false, 7> : s2k5_wgrad_kernel<false, 0>);
+    const int ki = 3 * yb + nar;
+    static bool attr[6] = {false, false, false, false, false, false};
     if (!attr[ki]) {
         if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
             return isg_check_launch("s2k5_wgrad_kernel: dynamic LDS");

@@ -432,10 +432,10 @@ static_assert(TX == 64, "the ring correction maps one lane per tile column");
 // the dx of one finished tile (LDS [16 ci][IH][IW]) through the caller's STORE / ACCUM sinks
 template <bool VX>
 ISG_DEV void hb_store_dx(const isg_mask_head& a, const SinkRow* sk, const float* dxs, int n, int iy0,
-                         int ix0) {
+                         int ix0, int tid) {
     using namespace hb;
     if (VX) {
-        for (int i = threadIdx.x; i < kCi * IH * IW / 4; i += kThreads) {
+        for (int i = tid; i < kCi * IH * IW / 4; i += kThreads) {
             const int ci = i >> 5, r = (i >> 2) & 7, qd = i & 3;
             const int iy = iy0 + r, ix = ix0 + 4 * qd;
             const SinkRow& q = sk[ci];
@@ -445,7 +445,7 @@ ISG_DEV void hb_store_dx(const isg_mask_head& a, const SinkRow* sk, const float*
             gst4(q.p, off, q.mode == ISG_SINK_ACCUM ? gld4(q.p, off) + v : v);
         }
     } else {
-        for (int i = threadIdx.x; i < kCi * IH * IW; i += kThreads) {
+        for (int i = tid; i < kCi * IH * IW; i += kThreads) {
             const int ci = i >> 7, r = (i >> 4) & 7, c = i & 15;
             const int iy = iy0 + r, ix = ix0 + c;
             const SinkRow& q = sk[ci];
@@ -491,7 +491,7 @@ ISG_DEV HbSrc hb_src(const VtLite& l, int Hi, int Wi) {
 }
 
 ISG_DEV void hb_issue(const HbSrc& hs, const float* dout0, int64_t dns, int n, int Y0, int X0,
-                      HbPrefetch& f) {
+                      HbPrefetch& f, int tid) {
     using namespace hb;
     const int OH = 4 * hs.Hi, OW = 4 * hs.Wi, iy0 = Y0 / 4, ix0 = X0 / 4;
     const int hw = hs.Hi * hs.Wi;
@@ -499,7 +499,7 @@ ISG_DEV void hb_issue(const HbSrc& hs, const float* dout0, int64_t dns, int n, i
     int ok = 0;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-        const int i = threadIdx.x + k * kThreads;
+        const int i = tid + k * kThreads;
         const int r = i / DNQ, qd = i - r * DNQ;
         const int oy = Y0 - 3 + r, ox = X0 - 4 + 4 * qd;
         const bool in = (i < DSH * DNQ) & (oy >= 0) & (oy < OH) & (ox >= 0) & (ox < OW);
@@ -510,7 +510,7 @@ ISG_DEV void hb_issue(const HbSrc& hs, const float* dout0, int64_t dns, int n, i
     for (int k = 0; k < 4; ++k) {
         // opaque: recompute the per-lane channel addressing per tile instead of keeping 4
         // 64-bit offsets live across the whole tile loop (they spilled)
-        const int i = opaque(threadIdx.x + k * kThreads);
+        const int i = opaque(tid + k * kThreads);
         const int ci = i / (TSH * TSW / 4), rem = i - ci * (TSH * TSW / 4);
         const int r = rem / (TSW / 4), qd = rem - r * (TSW / 4);
         const int iy = iy0 - 1 + r, ix = ix0 - 4 + 4 * qd;
@@ -528,12 +528,12 @@ ISG_DEV void hb_issue(const HbSrc& hs, const float* dout0, int64_t dns, int n, i
     f.ok = ok;
 }
 
-ISG_DEV void hb_commit(const HbPrefetch& f, const XfLin* xl, float* Ts, float* Ds, float& db2) {
+ISG_DEV void hb_commit(const HbPrefetch& f, const XfLin* xl, float* Ts, float* Ds, float& db2, int tid) {
     using namespace hb;
     const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-        const int i = threadIdx.x + k * kThreads;
+        const int i = tid + k * kThreads;
         if (i < DSH * DNQ) {
             const int r = i / DNQ, qd = i - r * DNQ;
             const f32x4 v = (f.ok >> k) & 1 ? f.dl[k] : zero;
@@ -543,7 +543,7 @@ ISG_DEV void hb_commit(const HbPrefetch& f, const XfLin* xl, float* Ts, float* D
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        const int i = threadIdx.x + k * kThreads;
+        const int i = tid + k * kThreads;
         if (i < kCi * TSH * TSW / 4) {
             const int ci = i / (TSH * TSW / 4), rem = i - ci * (TSH * TSW / 4);
             // outside the image the convT input is zero padding, not transform(0)
@@ -557,53 +557,68 @@ ISG_DEV void hb_commit(const HbPrefetch& f, const XfLin* xl, float* Ts, float* D
     }
 }
 
+// One 512-thread workgroup per CU: two halves of 4 waves, each with its own tile in flight
+// and its own LDS tile buffers (2 x 77 KB), sharing the tables and combining their dW1 / Z'
+// / bias partials in LDS before the atomics — half the replica atomics of two 256-thread
+// workgroups (4096 per workgroup: ~6 us of chip-wide atomic throughput at 512 of them)
+// and one weight / table setup per 4 tiles instead of per 2.
 template <bool VX>
-__global__ __launch_bounds__(kThreads, 2) void head_bwd_kernel(isg_mask_head a, int ntx, int nty,
-                                                               int ntiles) {
+__global__ __launch_bounds__(2 * kThreads, 1) void head_bwd_kernel(isg_mask_head a, int ntx, int nty,
+                                                                   int ntiles) {
     using namespace hb;
-    __shared__ __attribute__((aligned(16))) float Ts[kCi * TSP];
-    __shared__ __attribute__((aligned(16))) float Ds[DSH * DSW];
-    __shared__ __attribute__((aligned(16))) float Xc[kCm * 16 * NCELL];  // dI, phase-split
-    __shared__ __attribute__((aligned(16))) float dxs[kCi * IH * IW];
-    __shared__ float ring[kCm * RING];
+    __shared__ __attribute__((aligned(16))) float Ts_[2][kCi * TSP];
+    __shared__ __attribute__((aligned(16))) float Ds_[2][DSH * DSW];
+    __shared__ __attribute__((aligned(16))) float Xc_[2][kCm * 16 * NCELL];  // dI, phase-split
+    __shared__ __attribute__((aligned(16))) float dxs_[2][kCi * IH * IW];
+    __shared__ float ring_[2][kCm * RING];
+    __shared__ float Cs_[2][kCm * 9];
+    __shared__ float red_[2][kCm * 4 + 4];
     __shared__ __attribute__((aligned(16))) float w2s[kCm * 9];
     __shared__ ChanCoef coef[kCi];
     __shared__ XfLin xl[kCi];
     __shared__ SinkRow sk[kCi];
-    __shared__ float Cs[kCm * 9];
-    __shared__ float red[kCm * 4 + 4];
     const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane((int)(tid >> 6));
+    const int h = __builtin_amdgcn_readfirstlane((int)(tid >> 8)), ht = tid & (kThreads - 1);
+    const int wave = __builtin_amdgcn_readfirstlane((int)((tid >> 6) & 3));
+    float* const Ts = Ts_[h];
+    float* const Ds = Ds_[h];
+    float* const Xc = Xc_[h];
+    float* const dxs = dxs_[h];
+    float* const ring = ring_[h];
+    float* const Cs = Cs_[h];
+    float* const red = red_[h];
     const int kq = lane >> 4, nl = lane & 15, aa = kq >> 1, bb = kq & 1;
     const int OH = 4 * a.Hi, OW = 4 * a.Wi;
     const int64_t hw = (int64_t)a.Hi * a.Wi;
     const int64_t rn = ISG_HEAD_RING(a.Hi, a.Wi);
+    const int nb = 2 * (int)gridDim.x;                                  // tile stride
+    const int nk = (ntiles - 2 * (int)blockIdx.x + nb - 1) / nb;        // half 0's count (>= half 1's)
     STAMP(0);
     const VtLite vl = vt_lite(a.x);
     const HbSrc hs = hb_src(vl, a.Hi, a.Wi);
     const float* dout0 = sgpr_p(a.dout);
     const int64_t dns = a.dout_n_stride;
-    f32x4 w1r[kW1 / 4 / kThreads];  // the convT weight, issued first: its LDS copy below
-#pragma unroll                       // then waits for these loads only
-    for (int k = 0; k < kW1 / 4 / kThreads; ++k) w1r[k] = gld4(a.w1, 4 * (tid + k * kThreads));
-    HbPrefetch pf;
-    if (VX && (int)blockIdx.x < ntiles) {  // the first tile's loads overlap the setup below
-        const int t2 = blockIdx.x % (ntx * nty);
-        hb_issue(hs, dout0, dns, blockIdx.x / (ntx * nty), (t2 / ntx) * TY, (t2 % ntx) * TX, pf);
-    }
-    load_vt_coefs(a.x, coef, tid, kThreads);
+    constexpr int NW1 = kW1 / 4 / (2 * kThreads);
+    f32x4 w1r[NW1];  // the convT weight, issued first: its LDS copy below waits for these only
 #pragma unroll
-    for (int k = 0; k < kW1 / 4 / kThreads; ++k) reinterpret_cast<f32x4*>(Xc)[tid + k * kThreads] = w1r[k];
+    for (int k = 0; k < NW1; ++k) w1r[k] = gld4(a.w1, 4 * (tid + k * 2 * kThreads));
+    HbPrefetch pf;
+    const int tile0 = 2 * (int)blockIdx.x + h;
+    if (VX && tile0 < ntiles) {  // the first tile's loads overlap the setup below
+        const int t2 = tile0 % (ntx * nty);
+        hb_issue(hs, dout0, dns, tile0 / (ntx * nty), (t2 / ntx) * TY, (t2 % ntx) * TX, pf, ht);
+    }
+    load_vt_coefs(a.x, coef, tid, 2 * kThreads);
+#pragma unroll
+    for (int k = 0; k < NW1; ++k) reinterpret_cast<f32x4*>(Xc_[0])[tid + k * 2 * kThreads] = w1r[k];
     if (tid < kCi) {
         SinkRow q = {};
         q.mode = ISG_SINK_NONE;
         if (a.dx.nsink > 0) q = sink_row(a.dx, tid, hw);
         sk[tid] = q;
     }
-    if (tid < kCm * 9) {
-        Cs[tid] = 0.f;
-        w2s[tid] = a.w2[tid];
-    }
+    if (tid < kCm * 9) w2s[tid] = a.w2[tid];
+    if (tid < 2 * kCm * 9) Cs_[tid / (kCm * 9)][tid % (kCm * 9)] = 0.f;
     __syncthreads();
     if (tid < kCi) {
         const int c1 = vl.c1, c2 = vl.c2;
@@ -617,7 +632,7 @@ __global__ __launch_bounds__(kThreads, 2) void head_bwd_kernel(isg_mask_head a, 
 #pragma unroll
     for (int o = 0; o < 64; ++o) {
         const int co = o >> 4, r = (o >> 2) & 3, s = o & 3;
-        wdA[o] = Xc[((nl * kCm + co) * 8 + r + 4 * (1 - aa)) * 8 + s + 4 * (1 - bb)];
+        wdA[o] = Xc_[0][((nl * kCm + co) * 8 + r + 4 * (1 - aa)) * 8 + s + 4 * (1 - bb)];
     }
     // Z' N-tiles of this wave: 2 wave, 2 wave + 1 (of 7); column d = (dy, dx) of this lane
     // as a Ds offset
@@ -643,20 +658,27 @@ __global__ __launch_bounds__(kThreads, 2) void head_bwd_kernel(isg_mask_head a, 
     int pn = -1, piy0 = 0, pix0 = 0;  // the tile whose dx sits in dxs
     STAMP(1);
 
-    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const int n = tile / (ntx * nty), t2 = tile - n * ntx * nty;
+    int tile = tile0;
+    for (int kt = 0; kt < nk; ++kt, tile += nb) {
+        // both halves run nk iterations (the workgroup-wide barriers); half 1's last one
+        // may have no tile
+        const bool act = tile < ntiles;
+        const int tc = act ? tile : 0;
+        const int n = tc / (ntx * nty), t2 = tc - n * ntx * nty;
         const int Y0 = (t2 / ntx) * TY, X0 = (t2 % ntx) * TX;
         const int iy0 = Y0 / 4, ix0 = X0 / 4;
         const bool top = Y0 == 0, bot = Y0 + TY >= OH, lft = X0 == 0, rgt = X0 + TX >= OW;
         const bool border = top || bot || lft || rgt;
         __syncthreads();  // the previous tile's LDS reads are done (tables and wdA ready)
-        if (pn >= 0) hb_store_dx<VX>(a, sk, dxs, pn, piy0, pix0);
+        if (pn >= 0) hb_store_dx<VX>(a, sk, dxs, pn, piy0, pix0, ht);
+        pn = -1;
         // ---- staging: dlogits (+ own sum), input region, the ring (border tiles)
-        if (VX) {
-            hb_commit(pf, xl, Ts, Ds, db2);
+        if (!act) {
+        } else if (VX) {
+            hb_commit(pf, xl, Ts, Ds, db2, ht);
         } else {
             const float* dout = a.dout + (int64_t)n * a.dout_n_stride;
-            for (int i = tid; i < DSH * DSW; i += kThreads) {
+            for (int i = ht; i < DSH * DSW; i += kThreads) {
                 const int r = i / DSW, c = i - r * DSW;
                 const int oy = Y0 - 3 + r, ox = X0 - 4 + c;
                 float v = 0.f;
@@ -664,7 +686,7 @@ __global__ __launch_bounds__(kThreads, 2) void head_bwd_kernel(isg_mask_head a, 
                 Ds[i] = v;
                 if (r >= 3 && r < 3 + TY && c >= 4 && c < 4 + TX) db2 += v;
             }
-            for (int i = tid; i < kCi * TSP; i += kThreads) {
+            for (int i = ht; i < kCi * TSP; i += kThreads) {
                 const int ci = i / TSP, r = (i / TSW) % TSH, c = i % TSW;
                 const int iy = iy0 - 1 + r, ix = ix0 - 4 + c;
                 float v = 0.f;
@@ -673,9 +695,9 @@ __global__ __launch_bounds__(kThreads, 2) void head_bwd_kernel(isg_mask_head a, 
                 Ts[i] = v;
             }
         }
-        if (border) {
+        if (act && border) {
             const float* rg = a.ring + (int64_t)n * kCm * rn;
-            for (int it = tid; it < kCm * RING; it += kThreads) {
+            for (int it = ht; it < kCm * RING; it += kThreads) {
                 const int co = it / RING, e = it - co * RING;
                 float v = 0.f;
                 if (e < 2 * RT) {  // top / bottom rows, corners included
@@ -691,17 +713,17 @@ __global__ __launch_bounds__(kThreads, 2) void head_bwd_kernel(isg_mask_head a, 
             }
         }
         __syncthreads();
-        if (pn < 0) STAMP(2);
+        if (kt == 0) STAMP(2);
         // ---- the next tile's loads, in flight during this tile's compute
-        if (VX && tile + (int)gridDim.x < ntiles) {
-            const int nt = tile + gridDim.x, nn = nt / (ntx * nty), nt2 = nt - nn * ntx * nty;
-            hb_issue(hs, dout0, dns, nn, (nt2 / ntx) * TY, (nt2 % ntx) * TX, pf);
+        if (VX && tile + nb < ntiles) {
+            const int nt = tile + nb, nn = nt / (ntx * nty), nt2 = nt - nn * ntx * nty;
+            hb_issue(hs, dout0, dns, nn, (nt2 / ntx) * TY, (nt2 % ntx) * TX, pf, ht);
         }
-        if (pn < 0) STAMP(3);
+        if (kt == 0) STAMP(3);
         // ---- intermediate gradient over the cell region (origin (Y0 - 2, X0 - 2)):
         //      dI[co][q] = sum_{ty,tx} w2[co][ty][tx] dl[q + 1 - ty][q + 1 - tx], zero outside
         //      the image, stored phase-split Xc[((co * 4 + r) * 4 + s) * NCELL + cy * CX + cx]
-        for (int it = tid; it < NDI; it += kThreads) {
+        for (int it = act ? ht : NDI; it < NDI; it += kThreads) {
             const int ql = it / CX, cx = it - ql * CX;
             const int cy = ql >> 2, r = ql & 3;
             const int qy = Y0 - 2 + ql;
@@ -740,7 +762,8 @@ __global__ __launch_bounds__(kThreads, 2) void head_bwd_kernel(isg_mask_head a, 
             }
         }
         __syncthreads();
-        if (pn < 0) STAMP(4);
+        if (kt == 0) STAMP(4);
+        if (!act) continue;
         // ---- border tiles: C[co][t] += dl[p] * I_full[p + t - 1] over the pairs whose
         //      intermediate pixel is outside the image (wave = co, lane = tile column / row)
         if (border) {
@@ -816,50 +839,69 @@ __global__ __launch_bounds__(kThreads, 2) void head_bwd_kernel(isg_mask_head a, 
                 if ((st & 3) == 3) asm volatile("" ::: "memory");
             }
         }
-        if (pn < 0) STAMP(5);
+        if (kt == 0) STAMP(5);
         pn = n; piy0 = iy0; pix0 = ix0;
     }
     __syncthreads();
     STAMP(6);
-    if (pn >= 0) hb_store_dx<VX>(a, sk, dxs, pn, piy0, pix0);
-    // ---- once per workgroup: dW1, Z' -> dW2, bias gradients, into replica rep
+    if (pn >= 0) hb_store_dx<VX>(a, sk, dxs, pn, piy0, pix0, ht);
+    // ---- once per workgroup: the halves' partials combined in LDS, then dW1, Z' -> dW2 and
+    //      the bias gradients into replica rep (half 0)
     const int rep = blockIdx.x % a.nrep;
     const int64_t ro = (int64_t)rep * a.rep_stride;
-    if (a.dw1) {
-        float* d = a.dw1 + ro;
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                atomicAdd(&d[(4 * kq + i) * (kCm * 64) + wave * 64 + t * 16 + nl], dw1[t][i]);
-    }
-    float* Zs = Xc;  // [16 ci][ZN]
+    float* const P1 = Xc_[1];            // half 1's dW1 partial [4096]
+    float* const Zs = Xc_[0];            // half 0's Z' [16 ci][ZN]
+    float* const Z1 = Xc_[1] + kW1;      // half 1's Z'
     float v1[kCm];
 #pragma unroll
     for (int co = 0; co < kCm; ++co) v1[co] = wave_sum(db1[co]);
     const float v2 = wave_sum(db2);
+    auto dw1_idx = [&](int t, int i) { return (4 * kq + i) * (kCm * 64) + wave * 64 + t * 16 + nl; };
+    float* const zdst = h ? Z1 : Zs;
 #pragma unroll
     for (int t = 0; t < 2; ++t)
         if (t == 0 || z2)
 #pragma unroll
-            for (int i = 0; i < 4; ++i) Zs[(4 * kq + i) * ZN + 16 * (2 * wave + t) + nl] = zp[t][i];
+            for (int i = 0; i < 4; ++i) zdst[(4 * kq + i) * ZN + 16 * (2 * wave + t) + nl] = zp[t][i];
+    if (h) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) P1[dw1_idx(t, i)] = dw1[t][i];
+    }
     if (lane == 0) {
 #pragma unroll
         for (int co = 0; co < kCm; ++co) red[co * 4 + wave] = v1[co];
         red[kCm * 4 + wave] = v2;
     }
     __syncthreads();
-    const float sdl = (red[kCm * 4] + red[kCm * 4 + 1]) + (red[kCm * 4 + 2] + red[kCm * 4 + 3]);
+    if (h) {
+        __syncthreads();
+        STAMP(7);
+        return;
+    }
+    if (a.dw1) {
+        float* d = a.dw1 + ro;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) atomicAdd(&d[dw1_idx(t, i)], dw1[t][i] + P1[dw1_idx(t, i)]);
+    }
+    auto red2 = [&](int j) {
+        return ((red_[0][j] + red_[0][j + 1]) + (red_[0][j + 2] + red_[0][j + 3])) +
+               ((red_[1][j] + red_[1][j + 1]) + (red_[1][j + 2] + red_[1][j + 3]));
+    };
+    const float sdl = red2(kCm * 4);
     // dW2[co][t] = sum_{ci, ky, kx} W1[ci][co][ky][kx] Z'[ci][(ky - ty + 1, kx - tx + 1)] from
     // the W1 values already in wdA: lane (ci = nl, (a, b) = kq) holds, for plane o = (co, r,
     // s), W1[ci][co][r + 4(1 - a)][s + 4(1 - b)]; wave = co, the 9 taps summed over the wave
     {
         float zr[6][6];  // Z' rows / columns 4(1-a) .. 4(1-a) + 5 of this lane's input channel
-        const float* z = Zs + nl * ZN + 4 * (1 - aa) * ZD + 4 * (1 - bb);
+        const int zo = nl * ZN + 4 * (1 - aa) * ZD + 4 * (1 - bb);
 #pragma unroll
         for (int r = 0; r < 6; ++r)
 #pragma unroll
-            for (int c = 0; c < 6; ++c) zr[r][c] = z[r * ZD + c];
+            for (int c = 0; c < 6; ++c) zr[r][c] = Zs[zo + r * ZD + c] + Z1[zo + r * ZD + c];
         float c9[9];
 #pragma unroll
         for (int t = 0; t < 9; ++t) c9[t] = 0.f;
@@ -884,12 +926,10 @@ __global__ __launch_bounds__(kThreads, 2) void head_bwd_kernel(isg_mask_head a, 
 #pragma unroll
         for (int t = 0; t < 9; ++t) {
             const float v = wave_sum(c9[t]);
-            if (lane == 0 && a.dw2) atomicAdd(a.dw2 + ro + co * 9 + t, v + b1 * sdl - Cs[co * 9 + t]);
+            if (lane == 0 && a.dw2)
+                atomicAdd(a.dw2 + ro + co * 9 + t, v + b1 * sdl - (Cs_[0][co * 9 + t] + Cs_[1][co * 9 + t]));
         }
-        if (lane == 1 && a.db1) {
-            const float s = (red[co * 4] + red[co * 4 + 1]) + (red[co * 4 + 2] + red[co * 4 + 3]);
-            atomicAdd(a.db1 + ro + co, s);
-        }
+        if (lane == 1 && a.db1) atomicAdd(a.db1 + ro + co, red2(co * 4));
         if (tid == 2 && a.db2) atomicAdd(a.db2 + ro, sdl);
     }
     __syncthreads();
@@ -955,15 +995,16 @@ extern "C" int32_t isg_mask_head_bwd(const isg_mask_head* a, isg_stream_t st) {
     const int ntx = (OW + TX - 1) / TX, nty = (OH + TY - 1) / TY;
     const int ntiles = ntx * nty * a->N;
     static const int env = getenv("ISG_HEAD_BWD_GRID") ? atoi(getenv("ISG_HEAD_BWD_GRID")) : 0;
-    const int grid = std::min(ntiles, env > 0 ? env : 512);  // 2 workgroups per CU
+    const int grid_v1 = std::min(ntiles, env > 0 ? env : 512);  // v1: 2 workgroups per CU
+    const int grid = std::min((ntiles + 1) / 2, env > 0 ? env : 256);  // 1 two-tile workgroup per CU
     static const bool v1 = getenv("ISG_HEAD_BWD_V1") && atoi(getenv("ISG_HEAD_BWD_V1"));
     if (v1) {
-        hipLaunchKernelGGL(head_bwd_v1_kernel, dim3(grid), dim3(kThreads), 0, st, *a, ntx, nty, ntiles);
+        hipLaunchKernelGGL(head_bwd_v1_kernel, dim3(grid_v1), dim3(kThreads), 0, st, *a, ntx, nty, ntiles);
         return isg_check_launch("head_bwd_v1_kernel");
     }
     if (head_bwd_vec(a))
-        hipLaunchKernelGGL(head_bwd_kernel<true>, dim3(grid), dim3(kThreads), 0, st, *a, ntx, nty, ntiles);
+        hipLaunchKernelGGL(head_bwd_kernel<true>, dim3(grid), dim3(2 * kThreads), 0, st, *a, ntx, nty, ntiles);
     else
-        hipLaunchKernelGGL(head_bwd_kernel<false>, dim3(grid), dim3(kThreads), 0, st, *a, ntx, nty, ntiles);
+        hipLaunchKernelGGL(head_bwd_kernel<false>, dim3(grid), dim3(2 * kThreads), 0, st, *a, ntx, nty, ntiles);
     return isg_check_launch("head_bwd_kernel");
 }
