@@ -24,6 +24,8 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef const float __attribute__((address_space(1)))* gcfloat_p;
 typedef float __attribute__((address_space(1)))* gfloat_p;
 ISG_DEV float gld(const float* p, int64_t i) { return ((gcfloat_p)p)[i]; }
+typedef const double __attribute__((address_space(1)))* gcdouble_p;
+ISG_DEV double gld_d(const double* p, int64_t i) { return ((gcdouble_p)p)[i]; }
 ISG_DEV void gst(float* p, int64_t i, float v) { ((gfloat_p)p)[i] = v; }
 typedef const f32x4 __attribute__((address_space(1)))* gcf32x4_p;
 // 16-B global load of 4 consecutive floats at p[i..i+3] (p + i 16-B aligned)

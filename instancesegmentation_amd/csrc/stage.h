@@ -338,11 +338,16 @@ ISG_DEV StatLoad<NG> stat_issue(const double* stats, const float* gamma, const f
     }
     const bool on = stats != nullptr;
     const double* sp = on ? stats : reinterpret_cast<const double*>(any);
+    // address = base + q * sq + g * sg: with `on` folded into the strides (not a select per
+    // load) the compiler keeps one load per slot instead of branching into a single shared
+    // load and copying it, whose join waited out every load in flight (vmcnt(0))
+    int sq = on ? 4 * bnC : 0, sg = on ? bnC : 0, s0 = on ? cl : 0;
+    asm volatile("" : "+v"(sq), "+v"(sg), "+v"(s0));
 #pragma unroll
     for (int g = 0; g < NG; ++g)
 #pragma unroll
         for (int q = 0; q < ISG_STAT_REP; ++q)
-            r.v[g][q] = sp[on ? (int64_t)q * 4 * bnC + (int64_t)g * bnC + cl : 0];
+            r.v[g][q] = gld_d(sp, (int64_t)q * sq + (int64_t)g * sg + s0);
     r.gamma = gld(gamma && on ? gamma + cl : any, 0);
     r.beta = gld(beta && on ? beta + cl : any, 0);
     return r;

@@ -547,6 +547,300 @@ int32_t pwg_dispatch(const PwgArgs& a, dim3 grid, size_t lds, int tpw, hipStream
     }
 }
 
+// ---- 1x1 weight gradient of the small maps, K split over the waves (pwk) ----------------
+// At 64^2 / 128^2 (bs2: 8K-32K pixels against a dW of a few thousand elements) pwg_kernel
+// spent three quarters of its time in latency (kbench stamps, 48 -> 128 at 64^2: 3.1 us
+// table / coefficient setup, 3.0 us first tile load, 1.5 us MFMA, 3.2 us atomics). Here a
+// workgroup owns a BR x BC block of dW (BR + BC <= 64 rows: RT x CT tiles of 16 x 16) and
+// super-tiles of 256 pixels. The loads of a super-tile need only kernel arguments for their
+// addresses (row j = wave + 4u is wave-uniform, one 1-KB run per wave and pass), so they
+// are issued BEFORE the BatchNorm coefficients are evaluated and setup shares their round
+// trip. Wave w multiplies pixels [64w, 64w + 64) for ALL the block's tiles (K split over
+// the waves); the four partials meet in LDS, then one atomic per dW element: 4x the pixels
+// per workgroup of pwg's 64-pixel tile at the same grid size — a quarter of its atomics.
+constexpr int kKTP = 256;            // pixels per super-tile
+constexpr int kKS = kKTP + 8;        // LDS row stride (8 mod 64, as pwg)
+constexpr int kKMaxRows = 64;        // BR + BC
+
+struct PwkArgs {
+    isg_vtensor dy, x;
+    float* dw;
+    float* dbias;
+    int64_t rep_stride;
+    int nrep;
+    int HW, R, C, ncb;
+    int fast, stat_on;  // fast: always 1 here (pwk_try)
+    int dbg;            // experiments (ISG_DBG): 1 no slab loads, 2 no coefficient loads, 4 no MFMA
+    int64_t P, ntiles, tiles_per_block;
+};
+
+// A row's staging coefficients when the lane's row may come from either tensor (pwk: the
+// dy rows and the x rows of one wave): the fields are picked per lane FIRST, then ONE set
+// of loads (coef_issue / coef_finish over a picked segment). Two coef_issue calls, one per
+// tensor, let the compiler finish the first tensor's statistics before issuing the second's
+// loads — a second memory round trip in the kernel's prologue.
+ISG_DEV ChanCoef pwk_row_coef(const VtSel& vd, int cdy, const VtSel& vx, int cx, bool is_dy,
+                              bool stat_on) {
+    int cld, clx;
+    const int sd = vt_seg(vd, cdy, cld), sx = vt_seg(vx, cx, clx);
+#define PWK_PICK(f) (is_dy ? ISG_SEL3(sd, f, vd) : ISG_SEL3(sx, f, vx))
+    const float* coef = PWK_PICK(coef);
+    const float* slope = PWK_PICK(slope);
+    const float* p = PWK_PICK(p);
+    const int xf = PWK_PICK(xf), bnC = PWK_PICK(bnC);
+    const double* stats = PWK_PICK(stats);
+    const float* gamma = PWK_PICK(gamma);
+    const float* beta = PWK_PICK(beta);
+    const float count = PWK_PICK(count), eps = PWK_PICK(eps);
+#undef PWK_PICK
+    const int cl = is_dy ? cld : clx;
+    const int idx = xf == ISG_XF_BN_BWD ? bnC + cl : cl;
+    const float* cp = coef ? coef + 4 * (int64_t)idx : p;
+    const float* sp = slope ? slope + cl : p;
+    const bool bn = xf == ISG_XF_BN_FWD || xf == ISG_XF_BN_BWD;
+    const f32x4 f = f32x4{gld(cp, 0), gld(cp, 1), gld(cp, 2), gld(cp, 3)};
+    const float sl = gld(sp, 0);
+    const StatLoad<4> st = stat_issue<4>(bn && !coef ? stats : nullptr, gamma, beta, bnC, cl, p, stat_on);
+    ChanCoef k = {0.f, 1.f, 0.f, 0.f};
+    if (xf == ISG_XF_BN_FWD) {
+        if (coef) {
+            k.c0 = f[0]; k.c1 = f[1]; k.c2 = f[2];
+        } else if (stats) {
+            double mean, rstd;
+            mean_rstd_of(stat_sum(st, 0), stat_sum(st, 1), count, eps, mean, rstd);
+            k = fwd_coef_of(mean, rstd, st.gamma, st.beta, 0.f);
+        }
+        k.c3 = slope ? sl : 0.f;
+    } else if (xf == ISG_XF_BN_BWD) {
+        if (coef) {
+            k = ChanCoef{f[0], f[1], f[2], f[3]};
+        } else {
+            double mean, rstd;
+            mean_rstd_of(stat_sum(st, 0), stat_sum(st, 1), count, eps, mean, rstd);
+            k = bwd_coef_of(mean, rstd, st.gamma, stat_sum(st, 2), stat_sum(st, 3), count);
+        }
+    }
+    return k;
+}
+
+template <int RT, int CT, bool HY>
+__global__ __launch_bounds__(kThreads) void pwk_kernel(PwkArgs a) {
+    constexpr int BR = 16 * RT, BC = 16 * CT, NR = BR + BC, NU = NR / 4, NUY = HY ? BR / 4 : 0;
+    constexpr int NT = RT * CT;
+    static_assert(NR <= kKMaxRows && NR % 4 == 0, "pwk block");
+    __shared__ __attribute__((aligned(16))) float S[kKMaxRows * kKS];
+    __shared__ ChanCoef tabK[kKMaxRows];
+    __shared__ float2 tabN[kKMaxRows];
+    __shared__ ChSrc tabA[kKMaxRows];
+    const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
+    const int kk = lane >> 4, pl = lane & 15;
+    const int rb = blockIdx.y / a.ncb, cb = blockIdx.y - rb * a.ncb;
+    const int r0 = rb * BR, c0 = cb * BC;
+    const int Rb = min(BR, a.R - r0), Cb = min(BC, a.C - c0);
+    STAMP(0);
+    const int64_t rep_off = (int64_t)((blockIdx.x + 7u * blockIdx.y) % (unsigned)a.nrep) * a.rep_stride;
+    const int64_t t0 = (int64_t)blockIdx.x * a.tiles_per_block;
+    const int64_t t1 = min(t0 + a.tiles_per_block, a.ntiles);
+    // ---- per-row tables, wave-local: wave w stages (and transforms) only the rows
+    //      j = w + 4u, so lane u of wave w builds row j's entries and no workgroup barrier
+    //      stands between the table and the first super-tile's loads
+    const int ju = wave + 4 * lane;  // this lane's table row (lane < NU)
+    const bool own = lane < NU;
+    const bool is_dy = ju < BR;
+    const int cdy = r0 + min(ju, Rb - 1), cx = c0 + min(max(ju - BR, 0), Cb - 1);
+    {
+        const VtSel vd = vt_sel(a.dy), vx = vt_sel(a.x);
+        if (own) {
+            const ChSrc ad = ch_addr(vd, cdy, a.HW), ax = ch_addr(vx, cx, a.HW);
+            ChSrc& e = tabA[ju];  // field by field (a select of whole records goes through scratch)
+            e.p = is_dy ? ad.p : ax.p; e.y = is_dy ? ad.y : ax.y;
+            e.ns = is_dy ? ad.ns : ax.ns; e.yns = is_dy ? ad.yns : ax.yns;
+            e.xf = is_dy ? ad.xf : ax.xf; e.act = is_dy ? ad.act : ax.act;
+        }
+    }
+    // the wave's LDS operations complete in order; this keeps the compiler from hoisting
+    // the table reads above the writes
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+    f32x4 v[NU], yv[NUY > 0 ? NUY : 1];
+    bool pv;
+    // row j = wave + 4u of the slab (wave-uniform): j < BR dy channel r0 + j, else x channel
+    // c0 + j - BR (clamped into the block: the repeats are cache hits, zeroed by `live`)
+    auto issue = [&](int64_t tl) {
+        const int64_t pg = tl * kKTP + 4 * lane;
+        pv = pg < a.P;
+        const int n = pv ? (int)(pg / a.HW) : 0;
+        const int pix = pv ? (int)(pg - (int64_t)n * a.HW) : 0;
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+            const ChSrc& t = tabA[wave + 4 * u];
+            if (a.dbg & 1) { v[u] = f32x4{0.f, 0.f, 0.f, 0.f}; continue; }
+            v[u] = gld4(t.p, (int64_t)n * t.ns + pix);
+            if constexpr (HY)
+                if (u < NUY) yv[u < NUY ? u : 0] = gld4(t.y, (int64_t)n * t.yns + pix);
+        }
+    };
+    if (t0 < t1) issue(t0);
+    // the coefficient loads go out behind the slab's (their waits may cover both: one round
+    // trip either way)
+    if (own) {
+        const VtSel vd = vt_sel(a.dy), vx = vt_sel(a.x);
+        const ChSrc& e = tabA[ju];
+        const int xf = e.xf, act = e.act;
+        // finalised coefficients or training-mode statistics only (host check: a.fast)
+        ChanCoef k = (a.dbg & 2) ? ChanCoef{0.f, 1.f, 0.f, 0.f} : pwk_row_coef(vd, cdy, vx, cx, is_dy, a.stat_on != 0);
+        if (xf == ISG_XF_PLAIN) k = ChanCoef{0.f, 1.f, 0.f, 0.f};
+        tabK[ju] = k;
+        const float neg = (xf != ISG_XF_BN_FWD || act == ISG_ACT_NONE) ? 1.f : act == ISG_ACT_RELU ? 0.f : k.c3;
+        tabN[ju] = float2{neg, xf == ISG_XF_BN_BWD ? 1.f : 0.f};
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    STAMP(1);
+
+    f32x4 acc[NT];
+#pragma unroll
+    for (int i = 0; i < NT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const bool do_bias = a.dbias && cb == 0;
+    float bs[BR / 4];
+#pragma unroll
+    for (int u = 0; u < BR / 4; ++u) bs[u] = 0.f;
+    // MFMA operand bases: lane (pl, kk) reads row 16 t + pl, pixels 64 wave + 16 g + 4 kk ..
+    const int kb = 64 * wave + 4 * kk;
+    for (int64_t tl = t0; tl < t1; ++tl) {
+        if (tl > t0) __syncthreads();  // the previous super-tile's operand reads are done
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+            const int j = wave + 4 * u;
+            const bool live = pv && (u < BR / 4 ? j < Rb : j - BR < Cb);
+            const ChanCoef k = tabK[j];
+            const float2 nb = tabN[j];
+            f32x4 o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float x = v[u][e];
+                const float y = (HY && u < NUY) ? yv[u < NUY ? u : 0][e] : x;
+                float zf = (x - k.c0) * k.c1 + k.c2;
+                zf = zf > 0.f ? zf : zf * nb.x;
+                const float zb = k.c0 * x + k.c1 * (y - k.c2) + k.c3;
+                o[e] = live ? (nb.y != 0.f ? zb : zf) : 0.f;
+            }
+            if (u < BR / 4) bs[u] += (o[0] + o[1]) + (o[2] + o[3]);
+            *reinterpret_cast<f32x4*>(&S[j * kKS + 4 * lane]) = o;
+        }
+        __syncthreads();
+        if (tl == t0) STAMP(2);
+        if (tl + 1 < t1) issue(tl + 1);  // under this super-tile's MFMAs
+#pragma unroll
+        for (int g = 0; g < ((a.dbg & 4) ? 0 : 64); g += 16) {
+            f32x4 a4[RT], b4[CT];
+#pragma unroll
+            for (int r = 0; r < RT; ++r) a4[r] = *reinterpret_cast<const f32x4*>(&S[(16 * r + pl) * kKS + kb + g]);
+#pragma unroll
+            for (int c = 0; c < CT; ++c) b4[c] = *reinterpret_cast<const f32x4*>(&S[(BR + 16 * c + pl) * kKS + kb + g]);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int r = 0; r < RT; ++r)
+#pragma unroll
+                    for (int c = 0; c < CT; ++c)
+                        acc[r * CT + c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[r][j], b4[c][j], acc[r * CT + c], 0, 0, 0);
+        }
+    }
+    STAMP(3);
+    // ---- the four waves' partials through LDS, then one atomic per element --------------
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) S[((wave * NT + i) * 4 + r) * 64 + lane] = acc[i][r];
+    __syncthreads();
+    float* const dwr = a.dw + rep_off;
+    {
+        const int r = tid >> 6, l = tid & 63;  // element (tile i, acc slot r, lane l)
+#pragma unroll
+        for (int i = 0; i < NT; ++i) {
+            const int e = (i * 4 + r) * 64 + l;
+            const float s = (S[e] + S[NT * 256 + e]) + (S[2 * NT * 256 + e] + S[3 * NT * 256 + e]);
+            const int row = (i / CT) * 16 + (l >> 4) * 4 + r, col = (i % CT) * 16 + (l & 15);
+            if (row < Rb && col < Cb) atomicAdd(&dwr[(int64_t)(r0 + row) * a.C + c0 + col], s);
+        }
+    }
+    if (do_bias) {
+#pragma unroll
+        for (int u = 0; u < BR / 4; ++u) {
+            const float s = wave_sum(bs[u]);
+            const int j = wave + 4 * u;
+            if (lane == 0 && j < Rb) atomicAdd(&a.dbias[rep_off + r0 + j], s);
+        }
+    }
+    STAMP(4);
+}
+
+template <int RT, int CT, bool HY>
+int32_t pwk_launch(const PwkArgs& a, dim3 grid, hipStream_t st) {
+    hipLaunchKernelGGL((pwk_kernel<RT, CT, HY>), grid, dim3(kThreads), 0, st, a);
+    return isg_check_launch("pwk_kernel");
+}
+
+// returns 1 when launched, 0 when the shape is not for this kernel, <0 on error
+int32_t pwk_try(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, float* dw,
+                float* dbias, int64_t rep_stride, int32_t nrep, hipStream_t st) {
+    static const int env = getenv("ISG_PWK") ? atoi(getenv("ISG_PWK")) : 1;  // 0: pwg only
+    static const int max_rc = getenv("ISG_PWK_MAXRC") ? atoi(getenv("ISG_PWK_MAXRC")) : 65536;
+    if (!env) return 0;
+    const int HW = g->H * g->W;
+    const int64_t P = (int64_t)g->N * HW;
+    if ((int64_t)g->Co * g->Ci > max_rc) return 0;
+    for (int i = 0; i < x->nseg; ++i)  // the x rows' transform is loaded as BN_FWD / plain only
+        if (x->s[i].xform == ISG_XF_BN_BWD) return 0;
+    PwkArgs a{};
+    a.dy = *dy; a.x = *x; a.dw = dw; a.dbias = dbias; a.rep_stride = rep_stride; a.nrep = nrep;
+    a.HW = HW; a.R = g->Co; a.C = g->Ci; a.P = P;
+    a.fast = pwg_fast(*dy) && pwg_fast(*x);
+    if (!a.fast) return 0;  // eval-mode statistics (direct ABI calls): pwg_kernel's fp64 path
+    a.stat_on = 0;
+    for (const isg_vtensor* v : {dy, x})
+        for (int s = 0; s < v->nseg; ++s) {
+            const isg_vseg& q = v->s[s];
+            if ((q.xform == ISG_XF_BN_FWD || q.xform == ISG_XF_BN_BWD) && !q.bn.coef && q.bn.stats) a.stat_on = 1;
+        }
+    const bool hy = pwg_has_y(*dy);
+    { const char* e = getenv("ISG_DBG"); a.dbg = e ? atoi(e) : 0; }
+    // block shape: the fewest slab rows loaded per super-tile over the whole dW
+    static const int shapes[6][2] = {{1, 3}, {3, 1}, {2, 2}, {1, 2}, {2, 1}, {1, 1}};
+    int best = -1;
+    int64_t best_rows = 0;
+    for (int i = 0; i < 6; ++i) {
+        const int br = 16 * shapes[i][0], bc = 16 * shapes[i][1];
+        const int64_t rows = (int64_t)((a.R + br - 1) / br) * ((a.C + bc - 1) / bc) * (br + bc);
+        if (best < 0 || rows < best_rows) { best = i; best_rows = rows; }
+    }
+    static const int env_shape = getenv("ISG_PWK_SHAPE") ? atoi(getenv("ISG_PWK_SHAPE")) : -1;
+    if (env_shape >= 0 && env_shape < 6) best = env_shape;
+    const int RT = shapes[best][0], CT = shapes[best][1];
+    a.ncb = (a.C + 16 * CT - 1) / (16 * CT);
+    const int64_t gy = (int64_t)((a.R + 16 * RT - 1) / (16 * RT)) * a.ncb;
+    a.ntiles = (P + kKTP - 1) / kKTP;
+    static const int env_wgs = getenv("ISG_PWK_WGS") ? atoi(getenv("ISG_PWK_WGS")) : 384;
+    a.tiles_per_block = std::max<int64_t>(1, (gy * a.ntiles) / env_wgs);
+    const int64_t gx = (a.ntiles + a.tiles_per_block - 1) / a.tiles_per_block;
+    if (gy > 65535) return 0;
+    const dim3 grid((unsigned)gx, (unsigned)gy);
+    int32_t rc;
+#define ISG_PWK_CASE(r, c)                                                              \
+    if (RT == r && CT == c)                                                             \
+        rc = hy ? pwk_launch<r, c, true>(a, grid, st) : pwk_launch<r, c, false>(a, grid, st); \
+    else
+    ISG_PWK_CASE(1, 3) ISG_PWK_CASE(3, 1) ISG_PWK_CASE(2, 2) ISG_PWK_CASE(1, 2) ISG_PWK_CASE(2, 1)
+    rc = hy ? pwk_launch<1, 1, true>(a, grid, st) : pwk_launch<1, 1, false>(a, grid, st);
+#undef ISG_PWK_CASE
+    return rc ? rc : 1;
+}
+
 // returns 1 when launched, 0 when the shape is not for this kernel, <0 on error
 int32_t pwg_try(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, float* dw,
                 float* dbias, int64_t rep_stride, int32_t nrep, hipStream_t st) {
@@ -557,6 +851,7 @@ int32_t pwg_try(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor
     if (g->OH != g->H || g->OW != g->W || g->Co < 2) return 0;
     const int HW = g->H * g->W;
     if (!pwg_src_ok(*dy, HW) || !pwg_src_ok(*x, HW)) return 0;
+    if (const int32_t k = pwk_try(g, dy, x, dw, dbias, rep_stride, nrep, st)) return k;
     PwgArgs a{};
     a.dy = *dy; a.x = *x; a.dw = dw; a.dbias = dbias; a.rep_stride = rep_stride; a.nrep = nrep;
     a.HW = HW; a.R = g->Co; a.C = g->Ci;

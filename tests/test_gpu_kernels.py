@@ -328,6 +328,52 @@ def test_conv_wgrad_dense(cfg):
     close(DB, dy.sum((0, 2, 3)), what="dbias")
 
 
+@pytest.mark.parametrize("xmode", ["eval", "train"])
+@pytest.mark.parametrize("cfg", [(48, 128, 20, 24), (128, 48, 16, 16), (40, 20, 12, 36),
+                                 (96, 48, 64, 64), (36, 48, 32, 32), (256, 128, 8, 8)])
+def test_pw_wgrad_bn_bwd(cfg, xmode):
+    """1x1 weight gradient with the train plan's operands: dy = training-mode BatchNorm
+    backward rebuilt on load from (grad, y) and consumer-side statistics, x = BatchNorm +
+    PReLU on load (wgrad.hip pwk_kernel for dW up to 65536 elements — ragged blocks and a
+    partial last super-tile here — pwg_kernel above), into replicas, against fp64."""
+    Ci, Co, H, W = cfg
+    N = 2
+    ge, OH, OW = _geom(N, Ci, Co, H, W, 1, 1, 0, 1)
+    yraw = rnd(N, Co, H, W, seed=51) + 0.3
+    gbn = rnd(N, Co, H, W, seed=52)
+    gamma, beta, st, _ = _bn_train_state(yraw, gbn, 8)
+    dy = _bn_bwd_ref(yraw, gbn, gamma)
+    x = rnd(N, Ci, H, W, seed=53)
+    xg, xb, xrm, xrv, xsl = bn_eval_params(Ci, 54)
+    if xmode == "train":  # batch statistics, finalised by the consumer (the fast path)
+        _, _, xst, _ = _bn_train_state(x, torch.zeros_like(x), 55)
+        xrm, xrv = x.mean((0, 2, 3)), x.var((0, 2, 3), unbiased=False)
+    xt = fwd_xform_ref(x, xg, xb, xrm, xrv, xsl, "prelu")
+    ref = torch.nn.grad.conv2d_weight(xt, (Co, Ci, 1, 1), dy)
+    Yr, Gb, GA, BE, ST = cuda32(yraw), cuda32(gbn), cuda32(gamma), cuda32(beta), rep_from(st)
+    dyseg = {"p": ptr(Gb), "y": ptr(Yr), "n_stride": Co * H * W, "y_n_stride": Co * H * W,
+             "C": Co, "xform": L.XF_BN_BWD, "bn": bn_spec_train(GA, BE, ST, N * H * W)}
+    X = cuda32(x)
+    XG = [cuda32(t) for t in (xg, xb, xrm, xrv, xsl)]
+    xseg = {"p": ptr(X), "n_stride": Ci * H * W, "C": Ci, "xform": L.XF_BN_FWD,
+            "act": L.ACT["prelu"], "slope": ptr(XG[4]), "bn": bn_spec_eval(*XG[:4])}
+    if xmode == "train":
+        XST = rep_from(xst)
+        xseg["bn"] = bn_spec_train(XG[0], XG[1], XST, N * H * W)
+    nw = Co * Ci
+    stride_ = nw + Co + 19
+    REP = torch.zeros(L.WREP * stride_, device=DEV)
+    call("isg_conv_wgrad_rep", geom(**ge), vt([dyseg], N, H, W), vt([xseg], N, H, W),
+         ptr(REP), ptr(REP[nw:]), stride_, L.WREP, stream())
+    OUT = torch.full((stride_,), float("nan"), device=DEV)
+    call("isg_sum_replicas", ptr(OUT), ptr(REP), stride_, L.WREP, stride_, stream())
+    close(OUT[:nw].view(Co, Ci, 1, 1), ref, what="1x1 wgrad (BN-bwd dy)")
+    # the BatchNorm-backward dy sums to ~0 per channel: bar relative to the summed magnitudes
+    derr = (OUT[nw:nw + Co].double().cpu() - dy.sum((0, 2, 3))).abs().max().item()
+    assert derr <= 1e-6 * dy.abs().sum((0, 2, 3)).max().item(), derr
+    assert torch.all(OUT[nw + Co:] == 0)
+
+
 @pytest.mark.parametrize("cfg", [DENSE[0], DENSE[1], DENSE[4], (16, 16, 24, 40, 3, 1, 1, 0)])
 def test_conv_wgrad_replicated(cfg):
     """isg_conv_wgrad_rep adds into L.WREP replicas (the train plan's layout); folding them
