@@ -8,6 +8,7 @@
 #include <cstring>
 #include <string>
 #include <utility>
+#include <deque>
 #include <vector>
 
 #include "../../include/isg.h"
@@ -220,19 +221,20 @@ enum { ISG_OPF_SIDE = 1, ISG_OPF_JOIN = 2, ISG_OPF_FORK_NOW = 4 };  // FORK_NOW:
 // fork / join events of the executor's side streams, per device (created on first use,
 // never destroyed; timing disabled): ev[0] fork, ev[1] join of side stream 0, ev[2] join
 // of side stream 1
-static int32_t side_events(hipEvent_t* fork, hipEvent_t* join, hipEvent_t* join2) {
-    static hipEvent_t ev[64][3];
+constexpr int kForkPool = 16;  // fork events of side-stream batches recorded but not yet launched
+static int32_t side_events(hipEvent_t* join, hipEvent_t* join2, hipEvent_t** forks) {
+    static hipEvent_t ev[64][2 + kForkPool];
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64)
         return isg_set_error(ISG_ERR_HIP, "exec: no device for the side stream");
     if (!ev[dev][0]) {
-        for (int i = 0; i < 3; ++i)
+        for (int i = 0; i < 2 + kForkPool; ++i)
             if (hipEventCreateWithFlags(&ev[dev][i], hipEventDisableTiming) != hipSuccess)
                 return isg_check_launch("exec: side-stream events");
     }
-    *fork = ev[dev][0];
-    *join = ev[dev][1];
-    *join2 = ev[dev][2];
+    *join = ev[dev][0];
+    *join2 = ev[dev][1];
+    *forks = &ev[dev][2];
     return ISG_OK;
 }
 struct Fix {
@@ -360,7 +362,7 @@ int32_t isg_exec_ms2(const void* ops, int32_t nops, void* const* table, isg_stre
                      isg_stream_t side, isg_stream_t side2) {
     const char* p = (const char*)ops;
     alignas(16) char buf[8192];
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_join2 = nullptr;
+    hipEvent_t ev_join = nullptr, ev_join2 = nullptr, *ev_forks = nullptr;
     bool forked = false, forked2 = false;  // side-stream work outstanding since the last join
     static const int batch = [] {
         // weight gradients deferred per fork: 48 with two side streams and one backward
@@ -369,17 +371,33 @@ int32_t isg_exec_ms2(const void* ops, int32_t nops, void* const* table, isg_stre
         const int b = e ? atoi(e) : 48;
         return b < 1 ? 1 : b;
     }();
+    // A batch's fork point is recorded on the main stream when the batch closes, but its
+    // kernels are issued only after `delay` more main-stream ops. Under stream capture the
+    // graph then holds the main-stream chain's next nodes BEFORE the batch's nodes, and
+    // the graph launch dispatches them first (with the batch issued at its fork point, the
+    // launch queued the whole batch ahead of the chain's continuation: the input-gradient
+    // chain stood still ~0.5 ms per step behind 40-odd weight gradients, kernel trace k6).
+    static const int delay = [] {
+        const char* e = getenv("ISG_SIDE_DELAY");
+        return e ? std::max(0, atoi(e)) : 0;
+    }();
+    struct Batch {
+        std::vector<std::pair<int32_t, std::string>> ops;
+        hipEvent_t ev;
+        int countdown;
+    };
     std::vector<std::pair<int32_t, std::string>> pending;
-    auto flush = [&]() -> int32_t {
-        if (pending.empty()) return ISG_OK;
+    std::deque<Batch> ready;
+    int pool_next = 0;
+    auto launch = [&](Batch& bt) -> int32_t {
         // a batch of weight gradients only (independent accumulations into the replica
         // buffers) is dealt over both side streams: their grids (128-512 workgroups) leave
         // most of the chip idle one at a time; anything else keeps its order on stream 0
         bool spread = side2 != nullptr;
-        for (auto& op : pending)
+        for (auto& op : bt.ops)
             spread = spread && (op.first == OP_CONV_WGRAD || op.first == OP_KP_STEM_WGRAD);
-        if (hipEventRecord(ev_fork, main_st) != hipSuccess || hipStreamWaitEvent(side, ev_fork, 0) != hipSuccess ||
-            (spread && hipStreamWaitEvent(side2, ev_fork, 0) != hipSuccess))
+        if (hipStreamWaitEvent(side, bt.ev, 0) != hipSuccess ||
+            (spread && hipStreamWaitEvent(side2, bt.ev, 0) != hipSuccess))
             return isg_check_launch("exec: fork side stream");
         if (!spread && forked2) {
             // a non-weight-gradient batch (e.g. the replica fold / gradient finalisation at
@@ -393,15 +411,35 @@ int32_t isg_exec_ms2(const void* ops, int32_t nops, void* const* table, isg_stre
         forked2 = forked2 || spread;
         alignas(16) char pb[8192];
         int k = 0;
-        for (auto& op : pending) {
+        for (auto& op : bt.ops) {
             std::memcpy(pb, op.second.data(), op.second.size());
             if (int32_t e = run_op(op.first, pb, spread && (k++ & 1) ? side2 : side)) return e;
         }
-        pending.clear();
         return ISG_OK;
     };
+    auto drain = [&](bool all) -> int32_t {  // issue the ready batches due (FIFO)
+        while (!ready.empty() && (all || ready.front().countdown <= 0)) {
+            if (int32_t e = launch(ready.front())) return e;
+            ready.pop_front();
+        }
+        return ISG_OK;
+    };
+    auto close_batch = [&]() -> int32_t {  // the pending batch's fork point is here
+        if (pending.empty()) return ISG_OK;
+        if ((int)ready.size() >= kForkPool)
+            if (int32_t e = launch(ready.front())) return e;
+        if ((int)ready.size() >= kForkPool) ready.pop_front();
+        Batch bt;
+        bt.ops.swap(pending);
+        bt.ev = ev_forks[pool_next++ % kForkPool];
+        bt.countdown = delay;
+        if (hipEventRecord(bt.ev, main_st) != hipSuccess) return isg_check_launch("exec: fork point");
+        ready.push_back(std::move(bt));
+        return drain(false);
+    };
     auto join = [&]() -> int32_t {
-        if (int32_t e = flush()) return e;
+        if (int32_t e = close_batch()) return e;
+        if (int32_t e = drain(true)) return e;
         if (forked) {
             forked = false;
             if (hipEventRecord(ev_join, side) != hipSuccess || hipStreamWaitEvent(main_st, ev_join, 0) != hipSuccess)
@@ -423,8 +461,8 @@ int32_t isg_exec_ms2(const void* ops, int32_t nops, void* const* table, isg_stre
         }
         if ((h.flags & ISG_OPF_SIDE) && side) {
             // the op depends on everything issued so far on the main stream
-            if (!ev_fork) {
-                if (int32_t e = side_events(&ev_fork, &ev_join, &ev_join2)) return e;
+            if (!ev_join) {
+                if (int32_t e = side_events(&ev_join, &ev_join2, &ev_forks)) return e;
             }
             st = side;
         }
@@ -446,9 +484,16 @@ int32_t isg_exec_ms2(const void* ops, int32_t nops, void* const* table, isg_stre
             // deferred: launched in batches behind one fork (a later fork only adds
             // dependencies, so batching is always safe)
             pending.emplace_back(h.kind, std::string(buf, buf + h.desc_bytes));
-            if ((int)pending.size() >= batch || (h.flags & ISG_OPF_FORK_NOW)) rc = flush();
+            if ((int)pending.size() >= batch || (h.flags & ISG_OPF_FORK_NOW)) {
+                rc = close_batch();
+                if (!rc && (h.flags & ISG_OPF_FORK_NOW)) rc = drain(true);
+            }
         } else {
             rc = run_op(h.kind, buf, st);
+            if (!rc && !ready.empty()) {
+                for (auto& bt : ready) --bt.countdown;
+                rc = drain(false);
+            }
         }
         if (rc) {
             std::string m = g_last_error;

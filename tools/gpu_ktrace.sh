@@ -11,7 +11,7 @@ cd /tmp && export TMPDIR=/tmp
 for e in "$@"; do
   ( export $e
   timeout -k 10 300 rocprofv3 --kernel-trace -d $R/gpurun_out/kt_${TAG}_$i -o run --output-format csv \
-      -- python3 $R/bench.py --steps ${STEPS:-20} --warmup 5 --no-cpu-baseline --no-infer --no-dense-leg \
+      -- python3 $R/bench.py --steps ${STEPS:-20} --warmup 5 --no-cpu-baseline --no-infer --no-dense-leg ${BENCH_ARGS:-} \
       > $R/gpurun_out/kt_${TAG}_$i.log 2>&1 ) || exit 1
   echo "$i [$e] $(tail -1 $R/gpurun_out/kt_${TAG}_$i.log | cut -c100-200)"
   i=$((i+1))

@@ -36,7 +36,8 @@ def main():
                 geo += " src[" + ",".join(f"C{v.s[j].C}xf{v.s[j].xform}" for j in range(v.nseg)) + "]"
                 if r.kind != L.OP_CONV_WGRAD:
                     geo += " sinks[" + ",".join(f"m{rec.out.s[j].mode}" for j in range(rec.out.nsink)) + "]"
-            print(f"{ph} {i:4d} kind={r.kind:2d} {r.label:34s} {geo}")
+            fl = "".join(c for c, b in (("S", 1), ("J", 2), ("F", 4)) if r.flags & b)
+            print(f"{ph} {i:4d} kind={r.kind:2d} {fl:3s} {r.label:34s} {geo}")
 
 
 if __name__ == "__main__":
