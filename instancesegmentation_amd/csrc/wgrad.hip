@@ -789,7 +789,12 @@ int32_t pwk_launch(const PwkArgs& a, dim3 grid, hipStream_t st) {
 // returns 1 when launched, 0 when the shape is not for this kernel, <0 on error
 int32_t pwk_try(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, float* dw,
                 float* dbias, int64_t rep_stride, int32_t nrep, hipStream_t st) {
-    static const int env = getenv("ISG_PWK") ? atoi(getenv("ISG_PWK")) : 1;  // 0: pwg only
+    // opt-in (ISG_PWK=1): faster alone (kbench 48 -> 128 at 64^2: 16.8 -> 13.1 us) but
+    // slower in the step (4.01 -> 4.11 ms, 2 interleaved pairs): its 256-384 workgroups of
+    // 68 KB LDS take the CUs the input-gradient chain runs on, where pwg's fewer, thinner
+    // workgroups leave them free — on the side streams a thin kernel beats a fast one
+    const char* pe = getenv("ISG_PWK");  // read per call: the parity test runs both paths
+    const int env = pe ? atoi(pe) : 0;
     static const int max_rc = getenv("ISG_PWK_MAXRC") ? atoi(getenv("ISG_PWK_MAXRC")) : 65536;
     if (!env) return 0;
     const int HW = g->H * g->W;

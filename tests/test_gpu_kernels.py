@@ -331,11 +331,13 @@ def test_conv_wgrad_dense(cfg):
 @pytest.mark.parametrize("xmode", ["eval", "train"])
 @pytest.mark.parametrize("cfg", [(48, 128, 20, 24), (128, 48, 16, 16), (40, 20, 12, 36),
                                  (96, 48, 64, 64), (36, 48, 32, 32), (256, 128, 8, 8)])
-def test_pw_wgrad_bn_bwd(cfg, xmode):
+@pytest.mark.parametrize("pwk", ["0", "1"])
+def test_pw_wgrad_bn_bwd(cfg, xmode, pwk, monkeypatch):
     """1x1 weight gradient with the train plan's operands: dy = training-mode BatchNorm
     backward rebuilt on load from (grad, y) and consumer-side statistics, x = BatchNorm +
-    PReLU on load (wgrad.hip pwk_kernel for dW up to 65536 elements — ragged blocks and a
-    partial last super-tile here — pwg_kernel above), into replicas, against fp64."""
+    PReLU on load (wgrad.hip pwg_kernel, and with ISG_PWK=1 pwk_kernel: ragged blocks and a
+    partial last super-tile here), into replicas, against fp64."""
+    monkeypatch.setenv("ISG_PWK", pwk)
     Ci, Co, H, W = cfg
     N = 2
     ge, OH, OW = _geom(N, Ci, Co, H, W, 1, 1, 0, 1)
