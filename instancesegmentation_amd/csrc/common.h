@@ -376,6 +376,9 @@ ISG_DEV bool fin_last_block(uint32_t* ctr) {
     if (threadIdx.x == 0 && threadIdx.y == 0) {
         const unsigned nb = gridDim.x * gridDim.y * gridDim.z;
         const unsigned b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+        // the HIP memory model's hand-off: release before the ticket, acquire
+        // in the last workgroup before it reads the other workgroups' statistics
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         bool last;
         if (nb <= 2 * ISG_FIN_SUBS) {
             last = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nb - 1;
@@ -385,6 +388,7 @@ ISG_DEV bool fin_last_block(uint32_t* ctr) {
             last = __hip_atomic_fetch_add(ctr + 1 + sub, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ns - 1 &&
                    __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ISG_FIN_SUBS - 1;
         }
+        if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         s_last = last ? 1 : 0;
     }
     __syncthreads();

@@ -816,6 +816,12 @@ int32_t isg_tail_bwd(const isg_tail_grad* t, isg_stream_t st) {
     const isg_tail& f = t->f;
     if ((f.H & 1) || (f.W & 1) || f.nterm < 1 || f.nterm > 3)
         return isg_set_error(ISG_ERR_UNSUPPORTED, "tail bwd: H, W must be even, 1..3 terms");
+    // the kernels load every accumulating term's old value before any write:
+    // two terms accumulating into one destination would lose one contribution
+    for (int i = 0; i < f.nterm; ++i)
+        for (int j = i + 1; j < f.nterm; ++j)
+            if (t->dterm[i] && t->dterm[i] == t->dterm[j] && (t->dterm_accum[i] || t->dterm_accum[j]))
+                return isg_set_error(ISG_ERR_INVALID, "tail bwd: terms %d and %d share a gradient destination", i, j);
     if (tail4_ok(f, t)) {
         dim3 grid4((unsigned)((((int64_t)f.H / 2) * (f.W / 4) + kThreads - 1) / kThreads), f.C, f.N);
         hipLaunchKernelGGL(tail_bwd4_kernel, grid4, dim3(kThreads), 0, st, *t);

@@ -925,9 +925,14 @@ int32_t isg_pw_gemm(const isg_conv_geom* g, const isg_vtensor* src, const float*
             const isg_sink& k = out->s[s];
             if (k.mode == ISG_SINK_ACTBWD && !k.bn.coef && k.bn.stats) b.stat_on = 1;
         }
+        // HY also selects the 4-group statistics loads (coef_issue<4>): a BN_BWD segment
+        // finalised by the consumer needs them even when its y is its own input (ADVICE r03:
+        // the 2-group form would apply identity coefficients there)
         bool hy = false;
         for (int s = 0; s < src->nseg; ++s)
-            if (src->s[s].xform == ISG_XF_BN_BWD && src->s[s].y && src->s[s].y != src->s[s].p) hy = true;
+            if (src->s[s].xform == ISG_XF_BN_BWD &&
+                ((src->s[s].y && src->s[s].y != src->s[s].p) || (!src->s[s].bn.coef && src->s[s].bn.stats)))
+                hy = true;
         // (BM, BP): rows first (fewer row blocks = fewer slab re-reads), then pixels; the
         // first configuration that fits the LDS and the per-lane load budget (8 weight and
         // 8 activation loads of 16 B), keeps >= 4 MFMA tiles per workgroup and gives >= 256

@@ -495,9 +495,16 @@ _BN_FINAL = os.environ.get("ISG_BN_FINAL", "0") == "1"
 # four-wave form all-consumer-side measured 4.39 vs 4.41 ms/step, profiles/r03u_ab.txt.)
 _BN_FINAL_COUNT = int(os.environ.get("ISG_BN_FINAL_COUNT", str(1 << 62)))
 # finalise BN coefficients in the producing kernel's last workgroup (isg_sink.fin_*)
-# instead of a separate OP_BN_FINAL launch (needs ISG_BN_FINAL=1). Opt-in: measured
-# slower (5.43 vs 5.17 ms/step fence-free, round 3; 7.16 vs 6.5 with a release fence).
-_BN_FUSE = _BN_FINAL and os.environ.get("ISG_BN_FUSE", "0") == "1"
+# instead of a separate OP_BN_FINAL launch. Withdrawn in round 4: measured slower (5.43 vs
+# 5.17 ms/step fence-free, round 3; 7.16 vs 6.5 with a release fence) and, with the
+# memory-model fences in fin_last_block, still 1.4e-3 (relative to scale) from the default
+# plan's gradients on the 2x128^2 fixture, deterministically across replays — a plan-level
+# ordering fault (a BatchNorm finalised before all of its statistics are in), not a race.
+# The kernels keep the mechanism; ISG_BN_FUSE=1 is refused until that is found.
+if _BN_FINAL and os.environ.get("ISG_BN_FUSE", "0") == "1":
+    raise RuntimeError("ISG_BN_FUSE is withdrawn (engine.py: its gradients differ from the "
+                       "default plan's); use ISG_BN_FINAL=1 alone for finalisation launches")
+_BN_FUSE = False
 
 
 def _buf_range(buf):

@@ -224,3 +224,35 @@ def test_side_close_orders_after_second_side_stream(monkeypatch):
             err = (g - base).abs().max().item()
             print(env, i, f"max abs diff {err:.2e} (scale {scale:.2e})")
             assert err <= 1e-5 * scale, (env, i, err)
+
+
+def test_bn_final_launches_match_default(monkeypatch):
+    """the opt-in BatchNorm finalisation launches (ISG_BN_FINAL=1: one
+    OP_BN_FINAL per layer turns the statistics into coefficients) must give the gradients of
+    the default plan (coefficients evaluated by the consumers). Three replays each. (The
+    fused form, finalised by the producer's last workgroup, failed this check in round 4 —
+    1.4e-3 of scale, deterministic — and is withdrawn, engine.py _BN_FUSE.)"""
+    from instancesegmentation_amd import engine
+    fx = SegmentFixture("segment20_n2_128.npz")
+    xs, y = _inputs(fx.x), torch.from_numpy(fx.mask).to(DEV)
+
+    def grads(final):
+        monkeypatch.setattr(engine, "_BN_FINAL", final)
+        tr = Trainer(_model(fx), fx.n, [(fx.n, 3, fx.h, fx.w), (fx.n, 17, fx.h, fx.w)],
+                     device=DEV).capture()
+        sd = tr.optimizer_state_dict()
+        sd["param_groups"][0]["lr"] = 0.0
+        tr.load_optimizer_state_dict(sd)
+        out = []
+        for _ in range(3):
+            tr.step(xs, y)
+            torch.cuda.synchronize()
+            out.append(tr.grad_flat.detach().double().cpu().clone())
+        return out
+
+    base = grads(False)[0]
+    scale = base.abs().max().item()
+    for i, g in enumerate(grads(True)):
+        err = (g - base).abs().max().item()
+        print("ISG_BN_FINAL=1", i, f"max abs diff {err:.2e} (scale {scale:.2e})")
+        assert err <= 1e-5 * scale, (i, err)

@@ -147,8 +147,12 @@ def test_bench_traffic_record_matches_dominant_op():
     assert "dw_init_conv.layer1" in by_label
     for r in runs:
         kern = [v for k, v in r["kernels"].items() if not k.startswith("__amd_rocclr")]
-        expect = sum(v.get("fetch_scale", 2.0) * v["FETCH_SIZE_kb_per_dispatch"]
-                     + v["WRITE_SIZE_kb_per_dispatch"] for v in kern) * 1024.0
+        if all("read_bytes_per_dispatch" in v for v in kern):
+            # round-4 records (tools/pmc_traffic_all.sh): bytes, the FETCH_SIZE doubling applied
+            expect = sum(v["read_bytes_per_dispatch"] + v["write_bytes_per_dispatch"] for v in kern)
+        else:
+            expect = sum(v.get("fetch_scale", 2.0) * v["FETCH_SIZE_kb_per_dispatch"]
+                         + v["WRITE_SIZE_kb_per_dispatch"] for v in kern) * 1024.0
         assert abs(r["hbm_bytes_per_launch"] - expect) <= 1e-6 * expect
     args = types.SimpleNamespace(batch=2, cin=20, size=1024)
     got = bench.pmc_traffic("dw_init_conv.layer1", args)
