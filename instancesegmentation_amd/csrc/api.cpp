@@ -68,6 +68,8 @@ static int32_t check_geom(const isg_conv_geom* g) {
     return ISG_OK;
 }
 
+static bool geom_ok(const isg_conv_geom* g) { return check_geom(g) == ISG_OK; }
+
 int32_t isg_tap_conv(const isg_conv_geom*, const isg_vtensor*, const float*, const isg_sinks*,
                      bool, hipStream_t);
 int32_t isg_s2k5_fwd(const isg_conv_geom*, const isg_vtensor*, const float*, const isg_sinks*,
@@ -244,6 +246,13 @@ struct Fix {
 
 static int32_t run_op_raw(int32_t kind, char* buf, isg_stream_t st);
 
+// wgrad.hip: grouped 1x1 weight gradients (the executor's side-stream batches)
+int32_t isg_pwg_plan_bytes();
+int32_t isg_pwg_group_max();
+int32_t isg_pwg_plan(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, float* dw,
+                     float* dbias, int64_t rep_stride, int32_t nrep, void* plan);
+int32_t isg_pwg_run(const void* const* plans, int32_t n, hipStream_t st);
+
 // BN finalisation the producing kernel did not fuse (its launcher did not report
 // isg_fin_note_handled): one isg_bn_finalize launch per sink, as before the fusion.
 static int32_t fin_fallback(const isg_sinks* sk, isg_stream_t st) {
@@ -256,7 +265,20 @@ static int32_t fin_fallback(const isg_sinks* sk, isg_stream_t st) {
     return ISG_OK;
 }
 
+// experiment (tools/gpu_ab.sh, timing only — the gradients are wrong): ISG_DBG_NOP_WGRAD=1
+// replaces every weight-gradient op with an empty one-wave launch (same graph nodes, no
+// work), =2 drops them (no nodes): separates the side streams' node count from their work
+__global__ void isg_nop_kernel() {}
+
 static int32_t run_op(int32_t kind, char* buf, isg_stream_t st) {
+    static const int nop_wgrad = getenv("ISG_DBG_NOP_WGRAD") ? atoi(getenv("ISG_DBG_NOP_WGRAD")) : 0;
+    if (nop_wgrad && kind == OP_CONV_WGRAD) {
+        if (nop_wgrad == 1) {
+            hipLaunchKernelGGL(isg_nop_kernel, dim3(1), dim3(64), 0, st);
+            return isg_check_launch("nop");
+        }
+        return ISG_OK;
+    }
     g_fin_handled = false;
     int32_t rc = run_op_raw(kind, buf, st);
     if (rc) return rc;
@@ -381,6 +403,9 @@ int32_t isg_exec_ms2(const void* ops, int32_t nops, void* const* table, isg_stre
         const char* e = getenv("ISG_SIDE_DELAY");
         return e ? std::max(0, atoi(e)) : 0;
     }();
+    // grouped 1x1 weight gradients in weight-gradient batches (opt-in ISG_PWG_GROUP=1
+    // until its in-step A/B is in: DESIGN §3.5)
+    static const bool pwg_group_on = getenv("ISG_PWG_GROUP") != nullptr;
     struct Batch {
         std::vector<std::pair<int32_t, std::string>> ops;
         hipEvent_t ev;
@@ -411,9 +436,48 @@ int32_t isg_exec_ms2(const void* ops, int32_t nops, void* const* table, isg_stre
         forked2 = forked2 || spread;
         alignas(16) char pb[8192];
         int k = 0;
-        for (auto& op : bt.ops) {
-            std::memcpy(pb, op.second.data(), op.second.size());
-            if (int32_t e = run_op(op.first, pb, spread && (k++ & 1) ? side2 : side)) return e;
+        auto next_st = [&]() { return spread && (k++ & 1) ? side2 : side; };
+        bool all_wgrad = true;
+        for (auto& op : bt.ops) all_wgrad = all_wgrad && (op.first == OP_CONV_WGRAD || op.first == OP_KP_STEM_WGRAD);
+        if (!pwg_group_on || !all_wgrad) {
+            for (auto& op : bt.ops) {
+                std::memcpy(pb, op.second.data(), op.second.size());
+                if (int32_t e = run_op(op.first, pb, next_st())) return e;
+            }
+            return ISG_OK;
+        }
+        // a batch of weight gradients only (independent accumulations): the 1x1 ones that
+        // would run on pwg_kernel go out grouped, up to isg_pwg_group_max() per launch of
+        // one instantiation (wgrad.hip pwg_group_kernel); each group at its first member
+        const size_t n = bt.ops.size();
+        const int gmax = isg_pwg_group_max();
+        std::vector<std::vector<char>> plans(n);
+        std::vector<int> key(n, 0);
+        for (size_t i = 0; i < n; ++i) {
+            if (bt.ops[i].first != OP_CONV_WGRAD) continue;
+            std::memcpy(pb, bt.ops[i].second.data(), bt.ops[i].second.size());
+            auto* r = (WgradRec*)pb;
+            if (!geom_ok(&r->g)) continue;
+            plans[i].resize((size_t)isg_pwg_plan_bytes());
+            key[i] = isg_pwg_plan(&r->g, &r->dy, &r->x, r->dw, r->dbias, r->rep_stride,
+                                  r->nrep < 1 ? 1 : r->nrep, plans[i].data());
+        }
+        std::vector<char> done(n, 0);
+        for (size_t i = 0; i < n; ++i) {
+            if (done[i]) continue;
+            if (key[i] > 0) {
+                const void* grp[8];
+                int m = 0;
+                for (size_t j = i; j < n && m < gmax && m < 8; ++j)
+                    if (!done[j] && key[j] == key[i]) {
+                        grp[m++] = plans[j].data();
+                        done[j] = 1;
+                    }
+                if (int32_t e = isg_pwg_run(grp, m, next_st())) return e;
+                continue;
+            }
+            std::memcpy(pb, bt.ops[i].second.data(), bt.ops[i].second.size());
+            if (int32_t e = run_op(bt.ops[i].first, pb, next_st())) return e;
         }
         return ISG_OK;
     };

@@ -351,9 +351,12 @@ ISG_DEV void pwg_issue(const PwgArgs& a, const ChSrc* tabA, int NR, int q, int c
     }
 }
 
+extern __shared__ f32x4 pwg_smem[];
+
+// the kernel body over block (bx, by) of problem a: pwg_kernel runs one problem on its own
+// 2-D grid, pwg_group_kernel several problems of one instantiation on one flat grid
 template <int TPW, int NU, bool HY>
-__global__ __launch_bounds__(kThreads) void pwg_kernel(PwgArgs a) {
-    extern __shared__ f32x4 pwg_smem[];
+ISG_DEV void pwg_body(const PwgArgs& a, const unsigned bx, const unsigned by) {
     char* const smem = reinterpret_cast<char*>(pwg_smem);
     ChSrc* const tabA = reinterpret_cast<ChSrc*>(smem);  // kThreads entries: BR dy rows, BC x rows
     ChanCoef* const tabK = reinterpret_cast<ChanCoef*>(smem + a.off_k);
@@ -365,11 +368,11 @@ __global__ __launch_bounds__(kThreads) void pwg_kernel(PwgArgs a) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = wave_id();
     const int kk = lane >> 4, pl = lane & 15;
-    const int rb = blockIdx.y / a.ncb, cb = blockIdx.y - rb * a.ncb;
+    const int rb = by / a.ncb, cb = by - rb * a.ncb;
     const int r0 = rb * a.BR, c0 = cb * a.BC;
     const int Rb = min(a.BR, a.R - r0), Cb = min(a.BC, a.C - c0);
     const int BR = a.BR, NR = a.BR + a.BC;
-    const int64_t rep_off = (int64_t)((blockIdx.x + 7u * blockIdx.y) % (unsigned)a.nrep) * a.rep_stride;
+    const int64_t rep_off = (int64_t)((bx + 7u * by) % (unsigned)a.nrep) * a.rep_stride;
     float* const dwr = a.dw + rep_off;
     STAMP(0);
 
@@ -422,7 +425,7 @@ __global__ __launch_bounds__(kThreads) void pwg_kernel(PwgArgs a) {
     const bool do_bias = a.dbias && cb == 0;
 
     const int q = tid & 15, cr = tid >> 4;
-    const int64_t t0 = (int64_t)blockIdx.x * a.tiles_per_block;
+    const int64_t t0 = (int64_t)bx * a.tiles_per_block;
     const int64_t t1 = min(t0 + a.tiles_per_block, a.ntiles);
     f32x4 v[NU], yv[NU];
     bool pv;
@@ -494,6 +497,39 @@ __global__ __launch_bounds__(kThreads) void pwg_kernel(PwgArgs a) {
     STAMP(4);
 }
 
+template <int TPW, int NU, bool HY>
+__global__ __launch_bounds__(kThreads) void pwg_kernel(PwgArgs a) {
+    pwg_body<TPW, NU, HY>(a, blockIdx.x, blockIdx.y);
+}
+
+// Up to kPwgGroup problems of one instantiation in one launch (the executor's side-stream
+// batches, api.cpp): measured, every side-stream node costs the step ~3 us even when it
+// does no work (ISG_DBG_NOP_WGRAD: 4.02 ms, 3.62 with the weight gradients as empty
+// launches, 3.35 with no launches), so the 1x1 weight gradients of a batch go out grouped.
+constexpr int kPwgGroup = 3;
+struct PwgGroupMeta {
+    int start[kPwgGroup + 1];  // flat block ranges
+    int gx[kPwgGroup];
+    int n;
+};
+
+// the records travel as separate kernel parameters (an array of them, indexed per branch,
+// was merged by the compiler into one body reading a copied array from scratch)
+template <int TPW, int NU, bool HY>
+__global__ __launch_bounds__(kThreads) void pwg_group_kernel(PwgArgs p0, PwgArgs p1, PwgArgs p2,
+                                                             PwgGroupMeta m) {
+    const int b = blockIdx.x;
+    if (m.n > 2 && b >= m.start[2]) {
+        const int l = b - m.start[2];
+        pwg_body<TPW, NU, HY>(p2, l % m.gx[2], l / m.gx[2]);
+    } else if (m.n > 1 && b >= m.start[1]) {
+        const int l = b - m.start[1];
+        pwg_body<TPW, NU, HY>(p1, l % m.gx[1], l / m.gx[1]);
+    } else {
+        pwg_body<TPW, NU, HY>(p0, b % m.gx[0], b / m.gx[0]);
+    }
+}
+
 bool g_aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 bool pwg_src_ok(const isg_vtensor& v, int HW) {
@@ -535,17 +571,6 @@ int32_t pwg_launch(const PwgArgs& a, dim3 grid, size_t lds, hipStream_t st) {
     return isg_check_launch("pwg_kernel");
 }
 
-template <int NU, bool HY>
-int32_t pwg_dispatch(const PwgArgs& a, dim3 grid, size_t lds, int tpw, hipStream_t st) {
-    switch (tpw) {
-        case 1: return pwg_launch<1, NU, HY>(a, grid, lds, st);
-        case 2: return pwg_launch<2, NU, HY>(a, grid, lds, st);
-        case 3: return pwg_launch<3, NU, HY>(a, grid, lds, st);
-        case 4: return pwg_launch<4, NU, HY>(a, grid, lds, st);
-        case 5: case 6: return pwg_launch<6, NU, HY>(a, grid, lds, st);
-        default: return pwg_launch<8, NU, HY>(a, grid, lds, st);
-    }
-}
 
 // ---- 1x1 weight gradient of the small maps, K split over the waves (pwk) ----------------
 // At 64^2 / 128^2 (bs2: 8K-32K pixels against a dW of a few thousand elements) pwg_kernel
@@ -847,17 +872,28 @@ int32_t pwk_try(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor
 }
 
 // returns 1 when launched, 0 when the shape is not for this kernel, <0 on error
-int32_t pwg_try(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, float* dw,
-                float* dbias, int64_t rep_stride, int32_t nrep, hipStream_t st) {
+// a pwg launch, planned: its record, grid, dynamic LDS and instantiation
+struct PwgPlan {
+    PwgArgs a;
+    dim3 grid;
+    size_t lds;
+    int tpw, nu;  // instantiated TPW (1, 2, 3, 4, 6, 8) and NU (4, 8, 12)
+    bool hy;
+    int key() const { return 1 + (tpw * 16 + nu) * 2 + (hy ? 1 : 0); }
+};
+
+// the shape and operand checks of pwg_try and the launch geometry; false: not for pwg
+bool pwg_plan(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, float* dw,
+              float* dbias, int64_t rep_stride, int32_t nrep, PwgPlan& pl) {
     static const bool off = getenv("ISG_PWG_OFF") != nullptr;
-    if (off) return 0;
+    if (off) return false;
     if (!(g->KH == 1 && g->KW == 1 && g->SH == 1 && g->SW == 1 && g->PH == 0 && g->PW == 0))
-        return 0;
-    if (g->OH != g->H || g->OW != g->W || g->Co < 2) return 0;
+        return false;
+    if (g->OH != g->H || g->OW != g->W || g->Co < 2) return false;
     const int HW = g->H * g->W;
-    if (!pwg_src_ok(*dy, HW) || !pwg_src_ok(*x, HW)) return 0;
-    if (const int32_t k = pwk_try(g, dy, x, dw, dbias, rep_stride, nrep, st)) return k;
-    PwgArgs a{};
+    if (!pwg_src_ok(*dy, HW) || !pwg_src_ok(*x, HW)) return false;
+    PwgArgs& a = pl.a;
+    a = PwgArgs{};
     a.dy = *dy; a.x = *x; a.dw = dw; a.dbias = dbias; a.rep_stride = rep_stride; a.nrep = nrep;
     a.HW = HW; a.R = g->Co; a.C = g->Ci;
     a.P = (int64_t)g->N * HW;
@@ -868,7 +904,7 @@ int32_t pwg_try(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor
             const isg_vseg& q = v->s[s];
             if ((q.xform == ISG_XF_BN_FWD || q.xform == ISG_XF_BN_BWD) && !q.bn.coef && q.bn.stats) a.stat_on = 1;
         }
-    const bool hy = pwg_has_y(*dy) || pwg_has_y(*x);
+    pl.hy = pwg_has_y(*dy) || pwg_has_y(*x);
     a.ntiles = (a.P + kGTP - 1) / kGTP;
     int br = std::min(64, (a.R + 15) / 16 * 16);
     int bc = std::min(kGMaxRows - br, std::min(128, (a.C + 15) / 16 * 16));
@@ -895,16 +931,83 @@ int32_t pwg_try(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor
     static const int env_tpb = getenv("ISG_PWG_TPB") ? atoi(getenv("ISG_PWG_TPB")) : 2;
     if (env_tpb > a.tiles_per_block) a.tiles_per_block = env_tpb;
     gx = (a.ntiles + a.tiles_per_block - 1) / a.tiles_per_block;
+    if (gx * gy >= (1ll << 31)) return false;
     a.off_k = (kThreads * (int)sizeof(ChSrc) + 15) & ~15;
     a.off_x = (a.off_k + kGMaxRows * (int)(sizeof(ChanCoef) + 2 * sizeof(float)) + 15) & ~15;
-    const size_t lds = (size_t)a.off_x + (size_t)(br + bc) * kGS * sizeof(float);
+    pl.lds = (size_t)a.off_x + (size_t)(br + bc) * kGS * sizeof(float);
     const int tpw = ((br / 16) * (bc / 16) + 3) / 4;
-    const dim3 grid((unsigned)gx, (unsigned)gy);
+    pl.tpw = tpw <= 4 ? tpw : tpw <= 6 ? 6 : 8;
+    pl.grid = dim3((unsigned)gx, (unsigned)gy);
     const int passes = (br + bc + 15) / 16;
-    int32_t rc;
-    if (passes <= 4) rc = hy ? pwg_dispatch<4, true>(a, grid, lds, tpw, st) : pwg_dispatch<4, false>(a, grid, lds, tpw, st);
-    else if (passes <= 8) rc = hy ? pwg_dispatch<8, true>(a, grid, lds, tpw, st) : pwg_dispatch<8, false>(a, grid, lds, tpw, st);
-    else rc = hy ? pwg_dispatch<12, true>(a, grid, lds, tpw, st) : pwg_dispatch<12, false>(a, grid, lds, tpw, st);
+    pl.nu = passes <= 4 ? 4 : passes <= 8 ? 8 : 12;
+    return true;
+}
+
+template <int TPW, int NU, bool HY>
+int32_t pwg_group_launch_t(const PwgPlan* const* pl, int n, hipStream_t st) {
+    PwgGroupMeta m{};
+    size_t lds = 0;
+    int64_t total = 0;
+    for (int i = 0; i < n; ++i) {
+        m.start[i] = (int)total;
+        m.gx[i] = (int)pl[i]->grid.x;
+        total += (int64_t)pl[i]->grid.x * pl[i]->grid.y;
+        lds = std::max(lds, pl[i]->lds);
+    }
+    m.start[n] = (int)total;
+    m.n = n;
+    if (total >= (1ll << 31)) return isg_set_error(ISG_ERR_UNSUPPORTED, "pwg group: grid");
+    auto k = pwg_group_kernel<TPW, NU, HY>;
+    static bool attr = false;
+    if (!attr) {
+        if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024) != hipSuccess)
+            return isg_check_launch("pwg_group_kernel: dynamic LDS");
+        attr = true;
+    }
+    const PwgArgs& a0 = pl[0]->a;
+    const PwgArgs& a1 = pl[n > 1 ? 1 : 0]->a;
+    const PwgArgs& a2 = pl[n > 2 ? 2 : 0]->a;
+    hipLaunchKernelGGL(k, dim3((unsigned)total), dim3(kThreads), lds, st, a0, a1, a2, m);
+    return isg_check_launch("pwg_group_kernel");
+}
+
+template <int TPW, int NU, bool HY>
+int32_t pwg_launch_plan(const PwgPlan* const* pl, int n, hipStream_t st) {
+    if (n == 1) return pwg_launch<TPW, NU, HY>(pl[0]->a, pl[0]->grid, pl[0]->lds, st);
+    return pwg_group_launch_t<TPW, NU, HY>(pl, n, st);
+}
+
+// n plans of one key (same instantiation), n <= kPwgGroup
+int32_t pwg_run(const PwgPlan* const* pl, int n, hipStream_t st) {
+    const PwgPlan& p = *pl[0];
+#define ISG_PWG_T(T)                                                                     \
+    if (p.tpw == T) {                                                                    \
+        if (p.nu == 4) return p.hy ? pwg_launch_plan<T, 4, true>(pl, n, st) : pwg_launch_plan<T, 4, false>(pl, n, st); \
+        if (p.nu == 8) return p.hy ? pwg_launch_plan<T, 8, true>(pl, n, st) : pwg_launch_plan<T, 8, false>(pl, n, st); \
+        return p.hy ? pwg_launch_plan<T, 12, true>(pl, n, st) : pwg_launch_plan<T, 12, false>(pl, n, st); \
+    }
+    ISG_PWG_T(1) ISG_PWG_T(2) ISG_PWG_T(3) ISG_PWG_T(4) ISG_PWG_T(6) ISG_PWG_T(8)
+#undef ISG_PWG_T
+    return isg_set_error(ISG_ERR_INVALID, "pwg: tpw %d", p.tpw);
+}
+
+// returns 1 when launched, 0 when the shape is not for this kernel, <0 on error
+int32_t pwg_try(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, float* dw,
+                float* dbias, int64_t rep_stride, int32_t nrep, hipStream_t st) {
+    {
+        static const bool off = getenv("ISG_PWG_OFF") != nullptr;
+        if (off) return 0;
+        if (!(g->KH == 1 && g->KW == 1 && g->SH == 1 && g->SW == 1 && g->PH == 0 && g->PW == 0))
+            return 0;
+        if (g->OH != g->H || g->OW != g->W || g->Co < 2) return 0;
+        const int HW = g->H * g->W;
+        if (!pwg_src_ok(*dy, HW) || !pwg_src_ok(*x, HW)) return 0;
+        if (const int32_t k = pwk_try(g, dy, x, dw, dbias, rep_stride, nrep, st)) return k;
+    }
+    PwgPlan pl;
+    if (!pwg_plan(g, dy, x, dw, dbias, rep_stride, nrep, pl)) return 0;
+    const PwgPlan* p = &pl;
+    const int32_t rc = pwg_run(&p, 1, st);
     return rc ? rc : 1;
 }
 
@@ -1025,3 +1128,33 @@ int32_t isg_dense_conv_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, cons
 #undef WG_LAUNCH
     return isg_check_launch("wgrad_kernel");
 }
+
+// ---- executor hooks (api.cpp): the 1x1 weight gradients of a side-stream batch, grouped --
+// isg_pwg_plan: > 0 (the instantiation key) when isg_conv_wgrad_rep would run this op on
+// pwg_kernel, the plan written into `plan` (isg_pwg_plan_bytes() bytes); 0 otherwise.
+// isg_pwg_run: launch n <= isg_pwg_group_max() plans of one key as one launch.
+extern "C" int32_t isg_pwg_plan_bytes() { return (int32_t)sizeof(PwgPlan); }
+extern "C" int32_t isg_pwg_group_max() { return kPwgGroup; }
+
+extern "C" int32_t isg_pwg_plan(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, float* dw,
+                     float* dbias, int64_t rep_stride, int32_t nrep, void* plan) {
+    const char* pe = getenv("ISG_PWK");
+    if (pe && atoi(pe)) return 0;  // the opt-in pwk path stays on the per-op route
+    if (!dw || nrep < 1 || (nrep > 1 && rep_stride <= 0) || g->groups != 1) return 0;
+    if (g->w_ci && g->w_ci != g->Ci) return 0;
+    if (vt_channels(dy) != g->Co || vt_channels(x) != g->Ci) return 0;
+    PwgPlan& pl = *static_cast<PwgPlan*>(plan);
+    if (!pwg_plan(g, dy, x, dw, dbias, rep_stride, nrep, pl)) return 0;
+    return pl.key();
+}
+
+extern "C" int32_t isg_pwg_run(const void* const* plans, int32_t n, hipStream_t st) {
+    if (n < 1 || n > kPwgGroup) return isg_set_error(ISG_ERR_INVALID, "pwg group of %d", n);
+    const PwgPlan* pl[kPwgGroup];
+    for (int i = 0; i < n; ++i) {
+        pl[i] = static_cast<const PwgPlan*>(plans[i]);
+        if (pl[i]->key() != pl[0]->key()) return isg_set_error(ISG_ERR_INVALID, "pwg group: mixed kernels");
+    }
+    return pwg_run(pl, n, st);
+}
+

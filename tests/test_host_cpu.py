@@ -261,3 +261,21 @@ def test_forked_pools_join_before_any_reader_of_their_buffer(n):
         if readers:  # (bottle1_1.pool is read by side-stream branches only)
             assert any(recs[j].flags & Record.OPF_JOIN for j in range(i + 1, readers[0] + 1)), \
                 (n, recs[i].label, recs[readers[0]].label)
+
+
+def test_library_has_no_undefined_isg_symbols():
+    """Every isg_* function the library calls is defined in it: a C-ABI declaration in one
+    translation unit against a C++-linkage definition in another links into a shared
+    library with the symbol left undefined, and fails only when first called on a GPU."""
+    import os
+    import shutil
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    so = os.path.join(root, "instancesegmentation_amd", "libisg.so")
+    nm = shutil.which("nm")
+    if not nm or not os.path.exists(so):
+        import pytest
+        pytest.skip("nm or libisg.so missing")
+    out = subprocess.run([nm, "-D", so], capture_output=True, text=True, check=True).stdout
+    undef = [l.split()[-1] for l in out.splitlines() if " U " in l and l.split()[-1].startswith("isg_")]
+    assert not undef, undef
