@@ -252,6 +252,12 @@ int32_t isg_pwg_group_max();
 int32_t isg_pwg_plan(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, float* dw,
                      float* dbias, int64_t rep_stride, int32_t nrep, void* plan);
 int32_t isg_pwg_run(const void* const* plans, int32_t n, hipStream_t st);
+// dw_convt.hip: grouped depthwise weight gradients
+int32_t isg_dwg_plan_bytes();
+int32_t isg_dwg_group_max();
+int32_t isg_dwg_plan(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, float* dw,
+                     float* dbias, int64_t rep_stride, int32_t nrep, void* plan);
+int32_t isg_dwg_run(const void* const* plans, int32_t n, hipStream_t st);
 
 // BN finalisation the producing kernel did not fuse (its launcher did not report
 // isg_fin_note_handled): one isg_bn_finalize launch per sink, as before the fusion.
@@ -406,6 +412,8 @@ int32_t isg_exec_ms2(const void* ops, int32_t nops, void* const* table, isg_stre
     // grouped 1x1 weight gradients in weight-gradient batches (4.04 -> 3.96
     // ms/step, 2 interleaved 200-step pairs; ISG_NO_PWG_GROUP=1 off)
     static const bool pwg_group_on = getenv("ISG_NO_PWG_GROUP") == nullptr;
+    // the depthwise ones too (opt-in ISG_DW_GROUP=1 until measured)
+    static const bool dwg_group_on = getenv("ISG_DW_GROUP") != nullptr;
     struct Batch {
         std::vector<std::pair<int32_t, std::string>> ops;
         hipEvent_t ev;
@@ -458,22 +466,27 @@ int32_t isg_exec_ms2(const void* ops, int32_t nops, void* const* table, isg_stre
             std::memcpy(pb, bt.ops[i].second.data(), bt.ops[i].second.size());
             auto* r = (WgradRec*)pb;
             if (!geom_ok(&r->g)) continue;
-            plans[i].resize((size_t)isg_pwg_plan_bytes());
+            plans[i].resize((size_t)std::max(isg_pwg_plan_bytes(), isg_dwg_plan_bytes()));
             key[i] = isg_pwg_plan(&r->g, &r->dy, &r->x, r->dw, r->dbias, r->rep_stride,
                                   r->nrep < 1 ? 1 : r->nrep, plans[i].data());
+            if (key[i] == 0 && dwg_group_on)
+                key[i] = isg_dwg_plan(&r->g, &r->dy, &r->x, r->dw, r->dbias, r->rep_stride,
+                                      r->nrep < 1 ? 1 : r->nrep, plans[i].data());
         }
         std::vector<char> done(n, 0);
         for (size_t i = 0; i < n; ++i) {
             if (done[i]) continue;
             if (key[i] > 0) {
+                const bool dwk = key[i] >= 1000;  // isg_dwg_plan's keys
+                const int cap = dwk ? isg_dwg_group_max() : gmax;
                 const void* grp[8];
                 int m = 0;
-                for (size_t j = i; j < n && m < gmax && m < 8; ++j)
+                for (size_t j = i; j < n && m < cap && m < 8; ++j)
                     if (!done[j] && key[j] == key[i]) {
                         grp[m++] = plans[j].data();
                         done[j] = 1;
                     }
-                if (int32_t e = isg_pwg_run(grp, m, next_st())) return e;
+                if (int32_t e = dwk ? isg_dwg_run(grp, m, next_st()) : isg_pwg_run(grp, m, next_st())) return e;
                 continue;
             }
             std::memcpy(pb, bt.ops[i].second.data(), bt.ops[i].second.size());

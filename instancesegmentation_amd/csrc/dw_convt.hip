@@ -444,13 +444,14 @@ __global__ __launch_bounds__(kThreads) void dw_wgrad_kernel(DwWgArgs a) {
 // the workgroup and added into this workgroup's weight-gradient replica. Same-size layers,
 // W % 4 == 0 (dw_wgrad_kernel otherwise).
 template <int KH_, int KW_>
-__global__ __launch_bounds__(kThreads) void dw_wgrad_tile_kernel(DwWgArgs a) {
+ISG_DEV void dw_wgrad_tile_body(const DwWgArgs& a, const unsigned bx, const unsigned by,
+                                const unsigned bz) {
     constexpr int KK = KH_ * KW_;
     __shared__ float Ts[kDtMaxR * kDtMaxC];
     __shared__ float sh[(KK + 1) * 4];
-    const int c = blockIdx.z % a.C, n = blockIdx.z / a.C;
+    const int c = bz % a.C, n = bz / a.C;
     const int H = a.H, W = a.W;
-    const int oy0 = blockIdx.y * kDtY, ox0 = blockIdx.x * kDtX;
+    const int oy0 = by * kDtY, ox0 = bx * kDtX;
     const int RH = kDtY + (KH_ - 1) * a.DH, RW = kDtX + (KW_ - 1) * a.DW;
     const int64_t hw = (int64_t)H * W;
     const isg_vseg& sx = a.x;
@@ -507,9 +508,43 @@ __global__ __launch_bounds__(kThreads) void dw_wgrad_tile_kernel(DwWgArgs a) {
         }
     block_reduce<KK + 1>(acc, sh);
     if (threadIdx.x == 0) {
-        const int64_t ro = (int64_t)((blockIdx.x + 3u * blockIdx.y + 7u * blockIdx.z) % (unsigned)a.nrep) * a.rep_stride;
+        const int64_t ro = (int64_t)((bx + 3u * by + 7u * bz) % (unsigned)a.nrep) * a.rep_stride;
         for (int t = 0; t < KK; ++t) atomicAdd(&a.dw[ro + c * KK + t], acc[t]);
         if (a.dbias) atomicAdd(&a.dbias[ro + c], acc[KK]);
+    }
+}
+
+template <int KH_, int KW_>
+__global__ __launch_bounds__(kThreads) void dw_wgrad_tile_kernel(DwWgArgs a) {
+    dw_wgrad_tile_body<KH_, KW_>(a, blockIdx.x, blockIdx.y, blockIdx.z);
+}
+
+// up to kDwgGroup depthwise weight gradients of one tap shape in one launch (the
+// executor's side-stream batches, as pwg_group_kernel): flat block ranges per problem
+constexpr int kDwgGroup = 6;
+struct DwgGroup {
+    DwWgArgs p[kDwgGroup];
+    int start[kDwgGroup + 1];
+    int gx[kDwgGroup], gy[kDwgGroup];
+    int n;
+};
+
+template <int KH_, int KW_>
+__global__ __launch_bounds__(kThreads) void dw_wgrad_group_kernel(DwgGroup g) {
+    const int b = blockIdx.x;
+    int i = 0;
+#pragma unroll
+    for (int k = 1; k < kDwgGroup; ++k) i = (k < g.n && b >= g.start[k]) ? k : i;
+    const int l = b - g.start[i];
+    const int gxy = g.gx[i] * g.gy[i];
+    const unsigned bz = l / gxy, r = l - bz * gxy, by = r / g.gx[i], bx = r - by * g.gx[i];
+    switch (i) {  // one inlined body per slot: a selected copy of the record would go through scratch
+        case 0: dw_wgrad_tile_body<KH_, KW_>(g.p[0], bx, by, bz); break;
+        case 1: dw_wgrad_tile_body<KH_, KW_>(g.p[1], bx, by, bz); break;
+        case 2: dw_wgrad_tile_body<KH_, KW_>(g.p[2], bx, by, bz); break;
+        case 3: dw_wgrad_tile_body<KH_, KW_>(g.p[3], bx, by, bz); break;
+        case 4: dw_wgrad_tile_body<KH_, KW_>(g.p[4], bx, by, bz); break;
+        default: dw_wgrad_tile_body<KH_, KW_>(g.p[5], bx, by, bz); break;
     }
 }
 
@@ -753,3 +788,78 @@ int32_t isg_convT_fwd(const isg_conv_geom* g, const isg_vtensor* x, const float*
     else hipLaunchKernelGGL((convT_kernel<4, 1>), grid, dim3(kThreads), 0, st, a);
     return isg_check_launch("convT_kernel");
 }
+
+// ---- executor hooks (api.cpp): the depthwise weight gradients of a side-stream batch,
+// grouped like the 1x1 ones (wgrad.hip isg_pwg_plan / isg_pwg_run) -----------------------
+namespace {
+struct DwgPlan {
+    DwWgArgs a;
+    unsigned gx, gy, gz;
+    int kh, kw;
+    int key() const { return 1000 + kh * 10 + kw; }
+};
+
+template <int KH_, int KW_>
+int32_t dwg_group_launch(const DwgPlan* const* pl, int n, hipStream_t st) {
+    DwgGroup g{};
+    int64_t total = 0;
+    for (int i = 0; i < n; ++i) {
+        g.p[i] = pl[i]->a;
+        g.start[i] = (int)total;
+        g.gx[i] = (int)pl[i]->gx;
+        g.gy[i] = (int)pl[i]->gy;
+        total += (int64_t)pl[i]->gx * pl[i]->gy * pl[i]->gz;
+    }
+    g.start[n] = (int)total;
+    g.n = n;
+    if (total >= (1ll << 31)) return isg_set_error(ISG_ERR_UNSUPPORTED, "dw wgrad group: grid");
+    hipLaunchKernelGGL((dw_wgrad_group_kernel<KH_, KW_>), dim3((unsigned)total), dim3(kThreads), 0, st, g);
+    return isg_check_launch("dw_wgrad_group_kernel");
+}
+}  // namespace
+
+extern "C" int32_t isg_dwg_plan_bytes() { return (int32_t)sizeof(DwgPlan); }
+extern "C" int32_t isg_dwg_group_max() { return kDwgGroup; }
+
+// > 0 (the tap-shape key) when isg_conv_wgrad_rep would run this op on dw_wgrad_tile_kernel
+extern "C" int32_t isg_dwg_plan(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x,
+                                float* dw, float* dbias, int64_t rep_stride, int32_t nrep, void* plan) {
+    if (!dw || nrep < 1 || (nrep > 1 && rep_stride <= 0)) return 0;
+    if (g->groups == 1 || g->groups != g->Ci || g->Ci != g->Co || (g->w_ci && g->w_ci != g->Ci)) return 0;
+    if (dy->nseg != 1 || x->nseg != 1 || g->KH * g->KW > kMaxTaps || x->s[0].xform == ISG_XF_BN_BWD) return 0;
+    if (dy->s[0].C != g->Co || x->s[0].C != g->Ci) return 0;
+    static const bool off = getenv("ISG_NO_DW_TILE") != nullptr;
+    const isg_vseg& d = dy->s[0];
+    const bool ok = !off && g->SH == 1 && g->SW == 1 && g->OH == g->H && g->OW == g->W && g->W % 4 == 0 &&
+                    !((uintptr_t)d.p & 15) && d.n_stride % 4 == 0 &&
+                    (d.xform != ISG_XF_BN_BWD || (!((uintptr_t)d.y & 15) && d.y_n_stride % 4 == 0)) &&
+                    (g->KH - 1) * g->DH <= 16 && (g->KW - 1) * g->DW <= 16;
+    const bool shape = (g->KH == 3 && g->KW == 3) || (g->KH == 5 && g->KW == 1) || (g->KH == 1 && g->KW == 5);
+    if (!ok || !shape) return 0;
+    DwgPlan& p = *static_cast<DwgPlan*>(plan);
+    p = DwgPlan{};
+    DwWgArgs& a = p.a;
+    a.dy = dy->s[0]; a.x = x->s[0]; a.dw = dw; a.dbias = dbias;
+    a.rep_stride = rep_stride; a.nrep = nrep;
+    a.N = g->N; a.C = g->Ci; a.H = g->H; a.W = g->W; a.OH = g->OH; a.OW = g->OW;
+    a.KH = g->KH; a.KW = g->KW; a.PH = g->PH; a.PW = g->PW; a.DH = g->DH; a.DW = g->DW;
+    p.gx = (unsigned)((g->W + kDtX - 1) / kDtX);
+    p.gy = (unsigned)((g->H + kDtY - 1) / kDtY);
+    p.gz = (unsigned)(g->Ci * g->N);
+    p.kh = g->KH;
+    p.kw = g->KW;
+    return p.key();
+}
+
+extern "C" int32_t isg_dwg_run(const void* const* plans, int32_t n, hipStream_t st) {
+    if (n < 1 || n > kDwgGroup) return isg_set_error(ISG_ERR_INVALID, "dw wgrad group of %d", n);
+    const DwgPlan* pl[kDwgGroup];
+    for (int i = 0; i < n; ++i) {
+        pl[i] = static_cast<const DwgPlan*>(plans[i]);
+        if (pl[i]->key() != pl[0]->key()) return isg_set_error(ISG_ERR_INVALID, "dw wgrad group: mixed shapes");
+    }
+    if (pl[0]->kh == 3) return dwg_group_launch<3, 3>(pl, n, st);
+    if (pl[0]->kh == 5) return dwg_group_launch<5, 1>(pl, n, st);
+    return dwg_group_launch<1, 5>(pl, n, st);
+}
+
