@@ -280,17 +280,20 @@ int32_t isg_sigmoid_bwd(const float* y, const float* dy, float* dx, int64_t n,
 
 /* torch.optim.Adam (defaults lr 1e-3, betas (0.9,0.999), eps 1e-8; train_instance.py:297)
  * over a flat fp32 buffer. `live` (uint8 per element, may be NULL) masks parameters
- * whose grad is None (they are skipped, as torch does). step is 1-based. */
+ * whose grad is None (they are skipped, as torch does). step is 1-based. The
+ * hyperparameters are doubles, as torch's python floats: 1-beta and the bias corrections
+ * are rounded from them the way torch does, so a torch optimizer state continues here
+ * bit-for-bit in the update formula. */
 int32_t isg_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
-                 const uint8_t* live, int64_t n, int32_t step, float lr, float beta1,
-                 float beta2, float eps, float weight_decay, isg_stream_t stream);
+                 const uint8_t* live, int64_t n, int32_t step, double lr, double beta1,
+                 double beta2, double eps, double weight_decay, isg_stream_t stream);
 
 /* Same update with the step counter in device memory: *step is incremented on the
  * stream first, then used — the launch sequence can be captured in a HIP graph and
  * replayed (the host-side form bakes `step` into the kernel arguments). */
 int32_t isg_adam_dev(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
-                     const uint8_t* live, int64_t n, int32_t* step, float lr, float beta1,
-                     float beta2, float eps, float weight_decay, isg_stream_t stream);
+                     const uint8_t* live, int64_t n, int32_t* step, double lr, double beta1,
+                     double beta2, double eps, double weight_decay, isg_stream_t stream);
 
 int32_t isg_fill_f64(double* p, int64_t n, double v, isg_stream_t stream);
 

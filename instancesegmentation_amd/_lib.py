@@ -20,7 +20,7 @@ SINK_STORE, SINK_ACCUM, SINK_ACTBWD, SINK_NONE = 0, 1, 2, 3
 MAX_SEGS = 3
 LIST_CHUNK = 32
 STAT_REP = int(os.environ.get("ISG_STAT_REP", "4"))  # accumulator replicas (isg.h ISG_STAT_REP)
-ABI_VERSION = 8
+ABI_VERSION = 9
 WREP = 16         # ISG_WREP: weight-gradient replicas (isg.h)
 
 
@@ -173,9 +173,10 @@ SIGNATURES = {
     "isg_sigmoid_fwd": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p]),
     "isg_sigmoid_bwd": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
     "isg_adam": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32,
-                           c_float, c_float, c_float, c_float, c_float, c_void_p]),
+                           c_double, c_double, c_double, c_double, c_double, c_void_p]),
     "isg_adam_dev": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
-                               c_void_p, c_float, c_float, c_float, c_float, c_float, c_void_p]),
+                               c_void_p, c_double, c_double, c_double, c_double, c_double,
+                               c_void_p]),
     "isg_fill_f64": (c_int32, [c_void_p, c_int64, c_double, c_void_p]),
     "isg_mask_paste": (c_int32, [c_void_p, c_int32, c_int32, c_void_p, c_int32, c_int32, c_void_p,
                                  c_void_p]),

@@ -86,7 +86,7 @@ static bool partial_w(const isg_conv_geom* g) { return g->w_ci > 0 && g->w_ci !=
 extern "C" {
 
 const char* isg_last_error(void) { return g_last_error.c_str(); }
-int32_t isg_abi_version(void) { return 8; }
+int32_t isg_abi_version(void) { return 9; }
 int32_t isg_stat_replicas(void) { return ISG_STAT_REP; }
 
 int32_t isg_conv_fwd(const isg_conv_geom* g, const isg_vtensor* x, const float* w,

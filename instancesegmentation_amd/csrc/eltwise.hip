@@ -731,29 +731,36 @@ __global__ void adam_kernel(float* p, const float* g, float* m, float* v, const 
 
 // Graph-replayable form: the 1-based step lives in device memory (incremented by
 // step_inc_kernel earlier in the same stream), bias corrections are formed in double
-// exactly like torch's host-side python floats, then rounded to f32.
+// exactly like torch's host-side python floats, then rounded to f32. The hyperparameters
+// arrive as doubles (torch's python floats): torch rounds 1-beta1 and 1-beta2 from the
+// DOUBLE betas (e.g. 1-0.999 -> 0.001f, where 1-(double)0.999f is 0.00099998713f) and forms
+// the bias corrections from them, so a float beta would leave this kernel self-consistent
+// but 1.3e-5 (relative) off torch's second moment whenever the optimizer state comes from
+// torch (a reference checkpoint, train_instance.py:320-328).
 __global__ void adam_dev_kernel(float* p, const float* g, float* m, float* v, const uint8_t* live,
-                                int64_t n, const int32_t* step, float lr, float b1, float b2,
-                                float eps, float wd) {
+                                int64_t n, const int32_t* step, double lr, double b1, double b2,
+                                double eps, double wd) {
 #pragma clang fp contract(off)
     const double st = (double)*step;
-    const double bc1 = 1.0 - pow((double)b1, st);
-    const double bc2 = 1.0 - pow((double)b2, st);
-    const float neg_step = (float)(-((double)lr / bc1));
+    const double bc1 = 1.0 - pow(b1, st);
+    const double bc2 = 1.0 - pow(b2, st);
+    const float neg_step = (float)(-(lr / bc1));
     const float bc2_sqrt = (float)sqrt(bc2);
-    const float w1 = (float)(1.0 - (double)b1);
-    const float one_m_b2 = (float)(1.0 - (double)b2);
+    const float w1 = (float)(1.0 - b1);
+    const float b2f = (float)b2;
+    const float one_m_b2 = (float)(1.0 - b2);
+    const float epsf = (float)eps, wdf = (float)wd;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x) {
         if (live && !live[i]) continue;
         float gi = g[i];
         const float pi = p[i];
-        if (wd != 0.f) gi = gi + wd * pi;
+        if (wdf != 0.f) gi = gi + wdf * pi;
         float mi = m[i];
         mi = mi + w1 * (gi - mi);
-        float vi = v[i] * b2;
+        float vi = v[i] * b2f;
         vi = vi + one_m_b2 * gi * gi;
-        const float denom = sqrtf(vi) / bc2_sqrt + eps;
+        const float denom = sqrtf(vi) / bc2_sqrt + epsf;
         m[i] = mi;
         v[i] = vi;
         p[i] = pi + neg_step * mi / denom;
@@ -919,23 +926,23 @@ int32_t isg_sigmoid_bwd(const float* y, const float* dy, float* dx, int64_t n, i
 }
 
 int32_t isg_adam(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
-                 const uint8_t* live, int64_t n, int32_t step, float lr, float beta1, float beta2,
-                 float eps, float weight_decay, isg_stream_t st) {
+                 const uint8_t* live, int64_t n, int32_t step, double lr, double beta1, double beta2,
+                 double eps, double weight_decay, isg_stream_t st) {
     if (step < 1) return isg_set_error(ISG_ERR_INVALID, "adam: step must be >= 1");
     // scalar math in double exactly like torch's python-side bias corrections
-    const double bc1 = 1.0 - std::pow((double)beta1, (double)step);
-    const double bc2 = 1.0 - std::pow((double)beta2, (double)step);
-    const float neg_step = (float)(-((double)lr / bc1));
+    const double bc1 = 1.0 - std::pow(beta1, (double)step);
+    const double bc2 = 1.0 - std::pow(beta2, (double)step);
+    const float neg_step = (float)(-(lr / bc1));
     const float bc2_sqrt = (float)std::sqrt(bc2);
     hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(kThreads), 0, st, param, grad, exp_avg,
-                       exp_avg_sq, live, n, (float)(1.0 - (double)beta1), beta2,
-                       (float)(1.0 - (double)beta2), bc2_sqrt, neg_step, eps, weight_decay);
+                       exp_avg_sq, live, n, (float)(1.0 - beta1), (float)beta2,
+                       (float)(1.0 - beta2), bc2_sqrt, neg_step, (float)eps, (float)weight_decay);
     return isg_check_launch("adam_kernel");
 }
 
 int32_t isg_adam_dev(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
-                     const uint8_t* live, int64_t n, int32_t* step, float lr, float beta1,
-                     float beta2, float eps, float weight_decay, isg_stream_t st) {
+                     const uint8_t* live, int64_t n, int32_t* step, double lr, double beta1,
+                     double beta2, double eps, double weight_decay, isg_stream_t st) {
     hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, st, step);
     hipLaunchKernelGGL(adam_dev_kernel, dim3(grid_for(n)), dim3(kThreads), 0, st, param, grad,
                        exp_avg, exp_avg_sq, live, n, step, lr, beta1, beta2, eps, weight_decay);

@@ -15,3 +15,17 @@ def pytest_configure(config):
 @pytest.fixture(scope="session")
 def golden_dir():
     return os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_terminal_summary(terminalreporter):
+    """The margin of every logits parity check of the run (tests/grad_check.py), printed
+    even under -q: err = max |GPU - fp64|, bar = the asserted bound, d32 = max |GPU - the
+    CPU-fp32 reference|, floor = the CPU-fp32 reference's own error."""
+    from tests.grad_check import LOGITS_MARGINS
+    if not LOGITS_MARGINS:
+        return
+    tr = terminalreporter
+    tr.write_line("logits parity margins (err/bar <= 1 passes):")
+    for tag, err, bar, d32, floor in LOGITS_MARGINS:
+        tr.write_line(f"  {tag:40s} err {err:.3e} bar {bar:.3e} err/bar {err / bar:.2f}  "
+                      f"vs CPU-fp32 {d32:.3e}  CPU-fp32 floor {floor:.3e}")

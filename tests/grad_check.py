@@ -32,6 +32,11 @@ def _t(x):
 # the CPU path's own rounding error).
 WELL_CONDITIONED = 5e-5
 
+# every logits check of the session: (tag, err vs fp64, bar, distance to CPU-fp32, CPU-fp32's
+# own error); conftest.py prints them as one table at the end of the run (also under -q), so
+# the driver's GPU-test record shows the margin of every check, not only pass/fail
+LOGITS_MARGINS = []
+
 
 def check_logits(got, ref64, ref32, tag="", strict=False):
     """strict: the input is in the well-conditioned regime by construction (a
@@ -42,9 +47,11 @@ def check_logits(got, ref64, ref32, tag="", strict=False):
     d32 = (got - ref32).abs().max().item()
     floor = (ref32 - ref64).abs().max().item()
     scale = max(1.0, ref64.abs().max().item())
-    print(f"{tag}: logits max abs err vs fp64 {err:.3e}, vs the CPU-fp32 reference "
-          f"{d32:.3e} (bar 1e-4; CPU-fp32 reference's own err {floor:.3e}; |logit|max "
-          f"{ref64.abs().max().item():.2f})")
+    bar = min(max(1e-4, 2.0 * floor), 1e-4 * scale)
+    print(f"{tag}: logits max abs err vs fp64 {err:.3e} (bar {bar:.3e}, err/bar "
+          f"{err / bar:.2f}), vs the CPU-fp32 reference {d32:.3e} (bar 1e-4; CPU-fp32 "
+          f"reference's own err {floor:.3e}; |logit|max {ref64.abs().max().item():.2f})")
+    LOGITS_MARGINS.append((tag, err, bar, d32, floor))
     assert err <= max(1e-4, 2.0 * floor), (err, floor)
     assert err <= 1e-4 * scale, (err, scale)
     if strict:

@@ -53,10 +53,20 @@ def _grads_by_key(tr):
 
 @pytest.mark.parametrize("captured", [False, True], ids=["eager", "graph"])
 def test_trainer_two_steps_match_reference(captured):
+    """Step 1 on the fixture's parameters; Adam step 1 on the GPU's own gradients against
+    torch.optim.Adam; then step 2 from DETERMINISTIC parameters: p1 = torch.optim.Adam's
+    step 1 on the reference's own fp64 gradients (CPU), loaded into the Trainer together
+    with that optimizer's state. Before round 5 step 2 ran on the GPU Adam's p1, which
+    carried the fp32-atomic summation order of the GPU's step-1 weight gradients into
+    step 2 (Adam's first step is ~lr*sign(g)), so step 2's inputs, its CPU-fp32 floor and its
+    error bar moved from run to run (Weak #1)."""
     fx = SegmentFixture("segment20_n2_128.npz")
+    mode = "graph" if captured else "eager"
     model = _model(fx)
-    cpu_model = _model(fx)  # the reference optimizer runs on this copy
+    cpu_model = _model(fx)  # the reference optimizer on the GPU's own gradients
     opt = torch.optim.Adam(cpu_model.parameters())  # train_instance.py:297
+    det_model = _model(fx)  # the reference optimizer on the reference's own gradients
+    det_opt = torch.optim.Adam(det_model.parameters())
     tr = Trainer(model, fx.n, [(fx.n, 3, fx.h, fx.w), (fx.n, 17, fx.h, fx.w)], device=DEV)
     if captured:
         tr.capture()
@@ -66,7 +76,7 @@ def test_trainer_two_steps_match_reference(captured):
     # ---- step 1 against the reference's own outputs -------------------------------
     tr.step(xs, y)
     torch.cuda.synchronize()
-    check_logits(tr.logits.cpu(), fx.z["logits64"], fx.z["logits32"], "step1")
+    check_logits(tr.logits.cpu(), fx.z["logits64"], fx.z["logits32"], f"trainer {mode} step1")
     assert abs(tr.loss() - float(fx.z["loss64"])) < 1e-5
     g1 = _grads_by_key(tr)
     ref1, flo1 = reference_grads(fx.params, fx.x, fx.mask, g1, fixture=fx, tag="step1")
@@ -87,13 +97,20 @@ def test_trainer_two_steps_match_reference(captured):
         np.testing.assert_allclose(q.detach().cpu().numpy(), p.detach().numpy(), rtol=2e-6,
                                    atol=1e-9, err_msg=f"adam step 1: {k}")
 
-    # ---- step 2: the oracle on the updated parameters --------------------------------
-    p1 = _cpu_state(tr.model)
+    # ---- step 2 from deterministic parameters: Adam step 1 on the reference gradients
+    for (k, p) in det_model.named_parameters():
+        p.grad = None if k in fx.grad_none else torch.from_numpy(fx.grad(k).copy()).float()
+    det_opt.step()
+    with torch.no_grad():
+        for p, q in zip(tr.model.parameters(), det_model.parameters()):
+            p.copy_(q)
+    tr.load_optimizer_state_dict(det_opt.state_dict())
+    p1 = {k: v.detach().cpu().numpy().copy() for k, v in det_model.state_dict().items()}
     ref_l2, ref_loss2, _, _ = segment_oracle.train_step(dict(p1), fx.x, fx.mask, torch.float64)
     l32, _, _, _ = segment_oracle.train_step(dict(p1), fx.x, fx.mask, torch.float32)
     tr.step()  # same static inputs
     torch.cuda.synchronize()
-    check_logits(tr.logits.cpu(), ref_l2.numpy(), l32.numpy(), "step2")
+    check_logits(tr.logits.cpu(), ref_l2.numpy(), l32.numpy(), f"trainer {mode} step2")
     assert abs(tr.loss() - ref_loss2.item()) < 1e-5
     g2 = _grads_by_key(tr)
     if os.environ.get("ISG_DUMP_DIR"):  # debugging aid: the step-2 state for CPU analysis
@@ -105,10 +122,10 @@ def test_trainer_two_steps_match_reference(captured):
     assert int(tr.step_dev.item()) == 2
 
     # Adam step 2 (bias corrections at step 2; exp_avg/exp_avg_sq carried over)
-    for (k, p) in cpu_model.named_parameters():
+    for (k, p) in det_model.named_parameters():
         p.grad = None if g2[k] is None else g2[k].clone()
-    opt.step()
-    for (k, p), (kk, q) in zip(cpu_model.named_parameters(), tr.model.named_parameters()):
+    det_opt.step()
+    for (k, p), (kk, q) in zip(det_model.named_parameters(), tr.model.named_parameters()):
         np.testing.assert_allclose(q.detach().cpu().numpy(), p.detach().numpy(), rtol=2e-6,
                                    atol=1e-9, err_msg=f"adam step 2: {k}")
     for k in fx.grad_none:  # torch.optim.Adam skips parameters whose grad is None
