@@ -190,21 +190,32 @@ int32_t isg_conv_dgrad(const isg_conv_geom* g, const isg_vtensor* dy, const floa
                        const isg_sinks* dx, isg_stream_t stream);
 
 /* Weight/bias gradient: dw += sum dy (x) im2col(x); dbias += sum dy (either may be
- * NULL). dw and dbias must be zeroed by the caller before the first contribution. */
+ * NULL), into fp64 accumulators that the caller zeroes before the first contribution and
+ * folds to fp32 with isg_sum_replicas (nrep 1). */
 int32_t isg_conv_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x,
-                       float* dw, float* dbias, isg_stream_t stream);
+                       double* dw, double* dbias, isg_stream_t stream);
 
-/* Weight-gradient replicas. A dW element receives one f32 atomic from every workgroup
+/* Weight-gradient replicas. A dW element receives one atomic add from every workgroup
  * along the pixel dimension (hundreds); same-address atomics serialise at the memory
  * side (~40 ns each), so the wgrad kernels add into one of `nrep` replicas of dw/dbias
- * (replica r at dw + r*rep_stride floats), chosen per workgroup, and one
- * isg_sum_replicas pass folds them at the end of the backward. */
+ * (replica r at dw + r*rep_stride elements), chosen per workgroup, and one
+ * isg_sum_replicas pass folds them at the end of the backward.
+ *
+ * The replicas are fp64 and every addend is a workgroup's fp32 partial (reduced in a fixed
+ * order inside the workgroup): an fp64 sum of fp32 values is EXACT — so the same whatever
+ * order the atomics land in — as long as the running sum stays within 2^29 of the smallest
+ * addend's magnitude (53 - 24 significand bits), and otherwise off by at most 2^-53 of
+ * the running sum, 2^-29 of the fp32 result's rounding step. The fold sums the replicas in
+ * fixed order and rounds once to fp32. With the BatchNorm statistics (fp64 sums of fp32
+ * workgroup partials, the same argument) the backward is reproducible bit for bit across
+ * runs (tests/test_gpu_trainer.py::test_backward_is_bitwise_reproducible); with fp32
+ * replicas it was not. */
 #define ISG_WREP 16
 int32_t isg_conv_wgrad_rep(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x,
-                           float* dw, float* dbias, int64_t rep_stride, int32_t nrep,
+                           double* dw, double* dbias, int64_t rep_stride, int32_t nrep,
                            isg_stream_t stream);
-/* dst[i] = sum_{r<nrep} src[r*stride + i] for i < n (fixed order: deterministic). */
-int32_t isg_sum_replicas(float* dst, const float* src, int64_t n, int32_t nrep, int64_t stride,
+/* dst[i] = (float) sum_{r<nrep} src[r*stride + i] for i < n (fp64, fixed order). */
+int32_t isg_sum_replicas(float* dst, const double* src, int64_t n, int32_t nrep, int64_t stride,
                          isg_stream_t stream);
 
 /* ConvTranspose2d forward (segment.py:305-306, 435-436) with kernel = 2*stride,
@@ -365,7 +376,7 @@ typedef struct {
     int64_t y_n_stride;
     double* stats;               /* fwd: NULL or the output's BN statistics block */
     isg_vtensor dy;              /* wgrad */
-    float* dw;                   /* wgrad: [Co][Ci][KH][KW] (+ replicas) */
+    double* dw;                  /* wgrad: [Co][Ci][KH][KW] fp64 (+ replicas) */
     int64_t rep_stride;
     int32_t nrep;
     int32_t k;                   /* pool: window */
@@ -389,7 +400,7 @@ int32_t isg_kp_pool(const isg_kp_stem* a, isg_stream_t stream);
  *        needs it (the 3x3's weight gradient border term).
  *   bwd: dx (sinks: STORE / ACCUM without statistics) = dL/dx; dw1/db1/dw2/db2 += the
  *        parameter gradients, added into replica (workgroup % nrep) of each (replica r at
- *        + r*rep_stride floats; NULL skips one); `ring` as written by the forward
+ *        + r*rep_stride elements; NULL skips one); `ring` as written by the forward
  *        (required). Replaces the unfused isg_convT_fwd + isg_conv_fwd (+ their dgrad /
  *        wgrad) pair, which round-trips the intermediate through HBM. */
 #define ISG_HEAD_RING(Hi, Wi) (2 * (4 * (int64_t)(Wi) + 2) + 2 * 4 * (int64_t)(Hi))
@@ -404,10 +415,10 @@ typedef struct {
     const float* dout;           /* bwd: dL/dlogits */
     int64_t dout_n_stride;
     isg_sinks dx;                /* bwd */
-    float* dw1;
-    float* db1;
-    float* dw2;
-    float* db2;
+    double* dw1;                 /* bwd: fp64 accumulators (+ replicas, isg_conv_wgrad_rep) */
+    double* db1;
+    double* dw2;
+    double* db2;
     int64_t rep_stride;
     int32_t nrep;
     int32_t N, Hi, Wi;

@@ -40,14 +40,14 @@ int32_t isg_dense_conv_fwd(const isg_conv_geom*, const isg_vtensor*, const float
                            hipStream_t);
 int32_t isg_dense_conv_dgrad(const isg_conv_geom*, const isg_vtensor*, const float*, const isg_sinks*,
                              hipStream_t);
-int32_t isg_dense_conv_wgrad(const isg_conv_geom*, const isg_vtensor*, const isg_vtensor*, float*,
-                             float*, int64_t, int32_t, hipStream_t);
+int32_t isg_dense_conv_wgrad(const isg_conv_geom*, const isg_vtensor*, const isg_vtensor*, double*,
+                             double*, int64_t, int32_t, hipStream_t);
 int32_t isg_depthwise_fwd(const isg_conv_geom*, const isg_vtensor*, const float*, const isg_sinks*,
                           hipStream_t);
 int32_t isg_depthwise_dgrad(const isg_conv_geom*, const isg_vtensor*, const float*, const isg_sinks*,
                             hipStream_t);
-int32_t isg_depthwise_wgrad(const isg_conv_geom*, const isg_vtensor*, const isg_vtensor*, float*,
-                            float*, int64_t, int32_t, hipStream_t);
+int32_t isg_depthwise_wgrad(const isg_conv_geom*, const isg_vtensor*, const isg_vtensor*, double*,
+                            double*, int64_t, int32_t, hipStream_t);
 
 static int32_t check_geom(const isg_conv_geom* g) {
     if (!g) return isg_set_error(ISG_ERR_INVALID, "conv: NULL geometry");
@@ -74,9 +74,9 @@ int32_t isg_tap_conv(const isg_conv_geom*, const isg_vtensor*, const float*, con
                      bool, hipStream_t);
 int32_t isg_s2k5_fwd(const isg_conv_geom*, const isg_vtensor*, const float*, const isg_sinks*,
                      hipStream_t);
-int32_t isg_s2k5_wgrad(const isg_conv_geom*, const isg_vtensor*, const isg_vtensor*, float*, float*,
+int32_t isg_s2k5_wgrad(const isg_conv_geom*, const isg_vtensor*, const isg_vtensor*, double*, double*,
                        int64_t, int32_t, hipStream_t);
-int32_t isg_tap_wgrad(const isg_conv_geom*, const isg_vtensor*, const isg_vtensor*, float*, float*,
+int32_t isg_tap_wgrad(const isg_conv_geom*, const isg_vtensor*, const isg_vtensor*, double*, double*,
                       int64_t, int32_t, hipStream_t);
 
 // a conv over the first Ci of the weight's w_ci input channels (the keypoint stem's RGB
@@ -113,7 +113,7 @@ int32_t isg_conv_dgrad(const isg_conv_geom* g, const isg_vtensor* dy, const floa
 }
 
 int32_t isg_conv_wgrad_rep(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x,
-                           float* dw, float* dbias, int64_t rep_stride, int32_t nrep,
+                           double* dw, double* dbias, int64_t rep_stride, int32_t nrep,
                            isg_stream_t st) {
     if (int32_t e = check_geom(g)) return e;
     if (nrep < 1 || (nrep > 1 && rep_stride <= 0))
@@ -132,7 +132,7 @@ int32_t isg_conv_wgrad_rep(const isg_conv_geom* g, const isg_vtensor* dy, const 
 }
 
 int32_t isg_conv_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x,
-                       float* dw, float* dbias, isg_stream_t st) {
+                       double* dw, double* dbias, isg_stream_t st) {
     return isg_conv_wgrad_rep(g, dy, x, dw, dbias, 0, 1, st);
 }
 
@@ -173,15 +173,15 @@ struct WgradRec {
     isg_conv_geom g;
     isg_vtensor dy;
     isg_vtensor x;
-    float* dw;
-    float* dbias;
+    double* dw;
+    double* dbias;
     int64_t rep_stride;
     int32_t nrep;
     int32_t pad_;
 };
 struct SumRepRec {
     float* dst;
-    const float* src;
+    const double* src;
     int64_t n;
     int64_t stride;
     int32_t nrep;
@@ -249,14 +249,14 @@ static int32_t run_op_raw(int32_t kind, char* buf, isg_stream_t st);
 // wgrad.hip: grouped 1x1 weight gradients (the executor's side-stream batches)
 int32_t isg_pwg_plan_bytes();
 int32_t isg_pwg_group_max();
-int32_t isg_pwg_plan(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, float* dw,
-                     float* dbias, int64_t rep_stride, int32_t nrep, void* plan);
+int32_t isg_pwg_plan(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, double* dw,
+                     double* dbias, int64_t rep_stride, int32_t nrep, void* plan);
 int32_t isg_pwg_run(const void* const* plans, int32_t n, hipStream_t st);
 // dw_convt.hip: grouped depthwise weight gradients
 int32_t isg_dwg_plan_bytes();
 int32_t isg_dwg_group_max();
-int32_t isg_dwg_plan(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, float* dw,
-                     float* dbias, int64_t rep_stride, int32_t nrep, void* plan);
+int32_t isg_dwg_plan(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, double* dw,
+                     double* dbias, int64_t rep_stride, int32_t nrep, void* plan);
 int32_t isg_dwg_run(const void* const* plans, int32_t n, hipStream_t st);
 
 // BN finalisation the producing kernel did not fuse (its launcher did not report

@@ -23,6 +23,7 @@
 namespace {
 
 constexpr int kWaves = 4;
+static_assert(kWaves == 4, "the epilogue sums the per-wave partials of 4 waves");
 constexpr int kThreads = kWaves * 64;
 constexpr int kKtabMax = 1024;
 constexpr int kMaxRows = 256;
@@ -61,7 +62,8 @@ __global__ __launch_bounds__(kThreads) void gemm_conv_kernel(GemmArgs a) {
     __shared__ KEnt ktab[kKtabMax];
     __shared__ ChanCoef coef[ISG_MAX_CH];
     __shared__ SinkCoef scoef[kMaxRows];
-    __shared__ float red[3][kMaxRows];
+    // per-wave partials (summed in wave order before the flush: deterministic, no LDS atomics)
+    __shared__ float red[kWaves][3][kMaxRows];
     __shared__ int s_K, s_oy0, s_ox0, s_TH, s_TW;
 
     const int tid = threadIdx.x;
@@ -108,7 +110,7 @@ __global__ __launch_bounds__(kThreads) void gemm_conv_kernel(GemmArgs a) {
     }
     load_vt_coefs(a.src, coef, tid, kThreads);
     load_sink_coefs(a.out, scoef, tid, kThreads);
-    for (int i = tid; i < kMaxRows; i += kThreads) red[0][i] = red[1][i] = red[2][i] = 0.f;
+    for (int i = tid; i < kWaves * 3 * kMaxRows; i += kThreads) (&red[0][0][0])[i] = 0.f;
     __syncthreads();
 
     const int K = s_K;
@@ -179,10 +181,10 @@ __global__ __launch_bounds__(kThreads) void gemm_conv_kernel(GemmArgs a) {
                         rr.r1 += __shfl_xor(rr.r1, o, 64);
                         rr.r2 += __shfl_xor(rr.r2, o, 64);
                     }
-                    if (pl == 0 && row < a.M) {
-                        atomicAdd(&red[0][row], rr.r0);
-                        atomicAdd(&red[1][row], rr.r1);
-                        atomicAdd(&red[2][row], rr.r2);
+                    if (pl == 0 && row < a.M) {  // one lane of this wave owns the row
+                        red[wave][0][row] += rr.r0;
+                        red[wave][1][row] += rr.r1;
+                        red[wave][2][row] += rr.r2;
                     }
                 }
             }
@@ -190,7 +192,12 @@ __global__ __launch_bounds__(kThreads) void gemm_conv_kernel(GemmArgs a) {
     }
     if (need_red) {
         __syncthreads();
-        flush_sink_red(a.out, red[0], red[1], red[2], a.M, tid, kThreads);
+        for (int i = tid; i < 3 * kMaxRows; i += kThreads) {
+            float* r = &red[0][0][0] + i;
+            *r = ((r[0] + r[3 * kMaxRows]) + r[6 * kMaxRows]) + r[9 * kMaxRows];
+        }
+        __syncthreads();
+        flush_sink_red(a.out, red[0][0], red[0][1], red[0][2], a.M, tid, kThreads);
     }
     sinks_finalize(a.out);
 }

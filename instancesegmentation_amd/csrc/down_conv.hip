@@ -36,7 +36,7 @@ struct DownArgs {
     isg_vtensor x;     // wgrad: M channels, cell grid H x W
     isg_sinks out;     // input gradient: M channels on the cell grid
     const float* w;    // [M][C][2S][2S]
-    float* dw;
+    double* dw;
     int64_t rep_stride;
     int nrep;
     int N, M, C, H, W;  // cell grid
@@ -224,7 +224,7 @@ __global__ __launch_bounds__(kThreads) void down_wgrad_kernel(DownArgs a) {
         }
     }
     if (tid < ncol) {
-        float* const dwr = a.dw + (int64_t)(blockIdx.x % (unsigned)a.nrep) * a.rep_stride;
+        double* const dwr = a.dw + (int64_t)(blockIdx.x % (unsigned)a.nrep) * a.rep_stride;
 #pragma unroll
         for (int m = 0; m < M; ++m)
             if (m < a.M) atomicAdd(&dwr[((int64_t)m * a.C + c) * K * K + tap], acc[m >> 2][m & 3]);
@@ -610,8 +610,8 @@ static_assert(2 * kWgNW <= kWgLds, "s2k5 wgrad epilogue regions");
 struct S2wArgs {
     isg_vtensor dy;  // the conv's output gradient: M channels, OH x OW
     isg_vtensor x;   // its input: C channels, 2 OH x 2 OW
-    float* dw;       // [M][wc][5][5] (the first C input channels written)
-    float* dbias;
+    double* dw;       // [M][wc][5][5] (the first C input channels written)
+    double* dbias;
     int64_t rep_stride;
     int nrep;
     int N, M, C, wc, OH, OW;
@@ -857,7 +857,7 @@ __global__ __launch_bounds__(2 * kThreads, 1) void s2k5_wgrad_kernel(S2wArgs a) 
         }
         __syncthreads();  // E2
     }
-    float* const dwr = a.dw + (int64_t)(blockIdx.x % a.nrep) * a.rep_stride;
+    double* const dwr = a.dw + (int64_t)(blockIdx.x % a.nrep) * a.rep_stride;
     if (NARROW) {
         for (int e = tid; e < kNarNW; e += 2 * kThreads) {
             const int m = e / (kNarN * 16), n = e - m * (kNarN * 16), c = n / 25, tap = n - c * 25;
@@ -1175,7 +1175,7 @@ int32_t isg_down_conv_fwd(const isg_conv_geom* g, const isg_vtensor* src, const 
 // weight gradient of the stride-S down conv: dy = the conv's OUTPUT gradient (M channels
 // on the cell grid), x = its input (C channels, S x the grid) — the plan's roles
 int32_t isg_down_conv_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x,
-                            float* dw, float* dbias, int64_t rep_stride, int32_t nrep,
+                            double* dw, double* dbias, int64_t rep_stride, int32_t nrep,
                             hipStream_t st) {
     static const bool off = getenv("ISG_NO_DOWN_CONV") != nullptr;
     int S = 0;
@@ -1283,7 +1283,7 @@ int32_t isg_s2k5_fwd(const isg_conv_geom* g, const isg_vtensor* x, const float* 
 // 5x5 stride 2 pad 2 weight gradient with <= 16 input / output channels (s2k5_wgrad_kernel).
 // Returns 1 if launched, 0 if the shape is not for this kernel, <0 on error.
 int32_t isg_s2k5_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x,
-                       float* dw, float* dbias, int64_t rep_stride, int32_t nrep, hipStream_t st) {
+                       double* dw, double* dbias, int64_t rep_stride, int32_t nrep, hipStream_t st) {
     static const bool off = getenv("ISG_NO_S2K5_WGRAD") != nullptr;
     if (off || g->groups != 1 || g->SH != 2 || g->SW != 2 || g->KH != 5 || g->KW != 5 ||
         g->PH != 2 || g->PW != 2 || g->DH != 1 || g->DW != 1 || g->H != 2 * g->OH ||

@@ -375,8 +375,8 @@ constexpr int kDwU = 4;
 constexpr int kDwPix = kThreads * kDwU;
 struct DwWgArgs {
     isg_vseg dy, x;
-    float* dw;
-    float* dbias;
+    double* dw;
+    double* dbias;
     int64_t rep_stride;
     int nrep;
     int N, C, H, W, OH, OW, KH, KW, PH, PW, DH, DW;
@@ -720,7 +720,7 @@ int32_t isg_depthwise_dgrad(const isg_conv_geom* g, const isg_vtensor* dy, const
 }
 
 int32_t isg_depthwise_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x,
-                            float* dw, float* dbias, int64_t rep_stride, int32_t nrep,
+                            double* dw, double* dbias, int64_t rep_stride, int32_t nrep,
                             hipStream_t st) {
     if (dy->nseg != 1 || x->nseg != 1 || g->KH * g->KW > kMaxTaps || x->s[0].xform == ISG_XF_BN_BWD)
         return isg_set_error(ISG_ERR_UNSUPPORTED, "depthwise wgrad: need 1 seg, <= 9 taps, x not BN-backward");
@@ -823,7 +823,7 @@ extern "C" int32_t isg_dwg_group_max() { return kDwgGroup; }
 
 // > 0 (the tap-shape key) when isg_conv_wgrad_rep would run this op on dw_wgrad_tile_kernel
 extern "C" int32_t isg_dwg_plan(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x,
-                                float* dw, float* dbias, int64_t rep_stride, int32_t nrep, void* plan) {
+                                double* dw, double* dbias, int64_t rep_stride, int32_t nrep, void* plan) {
     if (!dw || nrep < 1 || (nrep > 1 && rep_stride <= 0)) return 0;
     if (g->groups == 1 || g->groups != g->Ci || g->Ci != g->Co || (g->w_ci && g->w_ci != g->Ci)) return 0;
     if (dy->nseg != 1 || x->nseg != 1 || g->KH * g->KW > kMaxTaps || x->s[0].xform == ISG_XF_BN_BWD) return 0;

@@ -778,20 +778,26 @@ __global__ void fill_f64_kernel(double* p, int64_t n, double v) {
 // Fold the ISG_WREP weight-gradient replicas: dst[i] = sum_r src[r*stride + i] (fixed
 // order), 4 elements per lane with 16-B loads where the layout allows.
 __global__ __launch_bounds__(kThreads) void sum_rep_kernel(float* __restrict__ dst,
-                                                            const float* __restrict__ src,
+                                                            const double* __restrict__ src,
                                                             int64_t n, int nrep, int64_t stride) {
+    typedef double f64x2 __attribute__((ext_vector_type(2)));
     const int64_t i4 = ((int64_t)blockIdx.x * kThreads + threadIdx.x) * 4;
     if (i4 >= n) return;
-    if (i4 + 4 <= n && (stride & 3) == 0 && ((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 15) == 0) {
-        f32x4 acc = *reinterpret_cast<const f32x4*>(src + i4);
-        for (int r = 1; r < nrep; ++r) acc += *reinterpret_cast<const f32x4*>(src + r * stride + i4);
-        *reinterpret_cast<f32x4*>(dst + i4) = acc;
+    if (i4 + 4 <= n && (stride & 3) == 0 && ((uintptr_t)src & 31) == 0 && ((uintptr_t)dst & 15) == 0) {
+        const f64x2* s0 = reinterpret_cast<const f64x2*>(src + i4);
+        f64x2 a0 = s0[0], a1 = s0[1];
+        for (int r = 1; r < nrep; ++r) {
+            const f64x2* sr = reinterpret_cast<const f64x2*>(src + r * stride + i4);
+            a0 += sr[0];
+            a1 += sr[1];
+        }
+        *reinterpret_cast<f32x4*>(dst + i4) = f32x4{(float)a0[0], (float)a0[1], (float)a1[0], (float)a1[1]};
         return;
     }
     for (int64_t i = i4; i < n && i < i4 + 4; ++i) {
-        float acc = src[i];
+        double acc = src[i];
         for (int r = 1; r < nrep; ++r) acc += src[r * stride + i];
-        dst[i] = acc;
+        dst[i] = (float)acc;
     }
 }
 
@@ -949,7 +955,7 @@ int32_t isg_adam_dev(float* param, const float* grad, float* exp_avg, float* exp
     return isg_check_launch("adam_dev_kernel");
 }
 
-int32_t isg_sum_replicas(float* dst, const float* src, int64_t n, int32_t nrep, int64_t stride,
+int32_t isg_sum_replicas(float* dst, const double* src, int64_t n, int32_t nrep, int64_t stride,
                          isg_stream_t st) {
     if (n <= 0) return 0;
     if (!dst || !src || nrep < 1 || (nrep > 1 && stride < n))

@@ -43,7 +43,7 @@ struct KpArgs {
     int64_t y_ns;
     double* stats;
     isg_vtensor dy;
-    float* dw;
+    double* dw;
     int64_t rep_stride;
     int nrep;
     int k;
@@ -287,7 +287,7 @@ __global__ __launch_bounds__(kThreads) void kp_wgrad_kernel(KpArgs a) {
             acc[u] += (s4[0] + s4[1]) + (s4[2] + s4[3]);
         }
     }
-    float* const dwr = a.dw + (int64_t)((blockIdx.x + 7u * blockIdx.y) % (unsigned)a.nrep) * a.rep_stride;
+    double* const dwr = a.dw + (int64_t)((blockIdx.x + 7u * blockIdx.y) % (unsigned)a.nrep) * a.rep_stride;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
         const int e = tid + u * kThreads;

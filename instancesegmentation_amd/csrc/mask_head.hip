@@ -364,7 +364,7 @@ __global__ __launch_bounds__(kThreads, 2) void head_bwd_v1_kernel(isg_mask_head 
     // ---- fold the partial weight gradients into this workgroup's replica
     const int rep = blockIdx.x % a.nrep;
     if (a.dw1) {
-        float* d = a.dw1 + (int64_t)rep * a.rep_stride;
+        double* d = a.dw1 + (int64_t)rep * a.rep_stride;
         // D lane: ci = 4kq + i, column (co, ky, kx) = (wave * 4 + t) * 16 + nl
 #pragma unroll
         for (int t = 0; t < 4; ++t)
@@ -386,7 +386,7 @@ __global__ __launch_bounds__(kThreads, 2) void head_bwd_v1_kernel(isg_mask_head 
         const float s = tid <= kCm * 9 ? acc2[tid]
                                        : (red[j * 4] + red[j * 4 + 1]) + (red[j * 4 + 2] + red[j * 4 + 3]);
         const int64_t ro = (int64_t)rep * a.rep_stride;
-        float* dst = nullptr;
+        double* dst = nullptr;
         if (tid < kCm * 9) dst = a.dw2 ? a.dw2 + ro + tid : nullptr;
         else if (tid == kCm * 9) dst = a.db2 ? a.db2 + ro : nullptr;
         else dst = a.db1 ? a.db1 + ro + (tid - kCm * 9 - 1) : nullptr;
@@ -881,7 +881,7 @@ __global__ __launch_bounds__(2 * kThreads, 1) void head_bwd_kernel(isg_mask_head
         return;
     }
     if (a.dw1) {
-        float* d = a.dw1 + ro;
+        double* d = a.dw1 + ro;
 #pragma unroll
         for (int t = 0; t < 4; ++t)
 #pragma unroll

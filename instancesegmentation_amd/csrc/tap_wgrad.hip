@@ -38,8 +38,8 @@ constexpr int kMaxC = 64;
 struct TwArgs {
     isg_vtensor dy;   // N x Co x OH x OW (Co <= 16)
     isg_vtensor x;    // N x C x H x W
-    float* dw;        // [Co][C][KH][KW], replica r at dw + r*rep_stride
-    float* dbias;     // [Co] or NULL
+    double* dw;        // [Co][C][KH][KW], replica r at dw + r*rep_stride
+    double* dbias;     // [Co] or NULL
     int64_t rep_stride;
     int nrep;
     int N, C, Co, H, W, OH, OW, KH, KW, SH, SW, PH, PW, DH, DW, KK;
@@ -221,7 +221,7 @@ __global__ __launch_bounds__(kThreads) void tap_wgrad_kernel(TwArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) red[(wave * 16 + kq * 4 + r) * ncol + t * 16 + pl] = acc[t][r];
     __syncthreads();
-    float* const dwr = a.dw + (int64_t)(blockIdx.x % a.nrep) * a.rep_stride;
+    double* const dwr = a.dw + (int64_t)(blockIdx.x % a.nrep) * a.rep_stride;
     for (int e = tid; e < 16 * ncol; e += kThreads) {
         const int co = e / ncol, j = e - co * ncol;
         const int t = j >> 4, l16 = j & 15;
@@ -378,8 +378,8 @@ constexpr int kDyPT = 7;       // dy tile elements per thread (16 x 4 x BX, BX <
 struct TwaArgs {
     isg_vtensor dy;
     isg_vtensor x;
-    float* dw;
-    float* dbias;
+    double* dw;
+    double* dbias;
     int64_t rep_stride;
     int nrep;
     int N, C, Co, H, W, OH, OW, KH, KW, PH, PW, KK;
@@ -550,7 +550,7 @@ __global__ __launch_bounds__(kThreads, 2) void tap_wgrad_all_kernel(TwaArgs a) {
     }
 
     // ---- epilogue: waves own disjoint columns; one atomic per dW element per workgroup
-    float* const dwr = a.dw + (int64_t)(blockIdx.x % a.nrep) * a.rep_stride;
+    double* const dwr = a.dw + (int64_t)(blockIdx.x % a.nrep) * a.rep_stride;
 #pragma unroll
     for (int t = 0; t < NTW; ++t) {
         if (!cval[t] || (a.dbg & 8)) continue;
@@ -666,8 +666,8 @@ bool twa_layout(TwaArgs& a, int& ntiles) {
 }
 
 // Returns 1 if launched, 0 if the shape is not for this kernel, <0 on error.
-int32_t twa_try(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, float* dw,
-                float* dbias, int64_t rep_stride, int32_t nrep, hipStream_t st) {
+int32_t twa_try(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, double* dw,
+                double* dbias, int64_t rep_stride, int32_t nrep, hipStream_t st) {
     static const bool off = getenv("ISG_NO_TWA") != nullptr;
     if (off || g->SH != 2 || g->SW != 2 || g->DH != 1 || g->DW != 1) return 0;
     if (g->PW % 2 || g->W % 2) return 0;
@@ -751,8 +751,8 @@ int32_t twa_try(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor
 }  // namespace
 
 // Returns 1 if launched, 0 if the shape is not for this kernel, <0 on error.
-int32_t isg_tap_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, float* dw,
-                      float* dbias, int64_t rep_stride, int32_t nrep, hipStream_t st) {
+int32_t isg_tap_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, double* dw,
+                      double* dbias, int64_t rep_stride, int32_t nrep, hipStream_t st) {
     static const bool off = getenv("ISG_NO_TAP_WGRAD") != nullptr;
     if (off || g->groups != 1 || g->Co > 16 || g->Ci > kMaxC) return 0;
     for (int i = 0; i < x->nseg; ++i)

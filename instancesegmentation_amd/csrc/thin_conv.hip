@@ -218,8 +218,8 @@ __global__ __launch_bounds__(kThreads) void thin_conv3_x4_kernel(ThinArgs a) {
 // per element into one of nrep replicas (include/isg.h ISG_WREP).
 struct ThinWgArgs {
     isg_vtensor dy, x;
-    float* dw;
-    float* dbias;
+    double* dw;
+    double* dbias;
     int64_t rep_stride;
     int nrep;
     int N, H, W;
@@ -339,8 +339,8 @@ int32_t isg_thin_conv(const isg_conv_geom* g, const isg_vtensor* src, const floa
 }
 
 // Returns 1 if launched, 0 if the shape is not for this kernel, <0 on error.
-int32_t isg_thin_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, float* dw,
-                       float* dbias, int64_t rep_stride, int32_t nrep, hipStream_t st) {
+int32_t isg_thin_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, double* dw,
+                       double* dbias, int64_t rep_stride, int32_t nrep, hipStream_t st) {
     static const bool off = getenv("ISG_NO_THIN_WGRAD") != nullptr;
     if (off || g->groups != 1 || g->SH != 1 || g->SW != 1 || g->KH != 3 || g->KW != 3 ||
         g->PH != 1 || g->PW != 1 || g->DH != 1 || g->DW != 1 || g->OH != g->H || g->OW != g->W ||

@@ -39,8 +39,8 @@ constexpr int kXs = 9216;           // halo floats per block (36 KB) incl. chann
 struct WgArgs {
     isg_vtensor dy;  // rows: N x R x OH x OW
     isg_vtensor x;   // gathered: N x Ci x H x W
-    float* dw;
-    float* dbias;
+    double* dw;
+    double* dbias;
     int64_t rep_stride;
     int nrep;
     int N, OH, OW, H, W, R, Ci, KH, KW, SH, SW, PH, PW, DH, DW;
@@ -160,7 +160,7 @@ __global__ __launch_bounds__(kThreads) void wgrad_kernel(WgArgs a) {
     const int ohw = a.OH * a.OW, xhw = a.H * a.W;
     // this workgroup's replica of dW / dbias (include/isg.h ISG_WREP)
     const int64_t rep_off = (int64_t)((blockIdx.x + 7u * blockIdx.y) % (unsigned)a.nrep) * a.rep_stride;
-    float* const dwr = a.dw + rep_off;
+    double* const dwr = a.dw + rep_off;
 
     for (int i = tid; i < Rb; i += kThreads) tA[i] = ch_table_entry(a.dy, r_lo + i, ohw);
     for (int i = tid; i < nci; i += kThreads) tX[i] = ch_table_entry(a.x, ci_lo + i, xhw);
@@ -325,8 +325,8 @@ constexpr int kGMaxRows = 192;      // BR + BC
 
 struct PwgArgs {
     isg_vtensor dy, x;
-    float* dw;
-    float* dbias;
+    double* dw;
+    double* dbias;
     int64_t rep_stride;
     int nrep;
     int HW, R, C, BR, BC, ncb;
@@ -373,7 +373,7 @@ ISG_DEV void pwg_body(const PwgArgs& a, const unsigned bx, const unsigned by) {
     const int Rb = min(a.BR, a.R - r0), Cb = min(a.BC, a.C - c0);
     const int BR = a.BR, NR = a.BR + a.BC;
     const int64_t rep_off = (int64_t)((bx + 7u * by) % (unsigned)a.nrep) * a.rep_stride;
-    float* const dwr = a.dw + rep_off;
+    double* const dwr = a.dw + rep_off;
     STAMP(0);
 
     // ---- tables: row j < BR is dy channel r0 + j, else x channel c0 + j - BR -------------
@@ -589,8 +589,8 @@ constexpr int kKMaxRows = 64;        // BR + BC
 
 struct PwkArgs {
     isg_vtensor dy, x;
-    float* dw;
-    float* dbias;
+    double* dw;
+    double* dbias;
     int64_t rep_stride;
     int nrep;
     int HW, R, C, ncb;
@@ -783,7 +783,7 @@ __global__ __launch_bounds__(kThreads) void pwk_kernel(PwkArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) S[((wave * NT + i) * 4 + r) * 64 + lane] = acc[i][r];
     __syncthreads();
-    float* const dwr = a.dw + rep_off;
+    double* const dwr = a.dw + rep_off;
     {
         const int r = tid >> 6, l = tid & 63;  // element (tile i, acc slot r, lane l)
 #pragma unroll
@@ -812,8 +812,8 @@ int32_t pwk_launch(const PwkArgs& a, dim3 grid, hipStream_t st) {
 }
 
 // returns 1 when launched, 0 when the shape is not for this kernel, <0 on error
-int32_t pwk_try(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, float* dw,
-                float* dbias, int64_t rep_stride, int32_t nrep, hipStream_t st) {
+int32_t pwk_try(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, double* dw,
+                double* dbias, int64_t rep_stride, int32_t nrep, hipStream_t st) {
     // opt-in (ISG_PWK=1): faster alone (kbench 48 -> 128 at 64^2: 16.8 -> 13.1 us) but
     // slower in the step (4.01 -> 4.11 ms, 2 interleaved pairs): its 256-384 workgroups of
     // 68 KB LDS take the CUs the input-gradient chain runs on, where pwg's fewer, thinner
@@ -883,8 +883,8 @@ struct PwgPlan {
 };
 
 // the shape and operand checks of pwg_try and the launch geometry; false: not for pwg
-bool pwg_plan(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, float* dw,
-              float* dbias, int64_t rep_stride, int32_t nrep, PwgPlan& pl) {
+bool pwg_plan(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, double* dw,
+              double* dbias, int64_t rep_stride, int32_t nrep, PwgPlan& pl) {
     static const bool off = getenv("ISG_PWG_OFF") != nullptr;
     if (off) return false;
     if (!(g->KH == 1 && g->KW == 1 && g->SH == 1 && g->SW == 1 && g->PH == 0 && g->PW == 0))
@@ -992,8 +992,8 @@ int32_t pwg_run(const PwgPlan* const* pl, int n, hipStream_t st) {
 }
 
 // returns 1 when launched, 0 when the shape is not for this kernel, <0 on error
-int32_t pwg_try(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, float* dw,
-                float* dbias, int64_t rep_stride, int32_t nrep, hipStream_t st) {
+int32_t pwg_try(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, double* dw,
+                double* dbias, int64_t rep_stride, int32_t nrep, hipStream_t st) {
     {
         static const bool off = getenv("ISG_PWG_OFF") != nullptr;
         if (off) return 0;
@@ -1021,19 +1021,19 @@ int vt_channels(const isg_vtensor* v) {
 
 ISG_STAMP_ACCESSOR(isg_dbg_stamps_wgrad)
 
-int32_t isg_tap_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, float* dw,
-                      float* dbias, int64_t rep_stride, int32_t nrep, hipStream_t st);
+int32_t isg_tap_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, double* dw,
+                      double* dbias, int64_t rep_stride, int32_t nrep, hipStream_t st);
 
-int32_t isg_thin_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, float* dw,
-                       float* dbias, int64_t rep_stride, int32_t nrep, hipStream_t st);
+int32_t isg_thin_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, double* dw,
+                       double* dbias, int64_t rep_stride, int32_t nrep, hipStream_t st);
 int32_t isg_down_conv_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x,
-                            float* dw, float* dbias, int64_t rep_stride, int32_t nrep,
+                            double* dw, double* dbias, int64_t rep_stride, int32_t nrep,
                             hipStream_t st);
 int32_t isg_s2k5_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x,
-                       float* dw, float* dbias, int64_t rep_stride, int32_t nrep, hipStream_t st);
+                       double* dw, double* dbias, int64_t rep_stride, int32_t nrep, hipStream_t st);
 
 int32_t isg_dense_conv_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x,
-                             float* dw, float* dbias, int64_t rep_stride, int32_t nrep,
+                             double* dw, double* dbias, int64_t rep_stride, int32_t nrep,
                              hipStream_t st) {
     if (vt_channels(dy) != g->Co || vt_channels(x) != g->Ci)
         return isg_set_error(ISG_ERR_INVALID, "conv wgrad: channel mismatch");
@@ -1136,8 +1136,8 @@ int32_t isg_dense_conv_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, cons
 extern "C" int32_t isg_pwg_plan_bytes() { return (int32_t)sizeof(PwgPlan); }
 extern "C" int32_t isg_pwg_group_max() { return kPwgGroup; }
 
-extern "C" int32_t isg_pwg_plan(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, float* dw,
-                     float* dbias, int64_t rep_stride, int32_t nrep, void* plan) {
+extern "C" int32_t isg_pwg_plan(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, double* dw,
+                     double* dbias, int64_t rep_stride, int32_t nrep, void* plan) {
     const char* pe = getenv("ISG_PWK");
     if (pe && atoi(pe)) return 0;  // the opt-in pwk path stays on the per-op route
     if (!dw || nrep < 1 || (nrep > 1 && rep_stride <= 0) || g->groups != 1) return 0;

@@ -36,7 +36,7 @@ S_IN = (6, 7)
 S_OUT = (8, 9)
 S_DOUT = (10, 11)
 S_DIN = (12, 13)
-S_WREP = 14  # L.WREP replicas of the flat parameter gradient (wgrad atomics, isg.h)
+S_WREP = 14  # L.WREP fp64 replicas of the flat parameter gradient (wgrad atomics, isg.h)
 S_TENSOR0 = 16
 
 ALIGN = 64  # elements (256 B) between arena buffers
@@ -281,11 +281,11 @@ class Graph:
         return Ptr(S_PGRAD, self.pgrad_off[k] * 4)
 
     def wrep_ptr(self, mod, attr):
-        """Replica 0 of a parameter's gradient in the S_WREP arena (L.WREP replicas of the
-        flat gradient, stride pgrad_size floats); folded into S_PGRAD by OP_SUM_REP."""
+        """Replica 0 of a parameter's gradient in the S_WREP arena (L.WREP fp64 replicas of
+        the flat gradient, stride pgrad_size doubles); folded into S_PGRAD by OP_SUM_REP."""
         k = self.pname(mod, attr)
         self.used_params.add(k)
-        return Ptr(S_WREP, self.pgrad_off[k] * 4)
+        return Ptr(S_WREP, self.pgrad_off[k] * 8)
 
     # -- allocation ----------------------------------------------------------------------
     def act_buf(self, C, H, W, name):
@@ -1119,7 +1119,7 @@ class Plan:
 
         def touches_early(r):
             for _, slot, off in r.fix:
-                if slot in (S_PGRAD, S_WREP) and off >= cut * 4:
+                if (slot == S_PGRAD and off >= cut * 4) or (slot == S_WREP and off >= cut * 8):
                     return True
                 if slot == S_STATS and any(lo <= off < hi for lo, hi in early_stats):
                     return True
@@ -1150,10 +1150,11 @@ class Plan:
                 b = v.segs[0].buf
                 gs.external[id(b)] = Buf(S_DIN[i], b.N, b.C, b.H, b.W, f"din{i}")
         bw = OpList()
-        # weight gradients accumulate (atomics) into L.WREP replicas, folded into S_PGRAD
-        # by OP_SUM_REP before the BN/PReLU finalisation overwrites its own entries
+        # weight gradients accumulate (fp64 atomics of fp32 workgroup partials: exact, so
+        # order-independent, isg.h ISG_WREP) into L.WREP replicas, folded into S_PGRAD by
+        # OP_SUM_REP before the BN/PReLU finalisation overwrites its own entries
         bw.add(Record(L.OP_MEMSET, L.MemsetRec, {"p": Ptr(S_WREP),
-                                                 "bytes": L.WREP * g.pgrad_size * 4}))
+                                                 "bytes": L.WREP * g.pgrad_size * 8}))
         body = OpList()
         gs.pending_final = []
         for op in reversed(g.ops):
@@ -1205,7 +1206,7 @@ class Plan:
             recs = []
             if hi > lo:
                 recs.append(Record(L.OP_SUM_REP, L.SumRepRec,
-                                   {"dst": Ptr(S_PGRAD, lo * 4), "src": Ptr(S_WREP, lo * 4),
+                                   {"dst": Ptr(S_PGRAD, lo * 4), "src": Ptr(S_WREP, lo * 8),
                                     "n": hi - lo, "stride": g.pgrad_size, "nrep": L.WREP},
                                    label="sum_wgrad_replicas"))
                 if not side:  # every forked weight gradient is in the replicas

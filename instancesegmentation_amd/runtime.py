@@ -118,7 +118,7 @@ class Runner:
         dev = act.device
         grad = _arena(max(p.grad_size, 1), torch.float32, dev)
         pgrad = _arena(max(p.graph.pgrad_size, 1), torch.float32, dev)
-        wrep = _arena(L.WREP * max(p.graph.pgrad_size, 1), torch.float32, dev)
+        wrep = _arena(L.WREP * max(p.graph.pgrad_size, 1), torch.float64, dev)
         dins = []
         for i, x in enumerate(xs):
             if in_grad[i]:

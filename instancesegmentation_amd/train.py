@@ -141,7 +141,7 @@ class Trainer:
         self.pgrad = self.grad_flat
         cut = self.plan.bucket_cut
         self.buckets = [self.comm[cut:], self.comm[:cut]]  # launch order: 1 (+buffers), 2
-        self.wrep = torch.empty(L.WREP * g.pgrad_size, dtype=torch.float32, device=dev)
+        self.wrep = torch.empty(L.WREP * g.pgrad_size, dtype=torch.float64, device=dev)
         self.logits = torch.empty(self.plan.out_shapes[0], dtype=torch.float32, device=dev)
         self.dlogits = torch.empty_like(self.logits)
         # BCELoss mean over this replica's pixels, pre-divided by the world size so the

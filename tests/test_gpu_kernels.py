@@ -226,7 +226,7 @@ def test_s2k5_wgrad(cfg):
              "C": Co, "xform": L.XF_BN_BWD, "bn": bn_spec_train(GA, BE, ST, N * OH * OW)}
     nw = Co * wci * 25
     stride_ = nw + Co + 5
-    REP = torch.zeros(L.WREP * stride_, device=DEV)
+    REP = torch.zeros(L.WREP * stride_, dtype=torch.float64, device=DEV)
     dbias_p = ptr(REP[nw:]) if wci == Ci else 0  # the partial-weight entry takes no bias
     call("isg_conv_wgrad_rep", geom(**ge), vt([dyseg], N, OH, OW), vt([xseg], N, H, W),
          ptr(REP), dbias_p, stride_, L.WREP, stream())
@@ -320,10 +320,11 @@ def test_conv_wgrad_dense(cfg):
     xseg = {"p": ptr(X), "n_stride": Ci * H * W, "C": Ci, "xform": L.XF_BN_FWD,
             "act": L.ACT["relu"], "bn": bn_spec_eval(*G[:4])}
     dyseg = {"p": ptr(DY), "n_stride": Co * OH * OW, "C": Co, "xform": L.XF_PLAIN}
-    DW = torch.zeros(Co, Ci, k, k, device=DEV)
-    DB = torch.zeros(Co, device=DEV)
+    DW = torch.zeros(Co, Ci, k, k, dtype=torch.float64, device=DEV)  # fp64 accumulators (isg.h)
+    DB = torch.zeros(Co, dtype=torch.float64, device=DEV)
     call("isg_conv_wgrad", geom(**ge), vt([dyseg], N, OH, OW), vt([xseg], N, H, W), ptr(DW),
          ptr(DB), stream())
+    DW, DB = DW.float(), DB.float()
     close(DW, ref, what="wgrad")
     close(DB, dy.sum((0, 2, 3)), what="dbias")
 
@@ -364,7 +365,7 @@ def test_pw_wgrad_bn_bwd(cfg, xmode, pwk, monkeypatch):
         xseg["bn"] = bn_spec_train(XG[0], XG[1], XST, N * H * W)
     nw = Co * Ci
     stride_ = nw + Co + 19
-    REP = torch.zeros(L.WREP * stride_, device=DEV)
+    REP = torch.zeros(L.WREP * stride_, dtype=torch.float64, device=DEV)
     call("isg_conv_wgrad_rep", geom(**ge), vt([dyseg], N, H, W), vt([xseg], N, H, W),
          ptr(REP), ptr(REP[nw:]), stride_, L.WREP, stream())
     OUT = torch.full((stride_,), float("nan"), device=DEV)
@@ -395,7 +396,7 @@ def test_conv_wgrad_replicated(cfg):
     X, DY = cuda32(x), cuda32(dy)
     nw = int(np.prod(wshape))
     stride_ = nw + Co + 37  # replica stride: weight, bias, padding (as in the flat layout)
-    REP = torch.zeros(L.WREP * stride_, device=DEV)
+    REP = torch.zeros(L.WREP * stride_, dtype=torch.float64, device=DEV)
     call("isg_conv_wgrad_rep", geom(**ge),
          vt([{"p": ptr(DY), "n_stride": Co * OH * OW, "C": Co, "xform": L.XF_PLAIN}], N, OH, OW),
          vt([{"p": ptr(X), "n_stride": Ci * H * W, "C": Ci, "xform": L.XF_PLAIN}], N, H, W),
@@ -457,11 +458,12 @@ def test_depthwise(cfg):
     # wgrad
     wref = torch.nn.grad.conv2d_weight(xt, (C, 1, kh, kw), dy, padding=(ph, pw), dilation=d,
                                        groups=C)
-    DWt = torch.zeros(C, 1, kh, kw, device=DEV)
-    DB = torch.zeros(C, device=DEV)
+    DWt = torch.zeros(C, 1, kh, kw, dtype=torch.float64, device=DEV)  # fp64 accumulators
+    DB = torch.zeros(C, dtype=torch.float64, device=DEV)
     call("isg_conv_wgrad", geom(**ge),
          vt([{"p": ptr(DY), "n_stride": C * H * W, "C": C, "xform": L.XF_PLAIN}], N, H, W),
          vt([xseg], N, H, W), ptr(DWt), ptr(DB), stream())
+    DWt, DB = DWt.float(), DB.float()
     close(DWt, wref, what="dw wgrad")
     close(DB, dy.sum((0, 2, 3)), what="dw dbias")
 

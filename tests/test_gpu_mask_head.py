@@ -72,15 +72,15 @@ def test_mask_head_fwd_bwd(N, Hi, Wi):
     pre = torch.randn(N, 6, Hi, Wi, device=DEV)
     dxb = pre.clone()
     R, nrep = 4096 + 4 + 36 + 1, L.WREP
-    rep = torch.zeros(nrep * R, device=DEV)
+    rep = torch.zeros(nrep * R, dtype=torch.float64, device=DEV)  # fp64 replicas (isg.h)
     rp = rep.data_ptr()
     sk = [{"p": dxa.data_ptr(), "n_stride": 10 * Hi * Wi, "c0": 0, "C": 10, "mode": L.SINK_STORE},
           {"p": dxb.data_ptr(), "n_stride": 6 * Hi * Wi, "c0": 10, "C": 6, "mode": L.SINK_ACCUM}]
     b = struct(L.MaskHead, dict(base, dout=d["dl"].data_ptr(), dout_n_stride=OH * OW,
-                                dx={"s": sk, "nsink": 2}, dw1=rp, db1=rp + 4 * 4096,
-                                dw2=rp + 4 * 4100, db2=rp + 4 * 4136, rep_stride=R, nrep=nrep))
+                                dx={"s": sk, "nsink": 2}, dw1=rp, db1=rp + 8 * 4096,
+                                dw2=rp + 8 * 4100, db2=rp + 8 * 4136, rep_stride=R, nrep=nrep))
     call("isg_mask_head_bwd", b, L.stream_ptr())
-    tot = rep.view(nrep, R).sum(0).cpu()
+    tot = rep.view(nrep, R).sum(0).float().cpu()
     dx = torch.cat([dxa.cpu(), (dxb - pre).cpu()], 1)
     errs = {"dx": _rel(dx, ref_g[0]), "dw1": _rel(tot[:4096].view(16, 4, 8, 8), ref_g[1]),
             "db1": _rel(tot[4096:4100], ref_g[2]), "dw2": _rel(tot[4100:4136].view(1, 4, 3, 3), ref_g[3]),

@@ -133,6 +133,50 @@ def test_trainer_two_steps_match_reference(captured):
                                       fx.params[k].astype(np.float32), err_msg=k)
 
 
+@pytest.mark.parametrize("cfg", ["fixture_128", "bench_1024_keypoints"])
+def test_backward_is_bitwise_reproducible(cfg):
+    """SURVEY.md §5 determinism ("run twice, compare bits"): the captured train step, replayed
+    on the same inputs and parameters (lr 0), and a second Trainer built from scratch give
+    bit-identical logits, loss and flat gradient. Every cross-workgroup reduction of the
+    step adds fp32 workgroup partials into fp64 accumulators (BatchNorm statistics, PReLU
+    slopes and, since round 5, the weight-gradient replicas), which is exact whatever the
+    order the atomics land in (include/isg.h ISG_WREP); the round-4 fp32 replicas were not."""
+    from instancesegmentation_amd.data import device_batch
+
+    def trainer():
+        if cfg == "fixture_128":
+            fx = SegmentFixture("segment20_n2_128.npz")
+            tr = Trainer(_model(fx), fx.n, [(fx.n, 3, fx.h, fx.w), (fx.n, 17, fx.h, fx.w)],
+                         device=DEV)
+            xs, y = _inputs(fx.x), torch.from_numpy(fx.mask).to(DEV)
+        else:
+            torch.manual_seed(1234)
+            xs, y = device_batch(2, 1024, 1024, DEV, seed=100, cin=20, keypoints=True)
+            tr = Trainer(Segment(20), 2, [tuple(x.shape) for x in xs], device=DEV)
+        tr.capture()
+        sd = tr.optimizer_state_dict()
+        sd["param_groups"][0]["lr"] = 0.0  # parameters fixed: every replay has one answer
+        tr.load_optimizer_state_dict(sd)
+        return tr, xs, y
+
+    def run(tr, xs, y):
+        tr.step(xs, y)
+        torch.cuda.synchronize()
+        return (tr.logits.detach().clone(), tr.grad_flat.detach().clone(),
+                tr.loss_acc.detach().clone())
+
+    tr, xs, y = trainer()
+    first = run(tr, xs, y)
+    outs = [run(tr, xs, y) for _ in range(3)]
+    del tr
+    tr2, xs2, y2 = trainer()
+    outs.append(run(tr2, xs2, y2))
+    for i, o in enumerate(outs):
+        diff = [int((a != b).sum().item()) for a, b in zip(o, first)]
+        print(f"{cfg} run {i + 1}: elements differing from run 0 (logits, grads, loss): {diff}")
+        assert diff == [0, 0, 0], (cfg, i, diff)
+
+
 @pytest.mark.parametrize("cin,n,h,w", [(20, 2, 1024, 1024), (20, 2, 800, 1344),
                                        (20, 1, 1536, 2048)],
                          ids=["bench_bs2_1024", "coco_bs2_1344x800", "supervisely_bs1_2048x1536"])

@@ -68,8 +68,8 @@ int main(int argc, char** argv) {
     std::vector<double> hs(C4, 0.5);
     CK(hipMemcpy(stats, hs.data(), C4 * sizeof(double), hipMemcpyHostToDevice));
     const int64_t nw = (int64_t)Co * Ci * k * k;
-    float* dw;
-    CK(hipMalloc(&dw, ISG_WREP * nw * sizeof(float)));
+    double* dw;  // fp64 weight-gradient replicas (isg.h ISG_WREP)
+    CK(hipMalloc(&dw, ISG_WREP * nw * sizeof(double)));
     float* wt = dalloc(nw, 0.f, 4);
     float* out;
     CK(hipMalloc(&out, std::max(nx, ny) * sizeof(float)));
@@ -121,7 +121,8 @@ int main(int argc, char** argv) {
     }
     // mask head (isg_mask_head_*): x = Ci(16) x H x W plain, logits 4H x 4W
     isg_mask_head mh{};
-    float *hw1 = nullptr, *hw2 = nullptr, *hdl = nullptr, *hdx = nullptr, *hrep = nullptr;
+    float *hw1 = nullptr, *hw2 = nullptr, *hdl = nullptr, *hdx = nullptr;
+    double* hrep = nullptr;
     if (!strncmp(op, "head", 4)) {
         vx.s[0].xform = ISG_XF_PLAIN;
         mh.x = vx;
@@ -129,7 +130,7 @@ int main(int argc, char** argv) {
         hw2 = dalloc(36, 0.f, 8);
         hdl = dalloc((size_t)N * 16 * H * W, 0.f, 9);
         CK(hipMalloc(&hdx, (size_t)N * 16 * H * W * sizeof(float)));
-        CK(hipMalloc(&hrep, (size_t)ISG_WREP * 4200 * sizeof(float)));
+        CK(hipMalloc(&hrep, (size_t)ISG_WREP * 4200 * sizeof(double)));
         mh.w1 = hw1; mh.b1 = bet; mh.w2 = hw2; mh.b2 = bet;
         mh.out = out; mh.out_n_stride = (int64_t)16 * H * W;
         mh.dout = hdl; mh.dout_n_stride = (int64_t)16 * H * W;
