@@ -235,10 +235,32 @@ class Keypoints:
 
 
 # ---------------------------------------------------------------------------------
+def param_layout(owner):
+    """The flat parameter order of a Trainer (train.flatten_module): the module's
+    parameter order, except that the weight of the second conv of each sibling pair — two
+    1x1 Convs reading the same input, declared by a module's `siblings()` (BottleneckDim_Res
+    convs.0 + resconv, segment.py:198-202; BottleneckUp_Res convs.0 + conv2, :326-331) —
+    follows the first one's weight directly, so the pair's weights [W1; W2] (and their
+    gradients) are ONE contiguous [C1 + C2][Ci] matrix and the pair runs as one GEMM
+    (Graph.conv_pair)."""
+    names = {id(m): pre for pre, m in owner.named_modules()}
+    order = [k for k, _ in owner.named_parameters()]
+    for m in owner.modules():
+        sib = getattr(m, "siblings", None)
+        if not callable(sib):
+            continue
+        a, b = sib()
+        ka, kb = f"{names[id(a)]}.conv.weight", f"{names[id(b)]}.conv.weight"
+        if ka in order and kb in order:
+            order.remove(kb)
+            order.insert(order.index(ka) + 1, kb)
+    return order
+
+
 class Graph:
     """Forward trace of an engine module at one input shape."""
 
-    def __init__(self, owner, N, train, need_grad):
+    def __init__(self, owner, N, train, need_grad, layout=None):
         self.owner = owner
         self.N = N
         self.train = train
@@ -257,13 +279,19 @@ class Graph:
         self.tensor_names = [k for k, _ in owner.named_parameters()] + \
                             [k for k, _ in owner.named_buffers()]
         self.tslot = {k: S_TENSOR0 + i for i, k in enumerate(self.tensor_names)}
-        self.param_names = [k for k, _ in owner.named_parameters()]
+        self.params = dict(owner.named_parameters())
+        named = list(self.params)
+        # the flat gradient's order: the parameter order, or a Trainer's layout (param_layout)
+        self.param_names = list(layout) if layout is not None else named
+        if sorted(self.param_names) != sorted(named):
+            raise ValueError("parameter layout is not a permutation of the module's parameters")
+        self.layout_pos = {k: i for i, k in enumerate(self.param_names)}
         self.param_shapes = {k: tuple(p.shape) for k, p in owner.named_parameters()}
         off = 0
         self.pgrad_off = {}
-        for k, p in owner.named_parameters():
+        for k in self.param_names:
             self.pgrad_off[k] = off
-            off += p.numel()  # packed: the flat grad buffer in parameter order
+            off += self.params[k].numel()  # packed: the flat grad buffer in layout order
         self.pgrad_size = off
         self.used_params = set()
 
@@ -390,6 +418,48 @@ class Graph:
         op.kp = kp
         self.ops.append(op)
         return Value([Val(out, 0, conv.out_channels, bnr, act, slope, grad=self.need_grad)])
+
+    def conv_pair(self, ca, cb, x):
+        """Two sibling Conv modules (1x1 conv + BatchNorm + act, segment.py:34-45) on the same
+        input x as ONE stacked GEMM: weights [Wa; Wb] (contiguous in a Trainer's parameter
+        layout, param_layout), output channels [0, Ca) to a's buffer and [Ca, Ca + Cb) to
+        b's through two sinks (own bias and BatchNorm statistics); the backward is one
+        K-stacked input gradient (Wa^T ga + Wb^T gb, no ACCUM pass) and one weight gradient
+        over the stacked rows. Returns (value_a, value_b), or None when the pair does not
+        qualify (then the caller emits two convs): not 1x1 / stride 1 / dense, no BN, or the
+        weights not adjacent in the layout AND in memory (a module's own parameters are
+        separate tensors; ISG_NO_STACK=1 off)."""
+        if os.environ.get("ISG_NO_STACK", "0") == "1":
+            return None
+        a, b = ca.conv, cb.conv
+        for c in (a, b):
+            if not (c.kernel_size == (1, 1) and c.stride == (1, 1) and c.padding == (0, 0)
+                    and c.dilation == (1, 1) and c.groups == 1 and c.bias is not None):
+                return None
+        if a.in_channels != b.in_channels or a.in_channels != x.C:
+            return None
+        bna, bnb = getattr(ca, "bn", None), getattr(cb, "bn", None)
+        if bna is None or bnb is None:
+            return None
+        ka, kb = self.pname(a, "weight"), self.pname(b, "weight")
+        if self.layout_pos[kb] != self.layout_pos[ka] + 1:
+            return None
+        wa, wb = a.weight, b.weight
+        if (wa.device != wb.device or not wa.is_contiguous() or not wb.is_contiguous()
+                or wb.data_ptr() != wa.data_ptr() + wa.numel() * wa.element_size()):
+            return None
+        H, W = x.H, x.W
+        geom = dict(N=self.N, Ci=x.C, H=H, W=W, Co=a.out_channels + b.out_channels, OH=H, OW=W,
+                    KH=1, KW=1, SH=1, SW=1, PH=0, PW=0, DH=1, DW=1, groups=1)
+        outs, vals = [], []
+        for cm, c in ((ca, a), (cb, b)):
+            out = self.act_buf(c.out_channels, H, W, self.mod_names.get(id(cm), "conv"))
+            bnr = self.bn_ref(cm.bn, self.N * H * W)
+            kind, slope = self.act_of(cm.act)
+            outs.append((c, out, bnr))
+            vals.append(Value([Val(out, 0, c.out_channels, bnr, kind, slope, grad=self.need_grad)]))
+        self.ops.append(ConvPairOp(self, geom, x, outs))
+        return vals[0], vals[1]
 
     def conv_transpose(self, ct, x, bn=None, act="none", slope=None, name=""):
         k, s, p = ct.kernel_size, ct.stride, ct.padding
@@ -835,6 +905,77 @@ class ConvOp:
             gs.bias_from_bn.append((self.mod, self.bnr))
 
 
+class ConvPairOp:
+    """Two sibling 1x1 convs on one input as one stacked GEMM (Graph.conv_pair)."""
+
+    def __init__(self, g, geom, x, outs):
+        self.g, self.geom, self.x, self.outs = g, geom, x, outs  # outs: [(conv, buf, bnr)] x2
+        self.bnr = None
+        self.bnrs = [bnr for _, _, bnr in outs]
+        self.label = "+".join(buf.name for _, buf, _ in outs)
+
+    def _cost(self, co):
+        ge = self.geom
+        P = ge["N"] * ge["H"] * ge["W"]
+        return 2 * P * co * ge["Ci"], 4 * P * ge["Ci"], 4 * P * co, 4 * co * ge["Ci"]
+
+    def fwd(self, ops):
+        g = self.g
+        segs = [fwd_seg(v, g.train) for v in self.x.segs]
+        sinks, c0 = [], 0
+        for c, buf, bnr in self.outs:
+            sk = {"p": buf.ptr(), "n_stride": buf.n_stride, "c0": c0, "C": buf.C,
+                  "mode": L.SINK_STORE, "bias": g.tptr(c, "bias")}
+            if g.train:
+                sk["stats"] = Ptr(S_STATS, bnr.stats_off * 8)
+            sinks.append(sk)
+            c0 += buf.C
+        ge = self.geom
+        fl, xb, yb, wb = self._cost(ge["Co"])
+        ops.add(Record(L.OP_CONV_FWD, L.ConvRec,
+                       {"g": ge, "a": vtensor(segs, g.N, ge["H"], ge["W"]),
+                        "w": g.tptr(self.outs[0][0], "weight"), "out": sinks_spec(sinks)},
+                       label=self.label, flops=fl, nbytes=xb + yb + wb))
+
+    def bwd(self, ops, gs):
+        g = self.g
+        ge = self.geom
+        parts = [(c, buf, bnr, gs.dy_seg(buf, bnr, g.train)) for c, buf, bnr in self.outs]
+        live = [p for p in parts if p[3] is not None]
+        if not live:
+            return
+        for c, buf, bnr, _ in live:
+            gs.bias_from_bn.append((c, bnr))
+        if len(live) == 1:  # one branch reaches the loss: its own conv's weight rows
+            c, buf, bnr, dy = live[0]
+            segs, w, dwp = [dy], g.tptr(c, "weight"), g.wrep_ptr(c, "weight")
+            co = buf.C
+        else:
+            segs = [p[3] for p in parts]
+            w = g.tptr(self.outs[0][0], "weight")
+            dwp = g.wrep_ptr(self.outs[0][0], "weight")
+            g.wrep_ptr(self.outs[1][0], "weight")  # its rows follow (param_layout)
+            co = ge["Co"]
+        sg = dict(ge, Co=co)
+        fl, xb, yb, wb = self._cost(co)
+        dyb = 2 * yb  # g and the saved y of the BatchNorm backward
+        dyv = vtensor(segs, g.N, ge["H"], ge["W"])
+        label = "+".join(p[1].name for p in live)
+        if self.x.grad:
+            sinks, c = [], 0
+            for v in self.x.segs:
+                sinks.append(gs.sink_for(v, c, g.train))
+                c += v.C
+            ops.add(Record(L.OP_CONV_DGRAD, L.ConvRec,
+                           {"g": sg, "a": dyv, "w": w, "out": sinks_spec(sinks)},
+                           label="dx_" + label, flops=fl, nbytes=dyb + xb + wb))
+        xsegs = [fwd_seg(v, g.train) for v in self.x.segs]
+        ops.add(Record(L.OP_CONV_WGRAD, L.WgradRec,
+                       {"g": sg, "dy": dyv, "x": vtensor(xsegs, g.N, ge["H"], ge["W"]),
+                        "dw": dwp, "rep_stride": g.pgrad_size, "nrep": L.WREP},
+                       label="dw_" + label, flops=fl, nbytes=dyb + xb + wb))
+
+
 class HeadOp:
     """Fused mask head (Graph.head): one forward and one backward record."""
 
@@ -1011,7 +1152,7 @@ class TailOp:
 class Plan:
     """Compiled forward (+ optional backward) op lists of one module at one shape."""
 
-    def __init__(self, owner, in_shapes, train, need_grad, in_grad, buckets=2):
+    def __init__(self, owner, in_shapes, train, need_grad, in_grad, buckets=2, layout=None):
         """buckets: gradient buckets of the backward (2: the stem's parameters finalised in a
         second part after the others, for a data-parallel exchange that overlaps the stem
         backward; 1: one part, every finalisation at the end — at world size 1 nothing
@@ -1019,7 +1160,7 @@ class Plan:
         input-gradient chain wait ~0.6 ms for the queued weight gradients)."""
         self.n_buckets = buckets
         N = in_shapes[0][0]
-        g = Graph(owner, N, train, need_grad)
+        g = Graph(owner, N, train, need_grad, layout)
         ins = [g.input(i, s[1], s[2], s[3], in_grad[i]) if len(s) == 4 else
                g.keypoints(i, s[0], s[1]) for i, s in enumerate(in_shapes)]
         outs = owner.emit(g, *ins)
@@ -1047,8 +1188,9 @@ class Plan:
             i0 = len(fw.recs)
             op.fwd(fw)
             bnr = getattr(op, "bnr", None)
-            if train and bnr is not None and bnr.fin and not getattr(op, "fused_final", False):
-                fw.add(bn_final_record([bnr], False))
+            for b in getattr(op, "bnrs", [bnr]):
+                if train and b is not None and b.fin and not getattr(op, "fused_final", False):
+                    fw.add(bn_final_record([b], False))
             if getattr(op, "side", False):
                 rng = [_buf_range(op.out)]
                 if bnr is not None:

@@ -204,10 +204,19 @@ class BottleneckDim_Res(EngineModule):
         self.prelu = nn.PReLU(outplanes)
         self.relu = nn.ReLU(inplace=True)
 
+    def siblings(self):
+        """The two 1x1 Convs reading x (engine.param_layout / Graph.conv_pair)."""
+        return self.convs[0], self.resconv[0]
+
     def emit(self, g, x):
-        with g.side_branch():  # forward: overlaps the convs chain (engine._fork_branches)
-            r = self.resconv[0].emit(g, x)
-        y = _chain(g, self.convs, x)
+        pair = g.conv_pair(self.convs[0], self.resconv[0], x)  # one stacked GEMM
+        if pair is not None:
+            y0, r = pair
+            y = _chain(g, self.convs[1:], y0)
+        else:
+            with g.side_branch():  # forward: overlaps the convs chain (engine._fork_branches)
+                r = self.resconv[0].emit(g, x)
+            y = _chain(g, self.convs, x)
         kind, slope = g.act_of(self.prelu if self.usePrelu else self.relu)
         return g.tail([(y, False), (r, False)], kind, slope, name=g.mod_names[id(self)])
 
@@ -280,16 +289,26 @@ class BottleneckUp_Res(EngineModule):
             nn.Conv2d(outplanes * 2, outplanes, 1, 1, 0),
         )
 
+    def siblings(self):
+        """The two 1x1 Convs reading x (engine.param_layout / Graph.conv_pair)."""
+        return self.convs[0], self.conv2[0]
+
     def emit(self, g, x, mp_indices):
         name = g.mod_names[id(self)]
         up, c1 = self.uppool[0], self.uppool[1]
         if not (isinstance(up, nn.UpsamplingNearest2d) and up.scale_factor in (2, 2.0, (2, 2))
                 and c1.kernel_size == (1, 1)):
             raise NotImplementedError("uppool must be nearest x2 followed by a 1x1 conv")
-        with g.side_branch():  # forward: overlaps the convs chain (engine._fork_branches)
-            r = self.conv2[0].emit(g, x)
-            u = g.conv(c1, cat(r, mp_indices), name=name + ".uppool")
-        y = self.convs[0].emit(g, x)
+        pair = g.conv_pair(self.convs[0], self.conv2[0], x)  # one stacked GEMM
+        if pair is not None:
+            y, r = pair
+            with g.side_branch():  # forward: overlaps the convT chain
+                u = g.conv(c1, cat(r, mp_indices), name=name + ".uppool")
+        else:
+            with g.side_branch():  # forward: overlaps the convs chain (engine._fork_branches)
+                r = self.conv2[0].emit(g, x)
+                u = g.conv(c1, cat(r, mp_indices), name=name + ".uppool")
+            y = self.convs[0].emit(g, x)
         kind, slope = g.act_of(self.convs[3])
         bn = self.convs[2] if isinstance(self.convs[2], nn.BatchNorm2d) else None
         y = g.conv_transpose(self.convs[1], y, bn=bn, act=kind, slope=slope,

@@ -13,7 +13,7 @@ import torch.nn as nn
 
 from . import _lib as L
 from .engine import (S_ACT, S_DIN, S_DOUT, S_GRAD, S_IN, S_OUT, S_PGRAD, S_STATS, S_TENSOR0,
-                     S_WREP, Plan)
+                     S_WREP, Plan, param_layout)
 
 
 # ISG_DEBUG_POISON=1: fill every arena with NaN before use so a read of memory that no
@@ -143,7 +143,7 @@ class Runner:
             p.bwd.run(tab, L.stream_ptr(dev), L.side_stream_ptr(dev))
         g = p.graph
         pgrads = []
-        for k in g.param_names:
+        for k in g.params:  # autograd wants them in parameter order (not the layout's)
             if k in p.used_params:
                 off = g.pgrad_off[k]
                 n = 1
@@ -191,7 +191,10 @@ def run_module(mod, xs):
     key = (tuple(tuple(x.shape) for x in xs), train, need_grad or any(in_grad), in_grad)
     runner = mod._plans.get(key)
     if runner is None:
-        plan = Plan(mod, [tuple(x.shape) for x in xs], train, need_grad or any(in_grad), in_grad)
+        # sibling 1x1 convs run stacked where their weights are adjacent in memory
+        # (train.flatten_module with engine.param_layout); separate tensors: two convs
+        plan = Plan(mod, [tuple(x.shape) for x in xs], train, need_grad or any(in_grad), in_grad,
+                    layout=param_layout(mod))
         runner = Runner(mod, plan)
         mod._plans[key] = runner
     if need_grad or any(in_grad):

@@ -26,7 +26,7 @@ import torch.distributed as dist
 
 from . import _lib as L
 from .engine import (S_ACT, S_DOUT, S_GRAD, S_IN, S_OUT, S_PGRAD, S_STATS, S_TENSOR0, S_WREP,
-                     Plan)
+                     Plan, param_layout)
 
 
 class GradSync:
@@ -65,22 +65,30 @@ class GradSync:
         self._pending = []
 
 
-def flatten_module(model, device, flatb=None):
+def flatten_module(model, device, flatb=None, order=None):
     """Re-bind every parameter and floating buffer of `model` as a view of one flat
-    buffer (params) / (float buffers, into `flatb` when given: the Trainer passes the
-    tail of its exchange buffer); returns (flat_params, flat_bufs, param_index)."""
-    params = [p for _, p in model.named_parameters()]
-    n = sum(p.numel() for p in params)
+    buffer (params, laid out in `order` — parameter names, default the parameter order;
+    the Trainer passes engine.param_layout, which puts sibling 1x1 conv weights next to
+    each other) / (float buffers, into `flatb` when given: the Trainer passes the tail of its
+    exchange buffer); returns (flat_params, flat_bufs, param_index) with param_index[i] =
+    (offset, numel) of the i-th parameter in parameter order."""
+    named = dict(model.named_parameters())
+    order = list(order) if order is not None else list(named)
+    if sorted(order) != sorted(named):
+        raise ValueError("flatten_module: order is not a permutation of the parameters")
+    n = sum(p.numel() for p in named.values())
     flat = torch.empty(n, dtype=torch.float32, device=device)
-    index = []
+    where = {}
     off = 0
     with torch.no_grad():
-        for p in params:
-            k = p.numel()
-            flat[off:off + k].copy_(p.detach().reshape(-1))
-            p.data = flat[off:off + k].view_as(p)
-            index.append((off, k))
-            off += k
+        for k in order:
+            p = named[k]
+            c = p.numel()
+            flat[off:off + c].copy_(p.detach().reshape(-1))
+            p.data = flat[off:off + c].view_as(p)
+            where[k] = (off, c)
+            off += c
+    index = [where[k] for k in named]
     fbufs = [(m, name, b) for m in model.modules() for name, b in m._buffers.items()
              if b is not None and b.is_floating_point()]
     nb = sum(b.numel() for _, _, b in fbufs)
@@ -124,14 +132,18 @@ class Trainer:
         n = sum(p.numel() for p in self.model.parameters())
         nb = _float_buffer_count(self.model)
         self.comm = torch.zeros(n + max(nb, 1), dtype=torch.float32, device=dev)
-        self.flat, self.flatb, self.index = flatten_module(self.model, dev, self.comm[n:])
+        layout = param_layout(self.model)
+        self.flat, self.flatb, self.index = flatten_module(self.model, dev, self.comm[n:], layout)
         self.in_shapes = [tuple(s) for s in in_shapes]
         # two gradient buckets only where an exchange overlaps the stem backward (Plan)
         self.plan = Plan(self.model, self.in_shapes, True, True,
                          tuple(False for _ in self.in_shapes),
-                         buckets=int(os.environ.get("ISG_BUCKETS", "0")) or (2 if self.world > 1 else 1))
+                         buckets=int(os.environ.get("ISG_BUCKETS", "0")) or (2 if self.world > 1 else 1),
+                         layout=layout)
         g = self.plan.graph
         assert g.pgrad_size == n
+        for k, (off, _) in zip(g.params, self.index):  # the plan's gradient layout is the flat one
+            assert g.pgrad_off[k] == off, k
         self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
         self.act = torch.empty(max(self.plan.act_size, 1), dtype=torch.float32, device=dev)
         self.stats = torch.empty(self.plan.stats_size, dtype=torch.float64, device=dev)

@@ -38,7 +38,7 @@ BLOCKS = {
 SIZES = [(16, 24), (32, 32), (12, 20)]
 
 
-def run_block(name, hw, seed=0):
+def run_block(name, hw, seed=0, stacked=False):
     make, ofn, cin = BLOCKS[name][:3]
     cskip = BLOCKS[name][3] if len(BLOCKS[name]) > 3 else 0
     torch.manual_seed(seed)
@@ -48,6 +48,10 @@ def run_block(name, hw, seed=0):
     sd = blk.state_dict()
     blk.load_state_dict({k: torch.as_tensor(pv["blk." + k]).to(sd[k].dtype) for k in sd})
     blk = blk.to(DEV).train()
+    if stacked:  # the Trainer's flat layout: sibling 1x1 convs run as one stacked GEMM
+        from instancesegmentation_amd.engine import param_layout
+        from instancesegmentation_amd.train import flatten_module
+        flatten_module(blk, DEV, order=param_layout(blk))
     H, W = hw
     rng = np.random.Generator(np.random.PCG64(seed))
     x = rng.normal(0, 1, (2, cin, H, W)).astype(np.float32)
@@ -83,10 +87,19 @@ def err(a, b):
     return (a - b).abs().max().item() / max(b.abs().max().item(), 1e-6)
 
 
+STACKED = ["dimres_prelu", "dimres_relu", "up_res", "up_res_other"]  # blocks with siblings()
+
+
 @pytest.mark.parametrize("hw", SIZES)
-@pytest.mark.parametrize("name", list(BLOCKS))
+@pytest.mark.parametrize("name", list(BLOCKS) + [n + ":stacked" for n in STACKED])
 def test_block_parity(name, hw):
-    blk, outs, ins, ros, rins, P = run_block(name, hw)
+    stacked = name.endswith(":stacked")
+    name = name.split(":")[0]
+    blk, outs, ins, ros, rins, P = run_block(name, hw, stacked=stacked)
+    if stacked:
+        from instancesegmentation_amd.engine import ConvPairOp
+        plan = next(iter(blk._plans.values())).plan
+        assert sum(isinstance(op, ConvPairOp) for op in plan.graph.ops) == 1
     for o, r in zip(outs, ros):
         assert err(o, r) < 1e-5, f"output {err(o, r):.2e}"
     for i, (xt, xr) in enumerate(zip(ins, rins)):  # input (and skip) gradients
