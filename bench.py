@@ -8,7 +8,8 @@ parallel with an RCCL gradient all-reduce.
 
 Prints ONE JSON line (rank 0) with the driver's contract fields plus:
   roofline     — the dominant kernel (largest share of step time, picked by a per-op
-                 timing pass), timed live in the timed region with HIP events around it;
+                 timing pass), timed live in every timed step by two timestamp launches
+                 around it in its place in the step (minus a calibration pair's cost);
   cpu_baseline — the oracle's CPU restatement (fp32 torch eager) of the same train step,
                  timed on this host's cores (rank 0, N=1 only).
 """
@@ -36,6 +37,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--profile-ops", default="", help="write per-op timing table to this path")
+    ap.add_argument("--dominant", default="",
+                    help="phase:label of the roofline op (skips the per-op timing pass, so a "
+                         "profiler sees training steps only), e.g. bwd:d_out0")
     ap.add_argument("--eager", action="store_true", help="no HIP graph capture")
     ap.add_argument("--no-infer", action="store_true", help="skip the inference leg")
     ap.add_argument("--input", default="keypoints", choices=("keypoints", "heatmaps"),
@@ -43,6 +47,8 @@ def parse():
                          "synthesised inside the stem, SURVEY.md §8f #1) or dense heatmaps")
     ap.add_argument("--no-dense-leg", action="store_true",
                     help="skip the second timing with dense heatmap inputs")
+    ap.add_argument("--no-dp-leg", action="store_true",
+                    help="skip the timing of the data-parallel step structure at world size 1")
     return ap.parse_args()
 
 
@@ -279,10 +285,10 @@ def cpu_baseline(args):
                       f"bs{args.batch} {args.size}x{args.size} on {threads} host threads"}
 
 
-def train_leg(args, dev, world, rank, keypoints, roofline):
+def train_leg(args, dev, world, rank, keypoints, roofline, dp_plan=None):
     """Time args.steps captured train steps (after args.warmup) on one input form; the
-    dominant op (per-op timing pass) is bracketed by HIP events inside every timed step
-    when `roofline`."""
+    dominant op (per-op timing pass) is bracketed by timestamp launches inside every timed
+    step when `roofline`. dp_plan: the data-parallel step structure (Trainer dp_plan)."""
     from instancesegmentation_amd.data import device_batch
     from instancesegmentation_amd.model.segment import Segment
     from instancesegmentation_amd.train import Trainer
@@ -292,13 +298,17 @@ def train_leg(args, dev, world, rank, keypoints, roofline):
     xs, mask = device_batch(args.batch, args.size, args.size, dev, seed=100 + rank, cin=args.cin,
                             keypoints=keypoints and args.cin == 20)
     in_shapes = [tuple(x.shape) for x in xs]
-    trainer = Trainer(model, args.batch, in_shapes, device=dev)
+    trainer = Trainer(model, args.batch, in_shapes, device=dev, dp_plan=dp_plan)
     trainer.step(xs, mask)
     torch.cuda.synchronize()
 
     # ---- dominant op (per-op timing pass, untimed) ----------------------------------
     dom = None
-    if roofline:
+    if roofline and args.dominant:
+        ph, lab = args.dominant.split(":", 1)
+        ol = trainer.plan.fwd if ph == "fwd" else trainer.plan.bwd
+        dom = (ph, next(i for i, r in enumerate(ol.recs) if r.label == lab))
+    elif roofline:
         rows = op_timing(trainer)
         if args.profile_ops and rank == 0:
             with open(args.profile_ops, "w") as f:
@@ -311,19 +321,22 @@ def train_leg(args, dev, world, rank, keypoints, roofline):
         dom = (best["phase"], best["idx"])
     trainer.step()  # restore a consistent state after the per-op pass
     torch.cuda.synchronize()
-    # capture the step into HIP graphs; the dominant op gets its own graph so HIP events
-    # bracket it inside every timed step
+    # capture the step into ONE HIP graph (world 1); the dominant op runs between two
+    # timestamp launches (OP_STAMP: the 100 MHz chip counter) in its place in the step, plus
+    # a back-to-back calibration pair — ROCm rejects timing events under graph capture, and
+    # cutting the step into graphs around the op (the round-4 form) added a graph boundary
+    # and a side-stream join to what was timed
     dom_rec = None
     if dom is not None:
         ol = trainer.plan.fwd if dom[0] == "fwd" else trainer.plan.bwd
         dom_rec = ol.recs[dom[1]]
+        trainer.stamp_at = dom
     if not args.eager:
-        trainer.capture(split=dom)
+        trainer.capture()
     for _ in range(args.warmup):
         trainer.step()
     torch.cuda.synchronize()
-    trainer.events = []
-    ev_pairs = trainer.events
+    trainer.stamp_reset()
 
     if world > 1:
         dist.barrier()
@@ -340,12 +353,23 @@ def train_leg(args, dev, world, rank, keypoints, roofline):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
     roof = None
-    if ev_pairs and dom_rec is not None:
-        ms = sum(a.elapsed_time(b) for a, b in ev_pairs) / len(ev_pairs)
-        roof = roofline_of(dom_rec, ms)
-        roof["kernel"] = f"{dom[0]}:{dom_rec.label}"
-        roof["avg_ms"] = round(ms, 4)
-        roof["traffic"] = pmc_traffic(dom_rec.label, args)
+    if dom_rec is not None:
+        op, cal, span = trainer.stamp_times()
+        if op:
+            raw = sum(op) / len(op)  # stamp to stamp: the op + the launch boundaries around it
+            brk = sorted(cal)[len(cal) // 2]  # what the bracket alone costs
+            ms = max(raw - brk, 1e-6)
+            roof = roofline_of(dom_rec, ms)
+            roof["kernel"] = f"{dom[0]}:{dom_rec.label}"
+            roof["avg_ms"] = round(ms, 4)
+            roof["bracket_ms"] = round(raw, 4)
+            roof["bracket_overhead_ms"] = round(brk, 4)
+            roof["timed_launches"] = len(op)
+            # the counter against the host clock: first to last stamp of the timed steps over
+            # (K - 1)/K of the host-timed region (should read ~1.0)
+            k = len(op)
+            roof["stamp_clock_check"] = round(span / (elapsed * 1e3 * (k - 1) / k), 3) if k > 1 else None
+            roof["traffic"] = pmc_traffic(dom_rec.label, args)
     res = {"value": world * args.batch * args.steps / elapsed,
            "ms_per_step": 1e3 * elapsed / args.steps, "loss": trainer.loss(), "roofline": roof}
     del trainer
@@ -364,6 +388,9 @@ def main():
     dense_leg = None
     if kp and not args.no_dense_leg:
         dense_leg = train_leg(args, dev, world, rank, False, False)
+    dp_leg = None
+    if world == 1 and not args.no_dp_leg:
+        dp_leg = train_leg(args, dev, world, rank, kp, False, dp_plan=True)
 
     value = main_leg["value"]
     out = {
@@ -389,6 +416,12 @@ def main():
                                  "loss": round(dense_leg["loss"], 6),
                                  "input": "dense 17-channel heatmaps read from HBM "
                                           "(train_batch(x, heatmaps))"}
+    if dp_leg is not None:
+        out["dp_plan_at_world1"] = {
+            "value": round(dp_leg["value"], 3), "ms_per_step": round(dp_leg["ms_per_step"], 3),
+            "what": "the step as it runs at world > 1 (two backward parts, two gradient buckets, "
+                    "three HIP graphs with the RCCL exchange points between them), at world 1 "
+                    "where the exchanges are no-ops: the per-GPU ceiling of weak scaling"}
     if rank == 0 and world == 1 and not args.no_infer:
         out["infer"] = infer_bench(dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -308,6 +308,13 @@ int32_t isg_adam_dev(float* param, const float* grad, float* exp_avg, float* exp
 
 int32_t isg_fill_f64(double* p, int64_t n, double v, isg_stream_t stream);
 
+/* Timestamp of the chip-global 100 MHz counter (s_memrealtime) when this launch runs on
+ * the stream: written to buf[1 + i], i = the old value of the uint32 counter at buf[0]
+ * (incremented; dropped when i >= cap). A pair around one op of the executor's list (the
+ * OP_STAMP record) times that op where it runs in the step, inside one HIP graph
+ * (bench.py's roofline; ROCm rejects timing events recorded under graph capture). */
+int32_t isg_stamp(uint64_t* buf, int32_t cap, isg_stream_t stream);
+
 /* ---- infer post-process (build-defined; infer.py:32-36 is a stub) -------- */
 
 /* A13: paste K crop probability maps [K,S,S] back onto an HxW canvas through their

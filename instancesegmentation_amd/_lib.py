@@ -21,7 +21,7 @@ MAX_SEGS = 3
 LIST_CHUNK = 32
 STAT_REP = int(os.environ.get("ISG_STAT_REP", "4"))  # accumulator replicas (isg.h ISG_STAT_REP)
 ABI_VERSION = 9
-WREP = 16         # ISG_WREP: weight-gradient replicas (isg.h)
+WREP = int(os.environ.get("ISG_WREP", "16"))  # weight-gradient replicas (isg.h ISG_WREP)
 
 
 class Bn(Structure):
@@ -140,16 +140,22 @@ class MemsetRec(Structure):
     _fields_ = [("p", c_void_p), ("bytes", c_int64)]
 
 
+class StampRec(Structure):
+    _fields_ = [("buf", c_void_p), ("cap", c_int32), ("pad_", c_int32)]
+
+
 OP_CONV_FWD, OP_CONV_DGRAD, OP_CONV_WGRAD, OP_CONVT_FWD = 1, 2, 3, 4
 OP_MAXPOOL_FWD, OP_MAXPOOL_BWD, OP_TAIL_FWD, OP_TAIL_BWD = 5, 6, 7, 8
 OP_BN_UPDATE, OP_GRAD_FINAL, OP_BCE, OP_MEMSET = 9, 10, 11, 12
 OP_SUM_REP, OP_BN_FINAL = 13, 14
 OP_KP_STEM_FWD, OP_KP_STEM_WGRAD, OP_KP_POOL = 15, 16, 17
 OP_HEAD_FWD, OP_HEAD_BWD = 18, 19
+OP_STAMP = 20
 
 _RECORD_CHECK = [(0, VTensor), (1, Sinks), (2, ConvRec), (3, WgradRec), (4, PoolRec), (5, Tail),
                  (6, TailGrad), (7, BnUpdate), (8, GradFinal), (9, BceRec), (10, Geom), (11, Bn),
-                 (12, VSeg), (13, Sink), (14, SumRepRec), (15, KpStem), (16, MaskHead)]
+                 (12, VSeg), (13, Sink), (14, SumRepRec), (15, KpStem), (16, MaskHead),
+                 (17, StampRec)]
 
 # exported symbol -> (restype, argtypes)
 SIGNATURES = {
@@ -178,6 +184,7 @@ SIGNATURES = {
                                c_void_p, c_double, c_double, c_double, c_double, c_double,
                                c_void_p]),
     "isg_fill_f64": (c_int32, [c_void_p, c_int64, c_double, c_void_p]),
+    "isg_stamp": (c_int32, [c_void_p, c_int32, c_void_p]),
     "isg_mask_paste": (c_int32, [c_void_p, c_int32, c_int32, c_void_p, c_int32, c_int32, c_void_p,
                                  c_void_p]),
     "isg_mask_nms_workspace": (c_int64, [c_int32, c_int32, c_int32]),

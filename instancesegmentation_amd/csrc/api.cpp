@@ -161,6 +161,7 @@ enum {
     OP_KP_POOL = 17,
     OP_HEAD_FWD = 18,
     OP_HEAD_BWD = 19,
+    OP_STAMP = 20,
 };
 
 struct ConvRec {
@@ -213,6 +214,11 @@ struct BceRec {
 struct MemsetRec {
     void* p;
     int64_t bytes;
+};
+struct StampRec {  // OP_STAMP: isg_stamp(buf, cap)
+    uint64_t* buf;
+    int32_t cap;
+    int32_t pad_;
 };
 
 struct OpHdr {
@@ -374,6 +380,11 @@ static int32_t run_op_raw(int32_t kind, char* buf, isg_stream_t st) {
         case OP_HEAD_BWD:
             rc = isg_mask_head_bwd((const isg_mask_head*)buf, st);
             break;
+        case OP_STAMP: {
+            auto* r = (StampRec*)buf;
+            rc = isg_stamp(r->buf, r->cap, st);
+            break;
+        }
         case OP_MEMSET: {
             auto* r = (MemsetRec*)buf;
             if (hipMemsetAsync(r->p, 0, (size_t)r->bytes, st) != hipSuccess)
@@ -609,6 +620,7 @@ int32_t isg_record_size(int32_t which) {
         case 14: return (int32_t)sizeof(SumRepRec);
         case 15: return (int32_t)sizeof(isg_kp_stem);
         case 16: return (int32_t)sizeof(isg_mask_head);
+        case 17: return (int32_t)sizeof(StampRec);
         default: return -1;
     }
 }

@@ -769,6 +769,16 @@ __global__ void adam_dev_kernel(float* p, const float* g, float* m, float* v, co
 
 __global__ void step_inc_kernel(int32_t* c) { *c += 1; }
 
+// One timestamp of the chip-global 100 MHz counter into the next slot of buf (isg_stamp):
+// slot index from a vector atomic on buf[0], the value written with a vector store.
+__global__ void stamp_kernel(unsigned long long* buf, int cap) {
+    if (threadIdx.x != 0) return;
+    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+    const unsigned i = atomicAdd(reinterpret_cast<unsigned*>(buf), 1u);
+    volatile unsigned long long* const v = buf;
+    if ((int)i < cap) v[1 + i] = t;
+}
+
 __global__ void fill_f64_kernel(double* p, int64_t n, double v) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x)
@@ -964,6 +974,12 @@ int32_t isg_sum_replicas(float* dst, const double* src, int64_t n, int32_t nrep,
     hipLaunchKernelGGL(sum_rep_kernel, dim3((unsigned)blocks), dim3(kThreads), 0, st, dst, src, n,
                        nrep, stride);
     return isg_check_launch("sum_rep_kernel");
+}
+
+int32_t isg_stamp(uint64_t* buf, int32_t cap, isg_stream_t st) {
+    if (!buf || cap < 0) return isg_set_error(ISG_ERR_INVALID, "stamp: bad arguments");
+    hipLaunchKernelGGL(stamp_kernel, dim3(1), dim3(64), 0, st, (unsigned long long*)buf, cap);
+    return isg_check_launch("stamp_kernel");
 }
 
 int32_t isg_fill_f64(double* p, int64_t n, double v, isg_stream_t st) {

@@ -37,6 +37,7 @@ S_OUT = (8, 9)
 S_DOUT = (10, 11)
 S_DIN = (12, 13)
 S_WREP = 14  # L.WREP fp64 replicas of the flat parameter gradient (wgrad atomics, isg.h)
+S_STAMP = 15  # timestamp buffer of OP_STAMP records (isg_stamp: uint32 counter, then slots)
 S_TENSOR0 = 16
 
 ALIGN = 64  # elements (256 B) between arena buffers
@@ -138,6 +139,25 @@ class OpList:
         """A compiled sub-list recs[i:j] (to bracket one op with events)."""
         o = OpList()
         o.recs = self.recs[i:j]
+        return o.compile()
+
+    def stamped(self, idx, cap):
+        """A compiled copy with OP_STAMP records (isg_stamp into slot S_STAMP) on the main
+        stream: a calibration pair first (two stamps back to back: what a bracket costs
+        without an op), then one right before and one right after record `idx` — the op
+        timed where it runs in the step, side streams and all, without cutting the list."""
+        import copy
+
+        def stamp():
+            return Record(L.OP_STAMP, L.StampRec, {"buf": Ptr(S_STAMP), "cap": cap}, label="stamp")
+        op = copy.copy(self.recs[idx])
+        before = stamp()
+        # a join the op carries happens before its first stamp; a side-stream op (a weight
+        # gradient) is timed on the main stream
+        before.flags = op.flags & Record.OPF_JOIN
+        op.flags &= ~(Record.OPF_JOIN | Record.OPF_SIDE | Record.OPF_FORK_NOW)
+        o = OpList()
+        o.recs = [stamp(), stamp()] + self.recs[:idx] + [before, op, stamp()] + self.recs[idx + 1:]
         return o.compile()
 
 

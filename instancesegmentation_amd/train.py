@@ -25,8 +25,10 @@ import torch
 import torch.distributed as dist
 
 from . import _lib as L
-from .engine import (S_ACT, S_DOUT, S_GRAD, S_IN, S_OUT, S_PGRAD, S_STATS, S_TENSOR0, S_WREP,
-                     Plan, param_layout)
+from .engine import (S_ACT, S_DOUT, S_GRAD, S_IN, S_OUT, S_PGRAD, S_STAMP, S_STATS, S_TENSOR0,
+                     S_WREP, Plan, param_layout)
+
+STAMP_HZ = 100e6  # s_memrealtime: the chip-global 100 MHz counter (MI355X_MICROARCH.md)
 
 
 class GradSync:
@@ -123,12 +125,17 @@ class Trainer:
     on a CPU device (tests drive its exchange over gloo); `step()` needs the GPU."""
 
     def __init__(self, model, batch, in_shapes, device=None, lr=1e-3, betas=(0.9, 0.999),
-                 eps=1e-8, weight_decay=0.0, process_group=None):
+                 eps=1e-8, weight_decay=0.0, process_group=None, dp_plan=None):
+        """dp_plan: build the data-parallel step structure (two backward parts, two gradient
+        buckets, three HIP graphs with the exchange markers between them) even at world
+        size 1, where the exchanges are no-ops — what that structure costs on one GPU
+        (bench.py's dp_plan leg). Default: only at world size > 1."""
         self.device = torch.device(device or "cuda")
         dev = self.device
         self.model = model.to(dev).train()
         self.sync = GradSync(process_group)
         self.world, self.rank = self.sync.world, self.sync.rank
+        self.dp_plan = self.world > 1 if dp_plan is None else bool(dp_plan)
         n = sum(p.numel() for p in self.model.parameters())
         nb = _float_buffer_count(self.model)
         self.comm = torch.zeros(n + max(nb, 1), dtype=torch.float32, device=dev)
@@ -138,7 +145,7 @@ class Trainer:
         # two gradient buckets only where an exchange overlaps the stem backward (Plan)
         self.plan = Plan(self.model, self.in_shapes, True, True,
                          tuple(False for _ in self.in_shapes),
-                         buckets=int(os.environ.get("ISG_BUCKETS", "0")) or (2 if self.world > 1 else 1),
+                         buckets=int(os.environ.get("ISG_BUCKETS", "0")) or (2 if self.dp_plan else 1),
                          layout=layout)
         g = self.plan.graph
         assert g.pgrad_size == n
@@ -181,6 +188,9 @@ class Trainer:
         self._captured = (None, None)
         self.events = []
         self.split = None
+        self.stamp_at = None  # (phase, index): OP_STAMP records around that op (stamp_times)
+        self.stamp_buf = torch.zeros(1 + 4 * 4096, dtype=torch.int64, device=dev)
+        self.table[S_STAMP] = self.stamp_buf.data_ptr()
 
     def _make_table(self):
         g = self.plan.graph
@@ -240,15 +250,21 @@ class Trainer:
     def _schedule(self, split=None):
         """The step as a list of units: callables issuing HIP work, or the markers
         'coll1'/'coll2' (eager RCCL bucket exchange), 'tic'/'toc' (timing events around
-        one op). split=(phase, idx) isolates op `idx` of the forward/backward list."""
+        one op). split=(phase, idx) isolates op `idx` of the forward/backward list.
+        self.stamp_at=(phase, idx): that op's list runs with OP_STAMP records around the op
+        (OpList.stamped) — timed in place, the list (and the graph) not cut."""
         def run_list(ol):
             return lambda: ol.run(self.table, L.stream_ptr(self.device), L.side_stream_ptr(self.device),
                                   L.side_stream2_ptr(self.device))
-        dp = self.world > 1
+        dp = self.dp_plan
         lists = [("fwd", self.plan.fwd)] + [("bwd", p) for p in self.plan.bwd_parts]
         units = []
         base = 0  # index of the current backward part's first op in the whole backward
         for j, (phase, ol) in enumerate(lists):
+            if self.stamp_at and self.stamp_at[0] == phase:
+                k = self.stamp_at[1] - (base if phase == "bwd" else 0)
+                if 0 <= k < len(ol.recs):
+                    ol = ol.stamped(k, self.stamp_buf.numel() - 1)
             i = None
             if split and split[0] == phase:
                 i = split[1] - (base if phase == "bwd" else 0)
@@ -272,6 +288,19 @@ class Trainer:
             units.append("coll2")
         units.append(self._adam)
         return units
+
+    def stamp_reset(self):
+        self.stamp_buf.zero_()
+
+    def stamp_times(self):
+        """Per step since stamp_reset: (ms of the stamped op between its two stamps, ms of the
+        back-to-back calibration pair), from the 100 MHz counter."""
+        buf = self.stamp_buf.cpu()
+        n = min(int(buf[0].item()) & 0xFFFFFFFF, buf.numel() - 1)
+        v = buf[1:1 + n - n % 4].view(-1, 4).double()
+        op = ((v[:, 3] - v[:, 2]) / STAMP_HZ * 1e3).tolist()
+        cal = ((v[:, 1] - v[:, 0]) / STAMP_HZ * 1e3).tolist()
+        return op, cal, (v[-1, 3] - v[0, 0]).item() / STAMP_HZ * 1e3 if len(v) else 0.0
 
     def _state(self):
         return [self.comm, self.flat, self.exp_avg, self.exp_avg_sq, self.step_dev,
