@@ -354,22 +354,18 @@ def train_leg(args, dev, world, rank, keypoints, roofline, dp_plan=None):
         elapsed = t.item()
     roof = None
     if dom_rec is not None:
-        op, cal, span = trainer.stamp_times()
-        if op:
-            raw = sum(op) / len(op)  # stamp to stamp: the op + the launch boundaries around it
-            brk = sorted(cal)[len(cal) // 2]  # what the bracket alone costs
-            ms = max(raw - brk, 1e-6)
-            roof = roofline_of(dom_rec, ms)
-            roof["kernel"] = f"{dom[0]}:{dom_rec.label}"
-            roof["avg_ms"] = round(ms, 4)
-            roof["bracket_ms"] = round(raw, 4)
-            roof["bracket_overhead_ms"] = round(brk, 4)
-            roof["timed_launches"] = len(op)
-            # the counter against the host clock: first to last stamp of the timed steps over
-            # (K - 1)/K of the host-timed region (should read ~1.0)
-            k = len(op)
-            roof["stamp_clock_check"] = round(span / (elapsed * 1e3 * (k - 1) / k), 3) if k > 1 else None
-            roof["traffic"] = pmc_traffic(dom_rec.label, args)
+        raw, brk, span = trainer.stamp_times(args.steps)  # stamp to stamp; a bracket alone
+        ms = max(raw - brk, 1e-6)
+        roof = roofline_of(dom_rec, ms)
+        roof["kernel"] = f"{dom[0]}:{dom_rec.label}"
+        roof["avg_ms"] = round(ms, 4)
+        roof["bracket_ms"] = round(raw, 4)
+        roof["bracket_overhead_ms"] = round(brk, 4)
+        roof["timed_launches"] = args.steps
+        # the counter against the host clock: first to last stamp of the timed steps over the
+        # host-timed region (just under 1.0: the stamps sit inside the steps)
+        roof["stamp_clock_check"] = round(span / (elapsed * 1e3), 3)
+        roof["traffic"] = pmc_traffic(dom_rec.label, args)
     res = {"value": world * args.batch * args.steps / elapsed,
            "ms_per_step": 1e3 * elapsed / args.steps, "loss": trainer.loss(), "roofline": roof}
     del trainer

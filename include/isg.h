@@ -308,12 +308,13 @@ int32_t isg_adam_dev(float* param, const float* grad, float* exp_avg, float* exp
 
 int32_t isg_fill_f64(double* p, int64_t n, double v, isg_stream_t stream);
 
-/* Timestamp of the chip-global 100 MHz counter (s_memrealtime) when this launch runs on
- * the stream: written to buf[1 + i], i = the old value of the uint32 counter at buf[0]
- * (incremented; dropped when i >= cap). A pair around one op of the executor's list (the
- * OP_STAMP record) times that op where it runs in the step, inside one HIP graph
- * (bench.py's roofline; ROCm rejects timing events recorded under graph capture). */
-int32_t isg_stamp(uint64_t* buf, int32_t cap, isg_stream_t stream);
+/* Timestamp t of the chip-global 100 MHz counter (s_memrealtime) when this launch runs on
+ * the stream, accumulated into buf (uint64, two's complement): buf[slot] += sign < 0 ? -t : t
+ * (slot 0 or 1), buf[2] = max(buf[2], t), buf[3] = min(buf[3], t). A (-, +) pair around one
+ * op of the executor's list (the OP_STAMP record) sums that op's time where it runs in the
+ * step, over every replay of one HIP graph (bench.py's roofline; ROCm rejects timing events
+ * recorded under graph capture). */
+int32_t isg_stamp(uint64_t* buf, int32_t slot, int32_t sign, isg_stream_t stream);
 
 /* ---- infer post-process (build-defined; infer.py:32-36 is a stub) -------- */
 

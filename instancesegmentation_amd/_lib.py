@@ -141,7 +141,7 @@ class MemsetRec(Structure):
 
 
 class StampRec(Structure):
-    _fields_ = [("buf", c_void_p), ("cap", c_int32), ("pad_", c_int32)]
+    _fields_ = [("buf", c_void_p), ("slot", c_int32), ("sign", c_int32)]
 
 
 OP_CONV_FWD, OP_CONV_DGRAD, OP_CONV_WGRAD, OP_CONVT_FWD = 1, 2, 3, 4
@@ -184,7 +184,7 @@ SIGNATURES = {
                                c_void_p, c_double, c_double, c_double, c_double, c_double,
                                c_void_p]),
     "isg_fill_f64": (c_int32, [c_void_p, c_int64, c_double, c_void_p]),
-    "isg_stamp": (c_int32, [c_void_p, c_int32, c_void_p]),
+    "isg_stamp": (c_int32, [c_void_p, c_int32, c_int32, c_void_p]),
     "isg_mask_paste": (c_int32, [c_void_p, c_int32, c_int32, c_void_p, c_int32, c_int32, c_void_p,
                                  c_void_p]),
     "isg_mask_nms_workspace": (c_int64, [c_int32, c_int32, c_int32]),

@@ -215,10 +215,10 @@ struct MemsetRec {
     void* p;
     int64_t bytes;
 };
-struct StampRec {  // OP_STAMP: isg_stamp(buf, cap)
+struct StampRec {  // OP_STAMP: isg_stamp(buf, slot, sign)
     uint64_t* buf;
-    int32_t cap;
-    int32_t pad_;
+    int32_t slot;
+    int32_t sign;
 };
 
 struct OpHdr {
@@ -382,7 +382,7 @@ static int32_t run_op_raw(int32_t kind, char* buf, isg_stream_t st) {
             break;
         case OP_STAMP: {
             auto* r = (StampRec*)buf;
-            rc = isg_stamp(r->buf, r->cap, st);
+            rc = isg_stamp(r->buf, r->slot, r->sign, st);
             break;
         }
         case OP_MEMSET: {
@@ -433,6 +433,7 @@ int32_t isg_exec_ms2(const void* ops, int32_t nops, void* const* table, isg_stre
     std::vector<std::pair<int32_t, std::string>> pending;
     std::deque<Batch> ready;
     int pool_next = 0;
+    int deal = 0;  // weight gradients alternate between the side streams across batches too
     auto launch = [&](Batch& bt) -> int32_t {
         // a batch of weight gradients only (independent accumulations into the replica
         // buffers) is dealt over both side streams: their grids (128-512 workgroups) leave
@@ -454,8 +455,9 @@ int32_t isg_exec_ms2(const void* ops, int32_t nops, void* const* table, isg_stre
         forked = true;
         forked2 = forked2 || spread;
         alignas(16) char pb[8192];
-        int k = 0;
-        auto next_st = [&]() { return spread && (k++ & 1) ? side2 : side; };
+        // consecutive one-op batches (the stem's weight gradients, forked one by one behind
+        // its input-gradient chain) land on different side streams and overlap
+        auto next_st = [&]() { return spread && (deal++ & 1) ? side2 : side; };
         bool all_wgrad = true;
         for (auto& op : bt.ops) all_wgrad = all_wgrad && (op.first == OP_CONV_WGRAD || op.first == OP_KP_STEM_WGRAD);
         if (!pwg_group_on || !all_wgrad) {

@@ -925,6 +925,37 @@ __global__ __launch_bounds__(2 * kThreads, 1) void s2k5_fwd_kernel(S2fArgs a) {
     const int t0 = L * a.tpw, t1 = min(t0 + a.tpw, a.ntiles);
     const int Ho = a.OH, Wo = a.OW, Hi = 2 * Ho, Wi = 2 * Wo;
     STAMP(0);
+    constexpr int NE = 4 * G * kWgNR * kWgQ;
+    constexpr int UX = (NE + kThreads - 1) / kThreads;
+    f32x4 xv[UX];
+    int n = 0, oy0 = 0, ox0 = 0;  // producers: the tile held in xv
+    auto tile_of = [&](int t, int& tn, int& ty0, int& tx0) {
+        const int tpi = a.tiles_x * a.tiles_y;
+        tn = t / tpi;
+        const int r = t - tn * tpi, ty = r / a.tiles_x;
+        ty0 = ty * kWgRows;
+        tx0 = (r - ty * a.tiles_x) * kWgX;
+    };
+    // DIRECT: the channel address from the kernel arguments (the first tile, before the
+    // table in LDS exists), else from tabx
+    auto load = [&](int t, auto direct) {
+        tile_of(t, n, oy0, ox0);
+#pragma unroll
+        for (int u = 0; u < UX; ++u) {
+            const int e = min(ptid + u * kThreads, NE - 1);
+            const int c = e / (kWgNR * kWgQ), rq = e - c * (kWgNR * kWgQ);
+            const int rr = rq / kWgQ, q = rq - rr * kWgQ;
+            const int iy = 2 * oy0 - 2 + rr, ix = 2 * ox0 - 4 + 4 * q;
+            const bool ok = c < a.C && (unsigned)iy < (unsigned)Hi && ix >= 0 && ix < Wi;
+            const S2Ch t = decltype(direct)::value ? s2_ch_addr(a.x, min(c, a.C - 1), Hi * Wi) : tabx[c];
+            xv[u] = gld4(t.p + (int64_t)n * t.ns, ok ? (int64_t)iy * Wi + ix : 0);
+        }
+    };
+    // ONE round trip before the first barrier (each barrier waits for every load of the
+    // workgroup): the producers' first tile, the weights, the consumers' BatchNorm
+    // coefficients and sink rows are all in flight together (round 4 issued the tile after
+    // the weights had landed, and the coefficients after that)
+    if (producer && t0 < t1) load(t0, std::true_type{});
     if (tid < kMaxM) tabx[tid] = s2_ch_addr(a.x, min(tid, a.C - 1), Hi * Wi);
     {  // the weight into buffer 1 (first written by the producers after barrier B): every
        // load of the thread in flight at once (a rolled loop paid one round trip per element)
@@ -938,36 +969,13 @@ __global__ __launch_bounds__(2 * kThreads, 1) void s2k5_fwd_kernel(S2fArgs a) {
             const int mc = e / 25, t = e - mc * 25, m = mc / a.C, c = mc - m * a.C;
             wv[u] = gld(a.w, ((int64_t)m * a.wc + c) * 25 + t);
         }
+        if (tid < kMaxM) tabx[tid].k = s2_coef_x(a.x, min(tid, a.C - 1), Hi * Wi);
+        else if (tid >= 64 && tid < 64 + kMaxM) ri[tid - 64] = sink_row(a.out, tid - 64, (int64_t)Ho * Wo);
 #pragma unroll
         for (int u = 0; u < UW; ++u)
             if (tid + u * 2 * kThreads < nw) wl[tid + u * 2 * kThreads] = wv[u];
     }
-    __syncthreads();  // S0: channel addresses, weight copy
-
-    constexpr int NE = 4 * G * kWgNR * kWgQ;
-    constexpr int UX = (NE + kThreads - 1) / kThreads;
-    f32x4 xv[UX];
-    int n = 0, oy0 = 0, ox0 = 0;  // producers: the tile held in xv
-    auto tile_of = [&](int t, int& tn, int& ty0, int& tx0) {
-        const int tpi = a.tiles_x * a.tiles_y;
-        tn = t / tpi;
-        const int r = t - tn * tpi, ty = r / a.tiles_x;
-        ty0 = ty * kWgRows;
-        tx0 = (r - ty * a.tiles_x) * kWgX;
-    };
-    auto load = [&](int t) {
-        tile_of(t, n, oy0, ox0);
-#pragma unroll
-        for (int u = 0; u < UX; ++u) {
-            const int e = min(ptid + u * kThreads, NE - 1);
-            const int c = e / (kWgNR * kWgQ), rq = e - c * (kWgNR * kWgQ);
-            const int rr = rq / kWgQ, q = rq - rr * kWgQ;
-            const int iy = 2 * oy0 - 2 + rr, ix = 2 * ox0 - 4 + 4 * q;
-            const bool ok = c < a.C && (unsigned)iy < (unsigned)Hi && ix >= 0 && ix < Wi;
-            const S2Ch& t = tabx[c];
-            xv[u] = gld4(t.p + (int64_t)n * t.ns, ok ? (int64_t)iy * Wi + ix : 0);
-        }
-    };
+    __syncthreads();  // S0: channel table, coefficients, sink rows, weight copy, tile t0 loaded
     auto store = [&](int buf) {
         float* const Xs = s2f_lds + buf * BAND;
 #pragma unroll
@@ -992,22 +1000,18 @@ __global__ __launch_bounds__(2 * kThreads, 1) void s2k5_fwd_kernel(S2fArgs a) {
     };
 
     if (producer) {
-        if (t0 < t1) load(t0);
-        __syncthreads();  // A: coefficients, sink rows, weight fragments read
         if (t0 < t1) store(0);
-        if (t0 + 1 < t1) load(t0 + 1);
-        __syncthreads();  // B: tile t0 staged
+        if (t0 + 1 < t1) load(t0 + 1, std::false_type{});
+        __syncthreads();  // B: tile t0 staged (the consumers read the weights before it)
         for (int t = t0; t < t1; ++t) {
             if (t + 1 < t1) {
                 store(((t - t0) & 1) ^ 1);  // registers hold tile t + 1
-                if (t + 2 < t1) load(t + 2);
+                if (t + 2 < t1) load(t + 2, std::false_type{});
             }
             __syncthreads();
         }
         __syncthreads();  // E
     } else {
-        if (tid < kMaxM) tabx[tid].k = s2_coef_x(a.x, min(tid, a.C - 1), Hi * Wi);
-        else if (tid >= 64 && tid < 64 + kMaxM) ri[tid - 64] = sink_row(a.out, tid - 64, (int64_t)Ho * Wo);
         float wa[G][25];
         {
             const float* wl = s2f_lds + BAND;
@@ -1031,7 +1035,6 @@ __global__ __launch_bounds__(2 * kThreads, 1) void s2k5_fwd_kernel(S2fArgs a) {
             const int m = min(4 * kq + i, a.M - 1);
             bias[i] = a.st16 && a.out.s[0].bias ? a.out.s[0].bias[m] : 0.f;
         }
-        __syncthreads();  // A
         __syncthreads();  // B
         STAMP(1);
         for (int t = t0; t < t1; ++t) {

@@ -769,14 +769,15 @@ __global__ void adam_dev_kernel(float* p, const float* g, float* m, float* v, co
 
 __global__ void step_inc_kernel(int32_t* c) { *c += 1; }
 
-// One timestamp of the chip-global 100 MHz counter into the next slot of buf (isg_stamp):
-// slot index from a vector atomic on buf[0], the value written with a vector store.
-__global__ void stamp_kernel(unsigned long long* buf, int cap) {
+// One timestamp of the chip-global 100 MHz counter, accumulated (isg_stamp): sign * t added
+// to buf[slot] and t folded into the max (buf[2]) / min (buf[3]) — vector atomics whose
+// results are not waited for, so the launch is as short as a launch gets.
+__global__ void stamp_kernel(unsigned long long* buf, int slot, int sign) {
     if (threadIdx.x != 0) return;
     const unsigned long long t = __builtin_amdgcn_s_memrealtime();
-    const unsigned i = atomicAdd(reinterpret_cast<unsigned*>(buf), 1u);
-    volatile unsigned long long* const v = buf;
-    if ((int)i < cap) v[1 + i] = t;
+    atomicAdd(buf + slot, sign < 0 ? 0ull - t : t);
+    atomicMax(buf + 2, t);
+    atomicMin(buf + 3, t);
 }
 
 __global__ void fill_f64_kernel(double* p, int64_t n, double v) {
@@ -976,9 +977,9 @@ int32_t isg_sum_replicas(float* dst, const double* src, int64_t n, int32_t nrep,
     return isg_check_launch("sum_rep_kernel");
 }
 
-int32_t isg_stamp(uint64_t* buf, int32_t cap, isg_stream_t st) {
-    if (!buf || cap < 0) return isg_set_error(ISG_ERR_INVALID, "stamp: bad arguments");
-    hipLaunchKernelGGL(stamp_kernel, dim3(1), dim3(64), 0, st, (unsigned long long*)buf, cap);
+int32_t isg_stamp(uint64_t* buf, int32_t slot, int32_t sign, isg_stream_t st) {
+    if (!buf || slot < 0 || slot > 1) return isg_set_error(ISG_ERR_INVALID, "stamp: bad arguments");
+    hipLaunchKernelGGL(stamp_kernel, dim3(1), dim3(64), 0, st, (unsigned long long*)buf, slot, sign);
     return isg_check_launch("stamp_kernel");
 }
 

@@ -141,23 +141,26 @@ class OpList:
         o.recs = self.recs[i:j]
         return o.compile()
 
-    def stamped(self, idx, cap):
+    def stamped(self, idx):
         """A compiled copy with OP_STAMP records (isg_stamp into slot S_STAMP) on the main
-        stream: a calibration pair first (two stamps back to back: what a bracket costs
-        without an op), then one right before and one right after record `idx` — the op
-        timed where it runs in the step, side streams and all, without cutting the list."""
+        stream: a calibration pair first (two stamps back to back, slot 1: what a bracket
+        costs without an op), then one right before and one right after record `idx` (slot
+        0) — the op timed where it runs in the step, side streams and all, without cutting
+        the list."""
         import copy
 
-        def stamp():
-            return Record(L.OP_STAMP, L.StampRec, {"buf": Ptr(S_STAMP), "cap": cap}, label="stamp")
+        def stamp(slot, sign):
+            return Record(L.OP_STAMP, L.StampRec, {"buf": Ptr(S_STAMP), "slot": slot,
+                                                   "sign": sign}, label="stamp")
         op = copy.copy(self.recs[idx])
-        before = stamp()
+        before = stamp(0, -1)
         # a join the op carries happens before its first stamp; a side-stream op (a weight
         # gradient) is timed on the main stream
         before.flags = op.flags & Record.OPF_JOIN
         op.flags &= ~(Record.OPF_JOIN | Record.OPF_SIDE | Record.OPF_FORK_NOW)
         o = OpList()
-        o.recs = [stamp(), stamp()] + self.recs[:idx] + [before, op, stamp()] + self.recs[idx + 1:]
+        o.recs = [stamp(1, -1), stamp(1, 1)] + self.recs[:idx] + [before, op, stamp(0, 1)] + \
+            self.recs[idx + 1:]
         return o.compile()
 
 
@@ -1199,6 +1202,12 @@ class Plan:
                 self._emit_output(g, o, ob)
             self.out_bufs.append(ob)
         self.out_shapes = [(N, b.C, b.H, b.W) for b in self.out_bufs]
+        # a training step's loss accumulator (one double): in the statistics arena, so the
+        # forward's memset zeroes it (no separate fill launch before the loss kernel)
+        self.loss_off = None
+        if train and need_grad:
+            self.loss_off = g.stats_size
+            g.stats_size += 8
         # ---- forward list
         fw = OpList()
         if g.stats_size:

@@ -166,7 +166,8 @@ class Trainer:
         # BCELoss mean over this replica's pixels, pre-divided by the world size so the
         # exchange's SUM is the replica mean (GradSync)
         self.grad_scale = 1.0 / (self.logits.numel() * self.world)
-        self.loss_acc = torch.zeros(1, dtype=torch.float64, device=dev)
+        # zeroed by the forward's statistics memset (Plan.loss_off)
+        self.loss_acc = self.stats[self.plan.loss_off:self.plan.loss_off + 1]
         self._pg_views = []
         for (k, p), (off, cnt) in zip(self.model.named_parameters(), self.index):
             self._pg_views.append((g.pgrad_off[k], off, cnt, k in self.plan.used_params))
@@ -189,7 +190,7 @@ class Trainer:
         self.events = []
         self.split = None
         self.stamp_at = None  # (phase, index): OP_STAMP records around that op (stamp_times)
-        self.stamp_buf = torch.zeros(1 + 4 * 4096, dtype=torch.int64, device=dev)
+        self.stamp_buf = torch.zeros(4, dtype=torch.int64, device=dev)  # isg_stamp's sums / max / min
         self.table[S_STAMP] = self.stamp_buf.data_ptr()
 
     def _make_table(self):
@@ -227,7 +228,6 @@ class Trainer:
         lib = L.lib()
         st = L.stream_ptr(self.device)
         n = self.logits.numel()
-        L.check(lib.isg_fill_f64(self.loss_acc.data_ptr(), 1, 0.0, st), "fill")
         L.check(lib.isg_bce_sigmoid(self.logits.data_ptr(), self.target.data_ptr(), n,
                                     self.loss_acc.data_ptr(), self.dlogits.data_ptr(),
                                     self.grad_scale, st), "bce")
@@ -264,7 +264,7 @@ class Trainer:
             if self.stamp_at and self.stamp_at[0] == phase:
                 k = self.stamp_at[1] - (base if phase == "bwd" else 0)
                 if 0 <= k < len(ol.recs):
-                    ol = ol.stamped(k, self.stamp_buf.numel() - 1)
+                    ol = ol.stamped(k)
             i = None
             if split and split[0] == phase:
                 i = split[1] - (base if phase == "bwd" else 0)
@@ -290,17 +290,15 @@ class Trainer:
         return units
 
     def stamp_reset(self):
-        self.stamp_buf.zero_()
+        self.stamp_buf.copy_(torch.tensor([0, 0, 0, 2 ** 63 - 1], dtype=torch.int64))
 
-    def stamp_times(self):
-        """Per step since stamp_reset: (ms of the stamped op between its two stamps, ms of the
-        back-to-back calibration pair), from the 100 MHz counter."""
-        buf = self.stamp_buf.cpu()
-        n = min(int(buf[0].item()) & 0xFFFFFFFF, buf.numel() - 1)
-        v = buf[1:1 + n - n % 4].view(-1, 4).double()
-        op = ((v[:, 3] - v[:, 2]) / STAMP_HZ * 1e3).tolist()
-        cal = ((v[:, 1] - v[:, 0]) / STAMP_HZ * 1e3).tolist()
-        return op, cal, (v[-1, 3] - v[0, 0]).item() / STAMP_HZ * 1e3 if len(v) else 0.0
+    def stamp_times(self, steps):
+        """Since stamp_reset, over `steps` replays: (mean ms of the stamped op between its two
+        stamps, mean ms of the back-to-back calibration pair, ms from the first to the last
+        stamp), from the 100 MHz counter."""
+        b = self.stamp_buf.cpu().tolist()
+        ms = 1e3 / STAMP_HZ
+        return b[0] * ms / steps, b[1] * ms / steps, (b[2] - b[3]) * ms
 
     def _state(self):
         return [self.comm, self.flat, self.exp_avg, self.exp_avg_sq, self.step_dev,
