@@ -431,24 +431,109 @@ constexpr int kSubPL = 432;                // channel plane (>= (kRowsPB + 2) * 
 static_assert(kSubPL >= (kRowsPB + 2) * kSubRS && kSubPL % 32 == 16, "staging plane");
 
 
+// Round 5: ONE memory round trip before the MFMAs — the band's interior quads and halo
+// columns (addresses straight from the kernel argument for a one-segment dy, the stem's
+// case), the weight, the coefficient and sink-row tables are all issued before the first
+// barrier (round 4: table + weight, then the band, then the halo columns, three trips) —
+// and each dy row's sink operands (the saved forward output of the ACTBWD sink) are loaded
+// before that row's MFMAs, not between them and the stores.
+ISG_DEV void sink_row_apply2_pre(const SinkRow& q, int n, int64_t pix, float v0, float v1,
+                                 v2f_t pre, float& s0, float& s1, float& s2) {
+    const int64_t off = (int64_t)n * q.ns + pix;
+    if (q.mode == ISG_SINK_STORE) {
+        v0 += q.bias;
+        v1 += q.bias;
+        *(gv2_p)((gfloat_p)q.p + off) = v2f_t{v0, v1};
+        s0 = v0 + v1;
+        s1 = v0 * v0 + v1 * v1;
+    } else if (q.mode == ISG_SINK_ACCUM) {
+        *(gv2_p)((gfloat_p)q.p + off) = v2f_t{pre[0] + v0, pre[1] + v1};
+        s0 = v0 + v1;
+        s1 = v0 * v0 + v1 * v1;
+    } else if (q.mode == ISG_SINK_ACTBWD) {
+        float g[2];
+        const float v[2] = {v0, v1};
+        s0 = s1 = s2 = 0.f;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const float z = (pre[e] - q.f.mean) * q.f.scale + q.f.beta;
+            float gv = v[e];
+            if (q.act == ISG_ACT_RELU) {
+                gv = z > 0.f ? v[e] : 0.f;
+            } else if (q.act == ISG_ACT_PRELU) {
+                gv = z > 0.f ? v[e] : v[e] * q.f.slope;
+                s2 += z > 0.f ? 0.f : z * v[e];
+            }
+            g[e] = gv;
+            s0 += gv;
+            s1 += gv * (pre[e] - q.f.mean);
+        }
+        *(gv2_p)((gfloat_p)q.p + off) = v2f_t{g[0], g[1]};
+    }
+}
+
 __global__ __launch_bounds__(kThreads) void sub2_dgrad_lds_kernel(DownArgs a) {
     constexpr int K = 5, P = 2, R0 = 1;
     __shared__ float wl[kMaxM * kMaxM * K * K];  // [c][m][kh][kw] (the weight's own layout)
     __shared__ __attribute__((aligned(16))) float Ls[kMaxM * kSubPL];  // [c][row][col] dy band
-    __shared__ ChT tab[kMaxM];
     __shared__ XfLin lin[kMaxM];
     __shared__ SinkRow ri[kMaxM];
     __shared__ float red[4][3][kMaxM];
     const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
     const int kq = lane >> 4, pl = lane & 15;
     const int Hs = a.H, Ws = a.W, Wd = 2 * Ws;
+    const int64_t HWs = (int64_t)Hs * Ws;
     const int n = blockIdx.z, j0 = blockIdx.x * 64, i0 = blockIdx.y * kRowsPB;
-    if (tid < a.C) {
-        const ChT t = ch_table_entry(a.dy, tid, (int64_t)Hs * Ws);
-        tab[tid] = t;
-        lin[tid] = xf_lin(t.xf, t.act, t.k);
+    STAMP(0);
+    // ---- every load of the prologue in one round trip ------------------------------------
+    constexpr int NQ = kMaxM * (kRowsPB + 2) * 16;  // (c, row, quad) interior quads
+    constexpr int U = NQ / kThreads;
+    static_assert(NQ % kThreads == 0, "staging split");
+    constexpr int NH = kMaxM * (kRowsPB + 2) * 2;   // (c, row, side) halo columns
+    static_assert(NH <= kThreads, "one halo element per thread");
+    const bool seg1 = a.dy.nseg == 1;
+    auto chan = [&](int c, const float*& p, const float*& y, int64_t& ns, int64_t& yns) {
+        if (seg1) {
+            const isg_vseg& sg = a.dy.s[0];
+            p = sg.p + (int64_t)c * HWs;
+            y = (sg.xform == ISG_XF_BN_BWD && sg.y) ? sg.y + (int64_t)c * HWs : p;
+            ns = sg.n_stride;
+            yns = (sg.xform == ISG_XF_BN_BWD && sg.y) ? sg.y_n_stride : sg.n_stride;
+        } else {
+            const ChSrc t = ch_src(vt_lite(a.dy), c, (int)HWs);
+            p = t.p; y = t.y; ns = t.ns; yns = t.yns;
+        }
+    };
+    f32x4 xv[U], yv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int e = tid + u * kThreads;
+        const int c = e / ((kRowsPB + 2) * 16), rq = e - c * (kRowsPB + 2) * 16;
+        const int rr = rq >> 4, q = rq & 15;
+        const int yy = i0 - 1 + rr, xx = j0 + 4 * q;
+        const bool ok = c < a.C && (unsigned)yy < (unsigned)Hs && xx < Ws;
+        const float *p, *y;
+        int64_t ns, yns;
+        chan(c < a.C ? c : 0, p, y, ns, yns);
+        const int64_t o = ok ? (int64_t)yy * Ws + xx : 0;
+        xv[u] = gld4(p + (int64_t)n * ns, o);
+        yv[u] = gld4(y + (int64_t)n * yns, o);  // == p unless BN_BWD (an L1 hit)
     }
-    if (tid < a.M) ri[tid] = sink_row(a.out, tid, (int64_t)2 * Hs * Wd);
+    float hx, hy;
+    bool hok;
+    {
+        const int e = min(tid, NH - 1);
+        const int c = e / ((kRowsPB + 2) * 2), rs = e - c * (kRowsPB + 2) * 2;
+        const int rr = rs >> 1, side = rs & 1;
+        const int yy = i0 - 1 + rr, xx = side ? j0 + 64 : j0 - 1;
+        hok = tid < NH && c < a.C && (unsigned)yy < (unsigned)Hs && (unsigned)xx < (unsigned)Ws;
+        const float *p, *y;
+        int64_t ns, yns;
+        chan(c < a.C ? c : 0, p, y, ns, yns);
+        const int64_t o = hok ? (int64_t)yy * Ws + xx : 0;
+        hx = gld(p + (int64_t)n * ns, o);
+        hy = gld(y + (int64_t)n * yns, o);
+    }
     {   // the weight: every load of the thread issued before the first store (a rolled loop
         // of predicated loads paid one L2 round trip per element: 25 in a row)
         constexpr int NW = kMaxM * kMaxM * K * K, UW = NW / kThreads;
@@ -464,85 +549,102 @@ __global__ __launch_bounds__(kThreads) void sub2_dgrad_lds_kernel(DownArgs a) {
             wv[u] = gld(a.w, (c < a.C && m < a.M) ? src : 0);
             wv[u] = (c < a.C && m < a.M && src < nw) ? wv[u] : 0.f;
         }
+        if (tid < a.C) {
+            const ChT t = ch_table_entry(a.dy, tid, HWs);
+            lin[tid] = xf_lin(t.xf, t.act, t.k);
+        }
+        if (tid < a.M) ri[tid] = sink_row(a.out, tid, (int64_t)2 * Hs * Wd);
 #pragma unroll
         for (int u = 0; u < UW; ++u) wl[tid + u * kThreads] = wv[u];
     }
     __syncthreads();
-    // ---- stage the band: interior quads (16-B loads), then the two halo columns
-    {
-        constexpr int NQ = kMaxM * (kRowsPB + 2) * 16;  // (c, row, quad)
-        constexpr int U = NQ / kThreads;
-        static_assert(NQ % kThreads == 0, "staging split");
-        f32x4 xv[U], yv[U];
-        int meta[U];
+    STAMP(1);
+    // ---- the band, transformed once per element, into LDS -----------------------------------
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int e = tid + u * kThreads;
-            const int c = e / ((kRowsPB + 2) * 16), rq = e - c * (kRowsPB + 2) * 16;
-            const int rr = rq >> 4, q = rq & 15;
-            const int yy = i0 - 1 + rr, xx = j0 + 4 * q;
-            const bool ok = c < a.C && (unsigned)yy < (unsigned)Hs && xx < Ws;
-            meta[u] = ok ? e : -1 - e;
-            const ChT t = tab[c < a.C ? c : 0];
-            const int64_t o = ok ? (int64_t)yy * Ws + xx : 0;
-            xv[u] = gld4(t.p + (int64_t)n * t.ns, o);
-            yv[u] = gld4(t.y + (int64_t)n * t.yns, o);  // == p unless BN_BWD (an L1 hit)
-        }
+    for (int u = 0; u < U; ++u) {
+        const int e = tid + u * kThreads;
+        const int c = e / ((kRowsPB + 2) * 16), rq = e - c * (kRowsPB + 2) * 16;
+        const int rr = rq >> 4, q = rq & 15;
+        const int yy = i0 - 1 + rr, xx = j0 + 4 * q;
+        const bool ok = c < a.C && (unsigned)yy < (unsigned)Hs && xx < Ws;
+        float* d = Ls + c * kSubPL + rr * kSubRS + 4 + 4 * q;
+        const XfLin l = lin[c < a.C ? c : 0];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const bool ok = meta[u] >= 0;
-            const int e = ok ? meta[u] : -1 - meta[u];
-            const int c = e / ((kRowsPB + 2) * 16), rq = e - c * (kRowsPB + 2) * 16;
-            const int rr = rq >> 4, q = rq & 15;
-            float* d = Ls + c * kSubPL + rr * kSubRS + 4 + 4 * q;
-            const XfLin l = lin[c < a.C ? c : 0];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) d[k] = ok ? xf_lin_apply(l, xv[u][k], yv[u][k]) : 0.f;
-        }
-        for (int e = tid; e < kMaxM * (kRowsPB + 2) * 2; e += kThreads) {
-            const int c = e / ((kRowsPB + 2) * 2), rs = e - c * (kRowsPB + 2) * 2;
-            const int rr = rs >> 1, side = rs & 1;
-            const int yy = i0 - 1 + rr, xx = side ? j0 + 64 : j0 - 1;
-            float v = 0.f;
-            if (c < a.C && (unsigned)yy < (unsigned)Hs && (unsigned)xx < (unsigned)Ws) {
-                const ChT t = tab[c];
-                const int64_t o = (int64_t)yy * Ws + xx;
-                const float x = gld(t.p + (int64_t)n * t.ns, o);
-                const float y = t.xf == ISG_XF_BN_BWD ? gld(t.y + (int64_t)n * t.yns, o) : x;
-                v = ch_xform(t.xf, t.act, t.k, x, y);
-            }
-            Ls[c * kSubPL + rr * kSubRS + (side ? 68 : 3)] = v;
-        }
+        for (int k = 0; k < 4; ++k) d[k] = ok ? xf_lin_apply(l, xv[u][k], yv[u][k]) : 0.f;
+    }
+    if (tid < NH) {
+        const int c = tid / ((kRowsPB + 2) * 2), rs = tid - c * (kRowsPB + 2) * 2;
+        const int rr = rs >> 1, side = rs & 1;
+        const XfLin l = lin[c < a.C ? c : 0];
+        Ls[c * kSubPL + rr * kSubRS + (side ? 68 : 3)] = hok ? xf_lin_apply(l, hx, hy) : 0.f;
     }
     __syncthreads();
+    STAMP(2);
+    float wreg[kMaxM / 4][K * K];  // A: W[c = 4g + kq][m = pl][kh][kw], the whole launch
+#pragma unroll
+    for (int g = 0; g < kMaxM / 4; ++g)
+#pragma unroll
+        for (int t = 0; t < K * K; ++t) wreg[g][t] = wl[((4 * g + kq) * kMaxM + pl) * K * K + t];
     const int jw = j0 + wave * 16;  // this wave's first cell
     float bs0[4] = {0.f, 0.f, 0.f, 0.f}, bs1[4] = {0.f, 0.f, 0.f, 0.f}, bs2[4] = {0.f, 0.f, 0.f, 0.f};
     const int i_end = min(Hs, i0 + kRowsPB);
+    const int jo = jw + pl;
+    const bool cok = jo < Ws;
+    const int joc = cok ? jo : 0;
     for (int i = i0; i < i_end; ++i) {
+        // this row's sink operands first (ACTBWD: the saved forward output; ACCUM: the old
+        // value), all 8 in flight under the row's MFMAs
+        v2f_t pre[4][2];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const SinkRow& q = ri[min(4 * kq + r, a.M - 1)];
+            const bool ab = q.mode == ISG_SINK_ACTBWD;
+            const float* base = ab ? q.y : q.p;
+            const bool live = (ab || q.mode == ISG_SINK_ACCUM) && base;  // else a dummy read
+            const int64_t bns = ab ? q.yns : q.ns;
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+                pre[r][u] = *(gcv2_p)((gcfloat_p)(live ? base : a.dy.s[0].p) +  // 16-B aligned (down_src_ok)
+                                      (live ? (int64_t)n * bns + (int64_t)(2 * i + u) * Wd + 2 * joc : 0));
+        }
         f32x4 acc[2][2];
 #pragma unroll
         for (int u = 0; u < 2; ++u)
 #pragma unroll
             for (int v = 0; v < 2; ++v) acc[u][v] = f32x4{0.f, 0.f, 0.f, 0.f};
         const float* lb = Ls + kq * kSubPL + (i - i0) * kSubRS + wave * 16 + pl + 3;
+        // A operands in registers (loaded once per workgroup, below), B software-pipelined:
+        // kernel row (g, kh) + 1's five values are read while row (g, kh)'s MFMAs issue
+        auto brow = [&](int gk, float (&b)[K]) {
+            const int g = gk / K, kh = gk - g * K;
+            const int au = (kh + P) & 1, rr = (au + P - kh) / 2 + R0;
+            const float* lg = lb + 4 * g * kSubPL + rr * kSubRS;
 #pragma unroll
-        for (int g = 0; g < kMaxM / 4; ++g) {
-            const float* wa = wl + ((4 * g + kq) * kMaxM + pl) * K * K;  // A: c = 4g + kq, m = pl
-            const float* lg = lb + 4 * g * kSubPL;
+            for (int kw = 0; kw < K; ++kw) {
+                const int av = (kw + P) & 1, qq = (av + P - kw) / 2 + R0;
+                b[kw] = lg[qq];
+            }
+        };
+        float b0[K], b1[K];
+        brow(0, b0);
 #pragma unroll
-            for (int kh = 0; kh < K; ++kh) {
-                const int au = (kh + P) & 1, rr = (au + P - kh) / 2 + R0;
+        for (int gk = 0; gk < (kMaxM / 4) * K; ++gk) {
+            float (&cur)[K] = (gk & 1) ? b1 : b0;
+            if (gk + 1 < (kMaxM / 4) * K) {
+                if (gk & 1) brow(gk + 1, b0);
+                else brow(gk + 1, b1);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            const int g = gk / K, kh = gk - g * K;
+            const int au = (kh + P) & 1;
 #pragma unroll
-                for (int kw = 0; kw < K; ++kw) {
-                    const int av = (kw + P) & 1, qq = (av + P - kw) / 2 + R0;
-                    acc[au][av] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[kh * K + kw], lg[rr * kSubRS + qq],
-                                                                       acc[au][av], 0, 0, 0);
-                }
+            for (int kw = 0; kw < K; ++kw) {
+                const int av = (kw + P) & 1;
+                acc[au][av] = __builtin_amdgcn_mfma_f32_16x16x4f32(wreg[g][kh * K + kw], cur[kw],
+                                                                   acc[au][av], 0, 0, 0);
             }
         }
         // epilogue: lane holds D[m = 4kq + r][cell = pl] of every phase
-        const int jo = jw + pl;
-        const bool cok = jo < Ws;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int m = 4 * kq + r;
@@ -551,7 +653,8 @@ __global__ __launch_bounds__(kThreads) void sub2_dgrad_lds_kernel(DownArgs a) {
 #pragma unroll
                 for (int u = 0; u < 2; ++u) {
                     float t0 = 0.f, t1 = 0.f, t2 = 0.f;
-                    sink_row_apply2(q, n, (int64_t)(2 * i + u) * Wd + 2 * jo, acc[u][0][r], acc[u][1][r], t0, t1, t2);
+                    sink_row_apply2_pre(q, n, (int64_t)(2 * i + u) * Wd + 2 * jo, acc[u][0][r],
+                                        acc[u][1][r], pre[r][u], t0, t1, t2);
                     bs0[r] += t0;
                     bs1[r] += t1;
                     bs2[r] += t2;
@@ -559,6 +662,7 @@ __global__ __launch_bounds__(kThreads) void sub2_dgrad_lds_kernel(DownArgs a) {
             }
         }
     }
+    STAMP(3);
     if (sinks_need_red(a.out)) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -578,6 +682,7 @@ __global__ __launch_bounds__(kThreads) void sub2_dgrad_lds_kernel(DownArgs a) {
         }
     }
     sinks_finalize(a.out);
+    STAMP(4);
 }
 
 // ---- 5x5 stride-2 pad-2 weight gradient, LDS-staged (the stem's second conv) ------------
@@ -813,23 +918,59 @@ __global__ __launch_bounds__(2 * kThreads, 1) void s2k5_wgrad_kernel(S2wArgs a) 
             // re-derived 25 addresses per step and waited out each read)
             if (nq && NARROW) {
                 const float* const nb = Xs + 2 * wave * kWgRS + kq + 1;
+                // the same operand pipeline as the wide form below, two quads per stage
+                float av0[2], av1[2], b0[2][kNarN], b1[2][kNarN];
+                auto quads = [&](int q2, float (&av)[2], float (&b)[2][kNarN]) {
 #pragma unroll
-                for (int q = 0; q < kWgX / 4; ++q) {
-                    const float av = ab[4 * q];
-                    bsum += av;
+                    for (int h = 0; h < 2; ++h) {
+                        av[h] = ab[4 * (2 * q2 + h)];
 #pragma unroll
-                    for (int t = 0; t < kNarN; ++t)
-                        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, nb[noff[t] + 4 * q], acc[t], 0, 0, 0);
+                        for (int t = 0; t < kNarN; ++t) b[h][t] = nb[noff[t] + 4 * (2 * q2 + h)];
+                    }
+                };
+                quads(0, av0, b0);
+#pragma unroll
+                for (int q2 = 0; q2 < kWgX / 8; ++q2) {
+                    float (&av)[2] = (q2 & 1) ? av1 : av0;
+                    float (&cur)[2][kNarN] = (q2 & 1) ? b1 : b0;
+                    if (q2 + 1 < kWgX / 8) {
+                        if (q2 & 1) quads(q2 + 1, av0, b0);
+                        else quads(q2 + 1, av1, b1);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        bsum += av[h];
+#pragma unroll
+                        for (int t = 0; t < kNarN; ++t)
+                            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[h], cur[h][t], acc[t], 0, 0, 0);
+                    }
                 }
             } else if (nq) {
+                // software-pipelined operands: quad q + 1's A value and 25 B values are read
+                // from LDS while quad q's 25 MFMAs issue (sched_barrier keeps the reads above
+                // them; the compiler's own schedule waited out each read's latency)
+                float av0, av1, b0[NACC], b1[NACC];
+                auto quad = [&](int q, float& av, float (&b)[NACC]) {
+                    av = ab[4 * q];
+#pragma unroll
+                    for (int j = 0; j < NACC; ++j)
+                        b[j] = bb[(j / 5) * kWgRS + ((j % 5) & 1) * kWgEW + ((j % 5) >> 1) + 4 * q];
+                };
+                quad(0, av0, b0);
 #pragma unroll
                 for (int q = 0; q < kWgX / 4; ++q) {
-                    const float av = ab[4 * q];
+                    float& av = (q & 1) ? av1 : av0;
+                    float (&cur)[NACC] = (q & 1) ? b1 : b0;
+                    if (q + 1 < kWgX / 4) {
+                        if (q & 1) quad(q + 1, av0, b0);
+                        else quad(q + 1, av1, b1);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
                     bsum += av;
 #pragma unroll
                     for (int j = 0; j < NACC; ++j)
-                        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(
-                            av, bb[(j / 5) * kWgRS + ((j % 5) & 1) * kWgEW + ((j % 5) >> 1) + 4 * q], acc[j], 0, 0, 0);
+                        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, cur[j], acc[j], 0, 0, 0);
                 }
             }
             __syncthreads();
@@ -897,6 +1038,8 @@ __global__ __launch_bounds__(2 * kThreads, 1) void s2k5_wgrad_kernel(S2wArgs a) 
 constexpr int kFwPL = 816;  // channel plane (>= 11 * 72; 16 mod 32: lanes k = 0 / 1 of a B read hit disjoint banks)
 static_assert(kFwPL >= kWgNR * kWgRS && kFwPL % 32 == 16, "s2k5 fwd plane");
 constexpr int kFwOut = kMaxM * kWgX + 4;  // one wave's output row in LDS: [16 channels][32 columns] (+4: bank shift)
+constexpr int kS2fMaxWc = 32;  // weight input channels the forward's whole-weight copy takes (G < 4)
+static_assert(kMaxM * kS2fMaxWc * 25 <= kMaxM * kFwPL, "s2k5 fwd weight copy fits one band buffer");
 
 struct S2fArgs {
     isg_vtensor x;  // C channels, 2 OH x 2 OW
@@ -947,8 +1090,21 @@ __global__ __launch_bounds__(2 * kThreads, 1) void s2k5_fwd_kernel(S2fArgs a) {
             const int rr = rq / kWgQ, q = rq - rr * kWgQ;
             const int iy = 2 * oy0 - 2 + rr, ix = 2 * ox0 - 4 + 4 * q;
             const bool ok = c < a.C && (unsigned)iy < (unsigned)Hi && ix >= 0 && ix < Wi;
-            const S2Ch t = decltype(direct)::value ? s2_ch_addr(a.x, min(c, a.C - 1), Hi * Wi) : tabx[c];
-            xv[u] = gld4(t.p + (int64_t)n * t.ns, ok ? (int64_t)iy * Wi + ix : 0);
+            const int64_t o = ok ? (int64_t)iy * Wi + ix : 0;
+            if constexpr (decltype(direct)::value) {
+                // one segment (the stem's input: the image / the layer-1 output): the plane
+                // address from the kernel argument directly, no segment selection
+                const int cc = min(c, a.C - 1);
+                if (a.x.nseg == 1) {
+                    xv[u] = gld4(a.x.s[0].p + (int64_t)n * a.x.s[0].n_stride + (int64_t)cc * Hi * Wi, o);
+                } else {
+                    const S2Ch t = s2_ch_addr(a.x, cc, Hi * Wi);
+                    xv[u] = gld4(t.p + (int64_t)n * t.ns, o);
+                }
+            } else {
+                const S2Ch& t = tabx[c];
+                xv[u] = gld4(t.p + (int64_t)n * t.ns, o);
+            }
         }
     };
     // ONE round trip before the first barrier (each barrier waits for every load of the
@@ -957,25 +1113,25 @@ __global__ __launch_bounds__(2 * kThreads, 1) void s2k5_fwd_kernel(S2fArgs a) {
     // the weights had landed, and the coefficients after that)
     if (producer && t0 < t1) load(t0, std::true_type{});
     if (tid < kMaxM) tabx[tid] = s2_ch_addr(a.x, min(tid, a.C - 1), Hi * Wi);
-    {  // the weight into buffer 1 (first written by the producers after barrier B): every
-       // load of the thread in flight at once (a rolled loop paid one round trip per element)
+    {  // the weight [M][wc][25] copied whole and linearly into buffer 1 (first written by
+       // the producers after barrier B): every load of the thread in flight at once (a rolled
+       // loop paid one round trip per element), no index division (the per-element (m, c,
+       // tap) split by runtime divisors was most of this prologue's instructions)
         float* wl = s2f_lds + BAND;
-        const int nw = a.M * a.C * 25;
-        constexpr int UW = (kMaxM * 4 * G * 25 + 2 * kThreads - 1) / (2 * kThreads);
+        const int nw = a.M * a.wc * 25;
+        constexpr int UW = (kMaxM * (G == 4 ? 16 : kS2fMaxWc) * 25 + 2 * kThreads - 1) / (2 * kThreads);
         float wv[UW];
 #pragma unroll
-        for (int u = 0; u < UW; ++u) {
-            const int e = min(tid + u * 2 * kThreads, nw - 1);
-            const int mc = e / 25, t = e - mc * 25, m = mc / a.C, c = mc - m * a.C;
-            wv[u] = gld(a.w, ((int64_t)m * a.wc + c) * 25 + t);
-        }
+        for (int u = 0; u < UW; ++u) wv[u] = gld(a.w, min(tid + u * 2 * kThreads, nw - 1));
         if (tid < kMaxM) tabx[tid].k = s2_coef_x(a.x, min(tid, a.C - 1), Hi * Wi);
         else if (tid >= 64 && tid < 64 + kMaxM) ri[tid - 64] = sink_row(a.out, tid - 64, (int64_t)Ho * Wo);
 #pragma unroll
         for (int u = 0; u < UW; ++u)
             if (tid + u * 2 * kThreads < nw) wl[tid + u * 2 * kThreads] = wv[u];
     }
+    STAMP(1);
     __syncthreads();  // S0: channel table, coefficients, sink rows, weight copy, tile t0 loaded
+    STAMP(2);
     auto store = [&](int buf) {
         float* const Xs = s2f_lds + buf * BAND;
 #pragma unroll
@@ -1020,7 +1176,7 @@ __global__ __launch_bounds__(2 * kThreads, 1) void s2k5_fwd_kernel(S2fArgs a) {
             for (int g = 0; g < G; ++g) {
                 const int c = 4 * g + kq;
                 const bool ok = pl < a.M && c < a.C;
-                const float* wp = wl + (m * a.C + (c < a.C ? c : 0)) * 25;
+                const float* wp = wl + (m * a.wc + (c < a.C ? c : 0)) * 25;
 #pragma unroll
                 for (int t = 0; t < 25; ++t) wa[g][t] = ok ? wp[t] : 0.f;
             }
@@ -1036,24 +1192,43 @@ __global__ __launch_bounds__(2 * kThreads, 1) void s2k5_fwd_kernel(S2fArgs a) {
             bias[i] = a.st16 && a.out.s[0].bias ? a.out.s[0].bias[m] : 0.f;
         }
         __syncthreads();  // B
-        STAMP(1);
+        STAMP(3);
         for (int t = t0; t < t1; ++t) {
             int tn, ty0, tx0;
             tile_of(t, tn, ty0, tx0);
             const float* const bb = s2f_lds + ((t - t0) & 1) * BAND + kq * kFwPL + 2 * wave * kWgRS + pl + 1;
             f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+            // software-pipelined B operands: the next kernel row's 10 values are read from
+            // LDS into a second register set while this row's 10 MFMAs issue (the compiler's
+            // own schedule reused 8 registers and waited out the read latency every 4-5
+            // MFMAs: ~0.5 of the MFMA rate in the loop, kbench stamps r07)
+            auto rowb = [&](int gk, float (&b)[10]) {
+                const int g = gk / 5, kh = gk - g * 5;
 #pragma unroll
-            for (int g = 0; g < G; ++g)
+                for (int kw = 0; kw < 5; ++kw) {
+                    const float* bp = bb + 4 * g * kFwPL + kh * kWgRS + (kw & 1) * kWgEW + (kw >> 1);
+                    b[2 * kw] = bp[0];
+                    b[2 * kw + 1] = bp[16];
+                }
+            };
+            float b0[10], b1[10];
+            rowb(0, b0);
 #pragma unroll
-                for (int kh = 0; kh < 5; ++kh)
+            for (int gk = 0; gk < 5 * G; ++gk) {
+                float (&cur)[10] = (gk & 1) ? b1 : b0;
+                float (&nxt)[10] = (gk & 1) ? b0 : b1;
+                if (gk + 1 < 5 * G) rowb(gk + 1, nxt);
+                // keep those reads above this row's MFMAs (the scheduler otherwise sinks each
+                // read next to its use and the loop waits out every LDS latency)
+                __builtin_amdgcn_sched_barrier(0);
+                const int g = gk / 5, kh = gk - g * 5;
 #pragma unroll
-                    for (int kw = 0; kw < 5; ++kw) {
-                        const float* bp = bb + 4 * g * kFwPL + kh * kWgRS + (kw & 1) * kWgEW + (kw >> 1);
+                for (int kw = 0; kw < 5; ++kw)
 #pragma unroll
-                        for (int h = 0; h < 2; ++h)
-                            acc[h] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[g][kh * 5 + kw], bp[16 * h], acc[h], 0, 0, 0);
-                    }
-            if (t == t0) STAMP(2);
+                    for (int h = 0; h < 2; ++h)
+                        acc[h] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[g][kh * 5 + kw], cur[2 * kw + h], acc[h], 0, 0, 0);
+            }
+            if (t == t0) STAMP(4);
             // epilogue: lane holds D[m = 4kq + i][px = pl] of pixel group h, row ty0 + wave
             const int oy = ty0 + wave;
             if (a.st16) {
@@ -1102,11 +1277,10 @@ __global__ __launch_bounds__(2 * kThreads, 1) void s2k5_fwd_kernel(S2fArgs a) {
                     }
                 }
             }
-            if (t == t0) STAMP(3);
             __syncthreads();
-            if (t == t0) STAMP(4);
+            if (t == t0) STAMP(5);
         }
-        STAMP(5);
+        STAMP(6);
         if (sinks_need_red(a.out)) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -1127,7 +1301,7 @@ __global__ __launch_bounds__(2 * kThreads, 1) void s2k5_fwd_kernel(S2fArgs a) {
             sink_row_flush(a.out, tid, r3[0], r3[1], r3[2]);
         }
     }
-    STAMP(6);
+    STAMP(7);
 }
 
 bool down_geom(const isg_conv_geom* g, int& S) {
@@ -1251,6 +1425,8 @@ int32_t isg_s2k5_fwd(const isg_conv_geom* g, const isg_vtensor* x, const float* 
              out->s[0].C == g->Co && g->OW % 4 == 0 && (uintptr_t)out->s[0].p % 16 == 0 &&
              out->s[0].n_stride % 4 == 0;
     a.N = g->N; a.M = g->Co; a.C = g->Ci; a.wc = g->w_ci ? g->w_ci : g->Ci; a.OH = g->OH; a.OW = g->OW;
+    const int G = (a.C + 3) / 4;
+    if (a.wc > (G == 4 ? 16 : kS2fMaxWc)) return 0;  // the whole-weight copy's bound
     a.tiles_x = (a.OW + kWgX - 1) / kWgX;
     a.tiles_y = (a.OH + kWgRows - 1) / kWgRows;
     const int64_t nt = (int64_t)a.N * a.tiles_x * a.tiles_y;
@@ -1269,7 +1445,6 @@ int32_t isg_s2k5_fwd(const isg_conv_geom* g, const isg_vtensor* x, const float* 
     const int grid = (int)((nt + a.tpw - 1) / a.tpw);
     // two bands + the four consumer waves' output rows (st16 epilogue)
     const size_t lds = ((size_t)2 * kMaxM * kFwPL + 4 * kFwOut) * sizeof(float);
-    const int G = (a.C + 3) / 4;
     auto k = G == 1 ? s2k5_fwd_kernel<1> : G == 2 ? s2k5_fwd_kernel<2> : G == 3 ? s2k5_fwd_kernel<3>
                                                                                 : s2k5_fwd_kernel<4>;
     static bool attr[5] = {false, false, false, false, false};
