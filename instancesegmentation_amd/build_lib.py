@@ -15,7 +15,7 @@ CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libisg.so")
 SOURCES = ["conv_mfma.hip", "pw_gemm.hip", "tap_conv.hip", "tap_wgrad.hip", "thin_conv.hip", "halo_conv.hip", "wgrad.hip", "dw_convt.hip", "eltwise.hip", "maskops.hip", "infer_ops.hip", "kp_stem.hip", "down_conv.hip", "mask_head.hip", "api.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall",
+FLAGS = ["--offload-arch=gfx950", "-O2", "-fno-unroll-loops", "-std=c++17", "-fPIC", "-Wall",
          "-Wno-unused-function", "-Wno-pass-failed"]
 
 
