@@ -83,7 +83,7 @@ typedef struct {
  *           raw y: A*g + B*(y - mean) + C                       (BatchNorm2d backward) */
 typedef struct {
     const float* p;
-    const float* y;        /* BN_BWD only */
+    const float* y;        /* BN_BWD only; NULL: y = p (with p's n_stride) */
     int64_t n_stride;      /* elements between images of p */
     int64_t y_n_stride;
     int32_t C;
@@ -119,23 +119,12 @@ typedef struct {
     const float* slope;    /* ACTBWD + PRELU */
     double* slope_grad;    /* ACTBWD + PRELU, C doubles per replica */
     isg_bn bn;             /* ACTBWD; bn.stats==NULL means "no BN" (identity) */
-    /* Fused BatchNorm finalisation (train). fin_mode 1: once every workgroup's output
-     * sums are in fin_bn.stats, write fin_bn's forward coefficients into fin_bn.coef
-     * (what isg_bn_finalize(bwd=0) writes); 2: the backward coefficients (bwd=1). The
-     * LAST workgroup of the producing launch does it (isg_sinks.fin_counter ticket). */
-    isg_bn fin_bn;
-    int32_t fin_mode;
-    int32_t fin_pad_;
 } isg_sink;
 
 typedef struct {
     isg_sink s[ISG_MAX_SEGS];
     int32_t nsink;
     int32_t pad_;
-    /* 33 zeroed uint32 (a two-level ticket) per launch when any sink has fin_mode != 0
-     * (the last workgroup re-zeroes them, so a HIP-graph replay finds them zero again);
-     * NULL otherwise */
-    uint32_t* fin_counter;
 } isg_sinks;
 
 typedef struct {

@@ -45,13 +45,11 @@ class Sink(Structure):
     _fields_ = [("p", c_void_p), ("n_stride", c_int64), ("c0", c_int32), ("C", c_int32),
                 ("mode", c_int32), ("act", c_int32), ("bias", c_void_p), ("stats", c_void_p),
                 ("y", c_void_p), ("y_n_stride", c_int64), ("slope", c_void_p),
-                ("slope_grad", c_void_p), ("bn", Bn), ("fin_bn", Bn), ("fin_mode", c_int32),
-                ("fin_pad_", c_int32)]
+                ("slope_grad", c_void_p), ("bn", Bn)]
 
 
 class Sinks(Structure):
-    _fields_ = [("s", Sink * MAX_SEGS), ("nsink", c_int32), ("pad_", c_int32),
-                ("fin_counter", c_void_p)]
+    _fields_ = [("s", Sink * MAX_SEGS), ("nsink", c_int32), ("pad_", c_int32)]
 
 
 class Geom(Structure):

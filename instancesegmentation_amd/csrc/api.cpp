@@ -8,16 +8,11 @@
 #include <cstring>
 #include <string>
 #include <utility>
-#include <deque>
 #include <vector>
 
 #include "../../include/isg.h"
 
 static thread_local std::string g_last_error;
-static thread_local bool g_fin_handled = false;
-
-void isg_fin_note_handled() { g_fin_handled = true; }
-
 
 int32_t isg_set_error(int32_t code, const char* fmt, ...) {
     char buf[512];
@@ -83,15 +78,29 @@ int32_t isg_tap_wgrad(const isg_conv_geom*, const isg_vtensor*, const isg_vtenso
 // part): only tap_conv / tap_wgrad index the weight with a separate channel count
 static bool partial_w(const isg_conv_geom* g) { return g->w_ci > 0 && g->w_ci != g->Ci; }
 
+// a BN_BWD segment without y (isg.h isg_vseg: y = p, at p's image stride), resolved once
+// here so no kernel has to know the convention
+static isg_vtensor resolve_y(const isg_vtensor* v) {
+    isg_vtensor r = *v;
+    for (int i = 0; i < r.nseg && i < ISG_MAX_SEGS; ++i)
+        if (r.s[i].xform == ISG_XF_BN_BWD && !r.s[i].y) {
+            r.s[i].y = r.s[i].p;
+            r.s[i].y_n_stride = r.s[i].n_stride;
+        }
+    return r;
+}
+
 extern "C" {
 
 const char* isg_last_error(void) { return g_last_error.c_str(); }
 int32_t isg_abi_version(void) { return 9; }
 int32_t isg_stat_replicas(void) { return ISG_STAT_REP; }
 
-int32_t isg_conv_fwd(const isg_conv_geom* g, const isg_vtensor* x, const float* w,
+int32_t isg_conv_fwd(const isg_conv_geom* g, const isg_vtensor* x_, const float* w,
                      const isg_sinks* out, isg_stream_t st) {
     if (int32_t e = check_geom(g)) return e;
+    const isg_vtensor xr = resolve_y(x_);
+    const isg_vtensor* x = &xr;
     if (partial_w(g)) {
         // the stem's RGB layer 1 (5x5 s2, weight over w_ci = 20 channels): s2k5_fwd_kernel
         const int32_t s = isg_s2k5_fwd(g, x, w, out, st);
@@ -104,18 +113,22 @@ int32_t isg_conv_fwd(const isg_conv_geom* g, const isg_vtensor* x, const float* 
     return isg_depthwise_fwd(g, x, w, out, st);
 }
 
-int32_t isg_conv_dgrad(const isg_conv_geom* g, const isg_vtensor* dy, const float* w,
+int32_t isg_conv_dgrad(const isg_conv_geom* g, const isg_vtensor* dy_, const float* w,
                        const isg_sinks* dx, isg_stream_t st) {
     if (int32_t e = check_geom(g)) return e;
+    const isg_vtensor dyr = resolve_y(dy_);
+    const isg_vtensor* dy = &dyr;
     if (partial_w(g)) return isg_set_error(ISG_ERR_UNSUPPORTED, "conv dgrad with w_ci != Ci");
     if (g->groups == 1) return isg_dense_conv_dgrad(g, dy, w, dx, st);
     return isg_depthwise_dgrad(g, dy, w, dx, st);
 }
 
-int32_t isg_conv_wgrad_rep(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x,
+int32_t isg_conv_wgrad_rep(const isg_conv_geom* g, const isg_vtensor* dy_, const isg_vtensor* x_,
                            double* dw, double* dbias, int64_t rep_stride, int32_t nrep,
                            isg_stream_t st) {
     if (int32_t e = check_geom(g)) return e;
+    const isg_vtensor dyr = resolve_y(dy_), xr = resolve_y(x_);
+    const isg_vtensor *dy = &dyr, *x = &xr;
     if (nrep < 1 || (nrep > 1 && rep_stride <= 0))
         return isg_set_error(ISG_ERR_INVALID, "conv wgrad: bad replicas %d / stride %lld", nrep,
                              (long long)rep_stride);
@@ -229,7 +242,7 @@ enum { ISG_OPF_SIDE = 1, ISG_OPF_JOIN = 2, ISG_OPF_FORK_NOW = 4 };  // FORK_NOW:
 // fork / join events of the executor's side streams, per device (created on first use,
 // never destroyed; timing disabled): ev[0] fork, ev[1] join of side stream 0, ev[2] join
 // of side stream 1
-constexpr int kForkPool = 16;  // fork events of side-stream batches recorded but not yet launched
+constexpr int kForkPool = 16;  // fork events of side-stream batches, used round robin
 static int32_t side_events(hipEvent_t* join, hipEvent_t* join2, hipEvent_t** forks) {
     static hipEvent_t ev[64][2 + kForkPool];
     int dev = 0;
@@ -250,57 +263,14 @@ struct Fix {
     int64_t offset;
 };
 
-static int32_t run_op_raw(int32_t kind, char* buf, isg_stream_t st);
-
 // wgrad.hip: grouped 1x1 weight gradients (the executor's side-stream batches)
 int32_t isg_pwg_plan_bytes();
 int32_t isg_pwg_group_max();
 int32_t isg_pwg_plan(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, double* dw,
                      double* dbias, int64_t rep_stride, int32_t nrep, void* plan);
 int32_t isg_pwg_run(const void* const* plans, int32_t n, hipStream_t st);
-// dw_convt.hip: grouped depthwise weight gradients
-int32_t isg_dwg_plan_bytes();
-int32_t isg_dwg_group_max();
-int32_t isg_dwg_plan(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, double* dw,
-                     double* dbias, int64_t rep_stride, int32_t nrep, void* plan);
-int32_t isg_dwg_run(const void* const* plans, int32_t n, hipStream_t st);
-
-// BN finalisation the producing kernel did not fuse (its launcher did not report
-// isg_fin_note_handled): one isg_bn_finalize launch per sink, as before the fusion.
-static int32_t fin_fallback(const isg_sinks* sk, isg_stream_t st) {
-    if (!sk || !sk->fin_counter || g_fin_handled) return ISG_OK;
-    for (int i = 0; i < sk->nsink && i < ISG_MAX_SEGS; ++i) {
-        if (!sk->s[i].fin_mode) continue;
-        isg_bn b = sk->s[i].fin_bn;
-        if (int32_t e = isg_bn_finalize(&b, 1, sk->s[i].fin_mode == 2 ? 1 : 0, st)) return e;
-    }
-    return ISG_OK;
-}
-
-// experiment (tools/gpu_ab.sh, timing only — the gradients are wrong): ISG_DBG_NOP_WGRAD=1
-// replaces every weight-gradient op with an empty one-wave launch (same graph nodes, no
-// work), =2 drops them (no nodes): separates the side streams' node count from their work
-__global__ void isg_nop_kernel() {}
 
 static int32_t run_op(int32_t kind, char* buf, isg_stream_t st) {
-    static const int nop_wgrad = getenv("ISG_DBG_NOP_WGRAD") ? atoi(getenv("ISG_DBG_NOP_WGRAD")) : 0;
-    if (nop_wgrad && kind == OP_CONV_WGRAD) {
-        if (nop_wgrad == 1) {
-            hipLaunchKernelGGL(isg_nop_kernel, dim3(1), dim3(64), 0, st);
-            return isg_check_launch("nop");
-        }
-        return ISG_OK;
-    }
-    g_fin_handled = false;
-    int32_t rc = run_op_raw(kind, buf, st);
-    if (rc) return rc;
-    const isg_sinks* sk = nullptr;
-    if (kind == OP_CONV_FWD || kind == OP_CONV_DGRAD || kind == OP_CONVT_FWD) sk = &((ConvRec*)buf)->out;
-    else if (kind == OP_MAXPOOL_BWD) sk = &((PoolRec*)buf)->dx;
-    return fin_fallback(sk, st);
-}
-
-static int32_t run_op_raw(int32_t kind, char* buf, isg_stream_t st) {
     int32_t rc = 0;
     switch (kind) {
         case OP_CONV_FWD: {
@@ -403,35 +373,22 @@ int32_t isg_exec_ms2(const void* ops, int32_t nops, void* const* table, isg_stre
     alignas(16) char buf[8192];
     hipEvent_t ev_join = nullptr, ev_join2 = nullptr, *ev_forks = nullptr;
     bool forked = false, forked2 = false;  // side-stream work outstanding since the last join
-    static const int batch = [] {
+    // both knobs are read per call (cheap next to a launch), so a test can switch them
+    const int batch = [] {
         // weight gradients deferred per fork: 48 with two side streams and one backward
         // part (4.415 -> 4.365 ms/step against 24; 36: 4.405, 64: 4.42, 96: 4.48 — r03y)
         const char* e = getenv("ISG_SIDE_BATCH");
         const int b = e ? atoi(e) : 48;
         return b < 1 ? 1 : b;
     }();
-    // A batch's fork point is recorded on the main stream when the batch closes, but its
-    // kernels are issued only after `delay` more main-stream ops. Under stream capture the
-    // graph then holds the main-stream chain's next nodes BEFORE the batch's nodes, and
-    // the graph launch dispatches them first (with the batch issued at its fork point, the
-    // launch queued the whole batch ahead of the chain's continuation: the input-gradient
-    // chain stood still ~0.5 ms per step behind 40-odd weight gradients, kernel trace k6).
-    static const int delay = [] {
-        const char* e = getenv("ISG_SIDE_DELAY");
-        return e ? std::max(0, atoi(e)) : 0;
-    }();
     // grouped 1x1 weight gradients in weight-gradient batches (4.04 -> 3.96
     // ms/step, 2 interleaved 200-step pairs; ISG_NO_PWG_GROUP=1 off)
-    static const bool pwg_group_on = getenv("ISG_NO_PWG_GROUP") == nullptr;
-    // the depthwise ones too (opt-in ISG_DW_GROUP=1 until measured)
-    static const bool dwg_group_on = getenv("ISG_DW_GROUP") != nullptr;
+    const bool pwg_group_on = getenv("ISG_NO_PWG_GROUP") == nullptr;
     struct Batch {
         std::vector<std::pair<int32_t, std::string>> ops;
         hipEvent_t ev;
-        int countdown;
     };
     std::vector<std::pair<int32_t, std::string>> pending;
-    std::deque<Batch> ready;
     int pool_next = 0;
     int deal = 0;  // weight gradients alternate between the side streams across batches too
     auto launch = [&](Batch& bt) -> int32_t {
@@ -479,27 +436,22 @@ int32_t isg_exec_ms2(const void* ops, int32_t nops, void* const* table, isg_stre
             std::memcpy(pb, bt.ops[i].second.data(), bt.ops[i].second.size());
             auto* r = (WgradRec*)pb;
             if (!geom_ok(&r->g)) continue;
-            plans[i].resize((size_t)std::max(isg_pwg_plan_bytes(), isg_dwg_plan_bytes()));
+            plans[i].resize((size_t)isg_pwg_plan_bytes());
             key[i] = isg_pwg_plan(&r->g, &r->dy, &r->x, r->dw, r->dbias, r->rep_stride,
                                   r->nrep < 1 ? 1 : r->nrep, plans[i].data());
-            if (key[i] == 0 && dwg_group_on)
-                key[i] = isg_dwg_plan(&r->g, &r->dy, &r->x, r->dw, r->dbias, r->rep_stride,
-                                      r->nrep < 1 ? 1 : r->nrep, plans[i].data());
         }
         std::vector<char> done(n, 0);
         for (size_t i = 0; i < n; ++i) {
             if (done[i]) continue;
             if (key[i] > 0) {
-                const bool dwk = key[i] >= 1000;  // isg_dwg_plan's keys
-                const int cap = dwk ? isg_dwg_group_max() : gmax;
                 const void* grp[8];
                 int m = 0;
-                for (size_t j = i; j < n && m < cap && m < 8; ++j)
+                for (size_t j = i; j < n && m < gmax && m < 8; ++j)
                     if (!done[j] && key[j] == key[i]) {
                         grp[m++] = plans[j].data();
                         done[j] = 1;
                     }
-                if (int32_t e = dwk ? isg_dwg_run(grp, m, next_st()) : isg_pwg_run(grp, m, next_st())) return e;
+                if (int32_t e = isg_pwg_run(grp, m, next_st())) return e;
                 continue;
             }
             std::memcpy(pb, bt.ops[i].second.data(), bt.ops[i].second.size());
@@ -507,29 +459,16 @@ int32_t isg_exec_ms2(const void* ops, int32_t nops, void* const* table, isg_stre
         }
         return ISG_OK;
     };
-    auto drain = [&](bool all) -> int32_t {  // issue the ready batches due (FIFO)
-        while (!ready.empty() && (all || ready.front().countdown <= 0)) {
-            if (int32_t e = launch(ready.front())) return e;
-            ready.pop_front();
-        }
-        return ISG_OK;
-    };
-    auto close_batch = [&]() -> int32_t {  // the pending batch's fork point is here
+    auto close_batch = [&]() -> int32_t {  // the pending batch forks here and is issued
         if (pending.empty()) return ISG_OK;
-        if ((int)ready.size() >= kForkPool)
-            if (int32_t e = launch(ready.front())) return e;
-        if ((int)ready.size() >= kForkPool) ready.pop_front();
         Batch bt;
         bt.ops.swap(pending);
         bt.ev = ev_forks[pool_next++ % kForkPool];
-        bt.countdown = delay;
         if (hipEventRecord(bt.ev, main_st) != hipSuccess) return isg_check_launch("exec: fork point");
-        ready.push_back(std::move(bt));
-        return drain(false);
+        return launch(bt);
     };
     auto join = [&]() -> int32_t {
         if (int32_t e = close_batch()) return e;
-        if (int32_t e = drain(true)) return e;
         if (forked) {
             forked = false;
             if (hipEventRecord(ev_join, side) != hipSuccess || hipStreamWaitEvent(main_st, ev_join, 0) != hipSuccess)
@@ -576,14 +515,9 @@ int32_t isg_exec_ms2(const void* ops, int32_t nops, void* const* table, isg_stre
             pending.emplace_back(h.kind, std::string(buf, buf + h.desc_bytes));
             if ((int)pending.size() >= batch || (h.flags & ISG_OPF_FORK_NOW)) {
                 rc = close_batch();
-                if (!rc && (h.flags & ISG_OPF_FORK_NOW)) rc = drain(true);
             }
         } else {
             rc = run_op(h.kind, buf, st);
-            if (!rc && !ready.empty()) {
-                for (auto& bt : ready) --bt.countdown;
-                rc = drain(false);
-            }
         }
         if (rc) {
             std::string m = g_last_error;

@@ -74,19 +74,11 @@ ISG_DEV int rep_of_block() {
 }
 // pointer to this workgroup's replica of an accumulator of n values
 ISG_DEV double* rep_ptr(double* base, int n) { return base + (int64_t)rep_of_block() * n; }
-// sum over replicas of element i of an accumulator of n values. fresh: read inside the
-// launch whose workgroups are still adding to it (the fused finalisation's last
-// workgroup): agent-scope loads (global_load sc1, past this CU's L1) of values that only
-// agent-scope atomics wrote (performed past every XCD's L2), so no release/acquire fence
-// pair is needed (MI355X_MICROARCH.md, inter-workgroup visibility, hand-off row 1).
-ISG_DEV double rep_sum(const double* base, int n, int i, bool fresh = false) {
+// sum over replicas of element i of an accumulator of n values (fixed order)
+ISG_DEV double rep_sum(const double* base, int n, int i) {
     double s = 0.0;
 #pragma unroll
-    for (int r = 0; r < ISG_STAT_REP; ++r) {
-        const double* p = base + (int64_t)r * n + i;
-        s += fresh ? __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                   : *p;
-    }
+    for (int r = 0; r < ISG_STAT_REP; ++r) s += base[(int64_t)r * n + i];
     return s;
 }
 
@@ -123,9 +115,9 @@ ISG_DEV ChanCoef bwd_coef_of(double mean, double rstd, float gamma, double gs, d
     return k;
 }
 
-ISG_DEV void bn_mean_rstd(const isg_bn& bn, int c, double& mean, double& rstd, bool fresh = false) {
+ISG_DEV void bn_mean_rstd(const isg_bn& bn, int c, double& mean, double& rstd) {
     if (bn.train) {
-        mean_rstd_of(rep_sum(bn.stats, 4 * bn.C, c, fresh), rep_sum(bn.stats, 4 * bn.C, bn.C + c, fresh),
+        mean_rstd_of(rep_sum(bn.stats, 4 * bn.C, c), rep_sum(bn.stats, 4 * bn.C, bn.C + c),
                      bn.count, bn.eps, mean, rstd);
     } else {
         mean = (double)bn.running_mean[c];
@@ -134,29 +126,29 @@ ISG_DEV void bn_mean_rstd(const isg_bn& bn, int c, double& mean, double& rstd, b
 }
 
 // forward coefficients of a BN_FWD segment channel
-ISG_DEV ChanCoef fwd_coef(const isg_bn& bn, const float* slope, int c, bool fresh = false) {
+ISG_DEV ChanCoef fwd_coef(const isg_bn& bn, const float* slope, int c) {
     if (bn.coef) {  // finalised once per layer (isg_bn_finalize)
         const f32x4 f = reinterpret_cast<const f32x4*>(bn.coef)[c];
         return ChanCoef{f[0], f[1], f[2], slope ? slope[c] : 0.f};
     }
     double mean, rstd;
-    bn_mean_rstd(bn, c, mean, rstd, fresh);
+    bn_mean_rstd(bn, c, mean, rstd);
     return fwd_coef_of(mean, rstd, bn.gamma[c], bn.beta[c], slope ? slope[c] : 0.f);
 }
 
 // backward coefficients: dy = A*g + B*(y-mean) + C
-ISG_DEV ChanCoef bwd_coef(const isg_bn& bn, int c, bool fresh = false) {
+ISG_DEV ChanCoef bwd_coef(const isg_bn& bn, int c) {
     if (bn.coef) {
         const f32x4 f = reinterpret_cast<const f32x4*>(bn.coef)[bn.C + c];
         return ChanCoef{f[0], f[1], f[2], f[3]};
     }
     double mean, rstd;
-    bn_mean_rstd(bn, c, mean, rstd, fresh);
+    bn_mean_rstd(bn, c, mean, rstd);
     double gam = (double)bn.gamma[c];
     ChanCoef k;
     if (bn.train) {
-        k = bwd_coef_of(mean, rstd, bn.gamma[c], rep_sum(bn.stats, 4 * bn.C, 2 * bn.C + c, fresh),
-                        rep_sum(bn.stats, 4 * bn.C, 3 * bn.C + c, fresh), bn.count);
+        k = bwd_coef_of(mean, rstd, bn.gamma[c], rep_sum(bn.stats, 4 * bn.C, 2 * bn.C + c),
+                        rep_sum(bn.stats, 4 * bn.C, 3 * bn.C + c), bn.count);
     } else {
         k.c0 = (float)(gam * rstd);
         k.c1 = 0.f;
@@ -354,80 +346,6 @@ ISG_DEV bool sinks_need_red(const isg_sinks& sk) {
     }
     return false;
 }
-
-// ---- fused BatchNorm finalisation ---------------------------------------------------
-// Every thread of every workgroup of a launch whose sinks carry fin_mode calls this LAST
-// (no early return before it). The handed-off bytes are the statistics, which every
-// workgroup writes ONLY with agent-scope atomic adds (performed past the XCD L2s): each
-// wave waits for its own atomics (vmcnt(0)), the workgroup barrier orders all waves
-// before lane 0's ticket add, and the last arriver reads the statistics with agent-scope
-// (sc1) loads (rep_sum fresh) — hand-off row 1 of MI355X_MICROARCH.md's inter-workgroup
-// table, with no release fence (an L2 write-back per workgroup, which had made this
-// fusion slower than the separate finalisation launch it replaces). Tickets are two
-// level — 32 sub-counters, the last arriver of each bumps the top counter — so at most
-// ~nb/32 workgroups contend on one address. The workgroup that completes the top counter
-// evaluates the coefficients (fp64, isg_bn_finalize's math), then re-zeroes the
-// counters. Counter block: ISG_FIN_CTR uint32 (top, then 32 subs), zeroed.
-#define ISG_FIN_SUBS 32
-ISG_DEV bool fin_last_block(uint32_t* ctr) {
-    __shared__ int s_last;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0 && threadIdx.y == 0) {
-        const unsigned nb = gridDim.x * gridDim.y * gridDim.z;
-        const unsigned b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
-        // the HIP memory model's hand-off: release before the ticket, acquire
-        // in the last workgroup before it reads the other workgroups' statistics
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        bool last;
-        if (nb <= 2 * ISG_FIN_SUBS) {
-            last = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nb - 1;
-        } else {
-            const unsigned sub = b % ISG_FIN_SUBS;
-            const unsigned ns = nb / ISG_FIN_SUBS + (sub < nb % ISG_FIN_SUBS ? 1u : 0u);
-            last = __hip_atomic_fetch_add(ctr + 1 + sub, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ns - 1 &&
-                   __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ISG_FIN_SUBS - 1;
-        }
-        if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        s_last = last ? 1 : 0;
-    }
-    __syncthreads();
-    return s_last != 0;
-}
-
-// Block-cooperative: the coefficients of one sink's fin_bn (fp64, isg_bn_finalize's math).
-ISG_DEV void fin_sink(const isg_sink& k) {
-    if (!k.fin_mode) return;
-    const int tid = threadIdx.x + threadIdx.y * blockDim.x, nt = blockDim.x * blockDim.y;
-    isg_bn bn = k.fin_bn;
-    float* const out = bn.coef;
-    bn.coef = nullptr;  // evaluate from the statistics
-    for (int c = tid; c < bn.C; c += nt) {
-        if (k.fin_mode == 1) {
-            const ChanCoef f = fwd_coef(bn, nullptr, c, true);
-            reinterpret_cast<f32x4*>(out)[c] = f32x4{f.c0, f.c1, f.c2, 0.f};
-        } else {
-            const ChanCoef f = bwd_coef(bn, c, true);
-            reinterpret_cast<f32x4*>(out)[bn.C + c] = f32x4{f.c0, f.c1, f.c2, f.c3};
-        }
-    }
-}
-
-ISG_DEV void fin_reset(uint32_t* ctr) {
-    const int tid = threadIdx.x + threadIdx.y * blockDim.x;
-    if (tid <= ISG_FIN_SUBS) __hip_atomic_store(ctr + tid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-ISG_DEV void sinks_finalize(const isg_sinks& sk) {
-    uint32_t* const ctr = sk.fin_counter;
-    if (!ctr || !fin_last_block(ctr)) return;
-    for (int s = 0; s < sk.nsink; ++s) fin_sink(s == 2 ? sk.s[2] : (s == 1 ? sk.s[1] : sk.s[0]));
-    fin_reset(ctr);
-}
-
-// Host: launchers of kernels that end in sinks_finalize() report it here, so the
-// executor knows whether a separate finalisation launch is still needed.
-void isg_fin_note_handled();
 
 // ---- diagnostic stamps (built only into the tools/kbench harness library) -------------
 // STAMP(i): thread 0 of each workgroup records s_memrealtime (100 MHz, chip-global) in

@@ -199,7 +199,6 @@ __global__ __launch_bounds__(kThreads) void gemm_conv_kernel(GemmArgs a) {
         __syncthreads();
         flush_sink_red(a.out, red[0][0], red[0][1], red[0][2], a.M, tid, kThreads);
     }
-    sinks_finalize(a.out);
 }
 
 int vt_channels(const isg_vtensor* v) {
@@ -233,7 +232,6 @@ int32_t dispatch_gemm(const GemmArgs& a, dim3 grid, hipStream_t st) {
         case 13: case 14: case 15: case 16: launch_gemm<16>(a, grid, st); break;
         default: return isg_set_error(ISG_ERR_UNSUPPORTED, "gemm conv: %d rows > 256", a.M);
     }
-    if (a.out.fin_counter) isg_fin_note_handled();
     return isg_check_launch("gemm_conv_kernel");
 }
 

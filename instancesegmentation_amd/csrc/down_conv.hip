@@ -152,7 +152,6 @@ __global__ __launch_bounds__(kThreads) void down_conv_kernel(DownArgs a) {
             sink_row_flush(a.out, tid, r3[0], r3[1], r3[2]);
         }
     }
-    sinks_finalize(a.out);
 }
 
 // weight gradient: tiles of TY x TX cells; lane t = column (c, kh, kw) < C*K*K <= 256
@@ -282,150 +281,18 @@ ISG_DEV void sink_row_apply2(const SinkRow& q, int n, int64_t pix, float v0, flo
     }
 }
 
-// MFMA form of the same input gradient (v_mfma_f32_16x16x4_f32): a wave owns 16
-// consecutive cells of one dy row and all 4 phases x 16 outputs of their 2x2 blocks.
-// K runs over (channel group of 4, tap): A[m][k] = W[4g + k][m][kh][kw] (lane: m = l&15,
-// k = l>>4), B[k][cell] = the transformed dy value of channel 4g + k at the tap's
-// neighbour of the cell (lane: k = l>>4, cell = l&15), one MFMA per (group, tap) into the
-// tap's phase accumulator: 4 x 25 MFMAs per 16 cells for Co = 16. D lane: m = 4(l>>4)+r.
 constexpr int kRowsPB = 4;  // dy rows per workgroup (measured: 1 row 81 us, 2 76, 4 67, 8 102)
 
-template <int K>
-__global__ __launch_bounds__(kThreads) void sub2_dgrad_mfma_kernel(DownArgs a) {
-    constexpr int P = K / 2, R0 = P / 2, NB = P + 1;
-    __shared__ float wl[kMaxM * kMaxM * K * K];  // [c][m][kh][kw] (the weight's own layout)
-    __shared__ ChT tab[kMaxM];
-    __shared__ SinkRow ri[kMaxM];
-    __shared__ float red[4][3][kMaxM];
-    const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
-    const int kq = lane >> 4, pl = lane & 15;
-    const int Hs = a.H, Ws = a.W, Wd = 2 * Ws;
-    if (tid < a.C) tab[tid] = ch_table_entry(a.dy, tid, (int64_t)Hs * Ws);
-    if (tid < a.M) ri[tid] = sink_row(a.out, tid, (int64_t)2 * Hs * Wd);
-    {   // the weight: every load of the thread issued before the first store (a rolled loop
-        // of predicated loads paid one L2 round trip per element: 25 in a row)
-        constexpr int NW = kMaxM * kMaxM * K * K, UW = NW / kThreads;
-        static_assert(NW % kThreads == 0, "weight copy split");
-        const int nw = a.C * a.M * K * K;
-        float wv[UW];
-#pragma unroll
-        for (int u = 0; u < UW; ++u) {
-            const int e = tid + u * kThreads;
-            const int c = e / (kMaxM * K * K), r = e - c * kMaxM * K * K;
-            const int m = r / (K * K), tap = r - m * K * K;
-            const int src = (c * a.M + m) * K * K + tap;
-            wv[u] = gld(a.w, (c < a.C && m < a.M) ? src : 0);
-            wv[u] = (c < a.C && m < a.M && src < nw) ? wv[u] : 0.f;
-        }
-#pragma unroll
-        for (int u = 0; u < UW; ++u) wl[tid + u * kThreads] = wv[u];
-    }
-    __syncthreads();
-    // block: 64 cells (4 waves x 16) of kRowsPB consecutive rows, one row at a time (the
-    // weight staging above is amortised over the rows); grid x = row segments, y = row
-    // groups, z = images
-    const int n = blockIdx.z;
-    const int jw = blockIdx.x * 64 + wave * 16;  // this wave's first cell
-    const int j = jw + pl;                       // this lane's B cell
-    float bs0[4] = {0.f, 0.f, 0.f, 0.f}, bs1[4] = {0.f, 0.f, 0.f, 0.f}, bs2[4] = {0.f, 0.f, 0.f, 0.f};
-    const int i_end = min(Hs, (int)(blockIdx.y + 1) * kRowsPB);
-    for (int i = blockIdx.y * kRowsPB; i < i_end; ++i) {
-    f32x4 acc[2][2];
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int v = 0; v < 2; ++v) acc[u][v] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // all channel groups unrolled (channels past C masked): the compiler can issue every
-    // group's neighbourhood loads ahead of the MFMAs
-#pragma unroll
-    for (int g = 0; g < kMaxM / 4; ++g) {
-        const int c = 4 * g + kq;
-        const bool cv = c < a.C;
-        const ChT t = tab[cv ? c : 0];
-        const bool bwd = t.xf == ISG_XF_BN_BWD;
-        const float* xp = t.p + (int64_t)n * t.ns;
-        const float* yp = t.y + (int64_t)n * t.yns;
-        float nb[NB][NB];
-        {
-            float rx[NB][NB], ry[NB][NB];
-            bool ok[NB][NB];
-#pragma unroll
-            for (int r = 0; r < NB; ++r)
-#pragma unroll
-                for (int q = 0; q < NB; ++q) {
-                    const int yy = i - R0 + r, xx = j - R0 + q;
-                    ok[r][q] = cv && (unsigned)yy < (unsigned)Hs && (unsigned)xx < (unsigned)Ws;
-                    const int64_t o = ok[r][q] ? (int64_t)yy * Ws + xx : 0;
-                    rx[r][q] = gld(xp, o);
-                    ry[r][q] = bwd ? gld(yp, o) : 0.f;
-                }
-#pragma unroll
-            for (int r = 0; r < NB; ++r)
-#pragma unroll
-                for (int q = 0; q < NB; ++q)
-                    nb[r][q] = ok[r][q] ? ch_xform(t.xf, t.act, t.k, rx[r][q], ry[r][q]) : 0.f;
-        }
-        const float* wa = wl + ((4 * g + kq) * kMaxM + pl) * K * K;  // A: c = 4g + kq, m = pl
-#pragma unroll
-        for (int kh = 0; kh < K; ++kh) {
-            const int au = (kh + P) & 1, rr = (au + P - kh) / 2 + R0;
-#pragma unroll
-            for (int kw = 0; kw < K; ++kw) {
-                const int av = (kw + P) & 1, qq = (av + P - kw) / 2 + R0;
-                acc[au][av] = __builtin_amdgcn_mfma_f32_16x16x4f32(wa[kh * K + kw], nb[rr][qq], acc[au][av], 0, 0, 0);
-            }
-        }
-    }
-    // epilogue: lane holds D[m = 4kq + r][cell = pl] of every phase
-    const int jo = jw + pl;
-    const bool cok = jo < Ws;
-    float* const s0 = bs0;
-    float* const s1 = bs1;
-    float* const s2 = bs2;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int m = 4 * kq + r;
-        if (cok && m < a.M) {
-            const SinkRow q = ri[m];
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                float t0 = 0.f, t1 = 0.f, t2 = 0.f;
-                sink_row_apply2(q, n, (int64_t)(2 * i + u) * Wd + 2 * jo, acc[u][0][r], acc[u][1][r], t0, t1, t2);
-                s0[r] += t0;
-                s1[r] += t1;
-                s2[r] += t2;
-            }
-        }
-    }
-    }  // rows
-    if (sinks_need_red(a.out)) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const float t0 = dpp_row16_sum(bs0[r]), t1 = dpp_row16_sum(bs1[r]), t2 = dpp_row16_sum(bs2[r]);
-            if (pl == 0) {
-                red[wave][0][4 * kq + r] = t0;
-                red[wave][1][4 * kq + r] = t1;
-                red[wave][2][4 * kq + r] = t2;
-            }
-        }
-        __syncthreads();
-        if (tid < a.M) {
-            float r3[3];
-#pragma unroll
-            for (int q3 = 0; q3 < 3; ++q3) r3[q3] = ((red[0][q3][tid] + red[1][q3][tid]) + red[2][q3][tid]) + red[3][q3][tid];
-            sink_row_flush(a.out, tid, r3[0], r3[1], r3[2]);
-        }
-    }
-    sinks_finalize(a.out);
-}
-
-// LDS-staged form (the path taken): the workgroup's dy band — kRowsPB + 2 rows x (64 + 2)
+// The input gradient as an MFMA GEMM (v_mfma_f32_16x16x4_f32): a wave owns 16 consecutive
+// cells of one dy row and all 4 phases x 16 outputs of their 2x2 blocks; K runs over
+// (channel group of 4, tap): A[m][k] = W[4g + k][m][kh][kw], B[k][cell] = the transformed
+// dy value of channel 4g + k at the tap's neighbour of the cell; one MFMA per (group, tap)
+// into the tap's phase accumulator. The workgroup's dy band — kRowsPB + 2 rows x (64 + 2)
 // columns x 16 channels — is loaded ONCE with 16-B loads, transformed once per element
 // (BatchNorm backward rebuilt from g and the saved y) and zero-padded into LDS; the MFMA
 // B operands are then conflict-free ds_read_b32 (channel planes 16 mod 32 banks apart).
-// The direct form above re-read every dy element from L2 in up to 9 lanes (4-B loads)
-// and re-transformed it each time: ~11 VALU instructions per MFMA, 61 % of wave cycles
-// waiting (profiles/r02f_pmc_sq_summary.txt).
+// (Round 2's direct form, operands straight from L2, re-read every dy element in up to 9
+// lanes and re-transformed it each time: 61 % of wave cycles waiting, removed in round 5.)
 constexpr int kSubRS = 72;                 // staged row: column x at x - (j0 - 4), 0..68
 constexpr int kSubPL = 432;                // channel plane (>= (kRowsPB + 2) * 72, 16 mod 32)
 static_assert(kSubPL >= (kRowsPB + 2) * kSubRS && kSubPL % 32 == 16, "staging plane");
@@ -681,7 +548,6 @@ __global__ __launch_bounds__(kThreads) void sub2_dgrad_lds_kernel(DownArgs a) {
             sink_row_flush(a.out, tid, r3[0], r3[1], r3[2]);
         }
     }
-    sinks_finalize(a.out);
     STAMP(4);
 }
 
@@ -721,7 +587,6 @@ struct S2wArgs {
     int nrep;
     int N, M, C, wc, OH, OW;
     int tiles_x, tiles_y, ntiles, tpw;
-    int dbg;  // ablation bits (ISG_S2W_DBG, experiments only): 1 no MFMA loop, 2 no global loads, 4 no LDS staging
 };
 
 // Branch-free staging record: x side v = (raw - k0) * k1 + k2, then v > 0 ? v : v * k3
@@ -804,7 +669,6 @@ __global__ __launch_bounds__(2 * kThreads, 1) void s2k5_wgrad_kernel(S2wArgs a) 
         const int r = t - n * tpi, ty = r / a.tiles_x;
         oy0 = ty * kWgRows;
         ox0 = (r - ty * a.tiles_x) * kWgX;
-        if (a.dbg & 2) return;
 #pragma unroll
         for (int u = 0; u < UX; ++u) {
             const int e = min(ptid + u * kThreads, NE - 1);
@@ -829,7 +693,6 @@ __global__ __launch_bounds__(2 * kThreads, 1) void s2k5_wgrad_kernel(S2wArgs a) 
         }
     };
     auto store = [&](int buf) {
-        if (a.dbg & 4) return;
         float* const Xs = s2w_lds + buf * kWgLds;
         float* const Ds = Xs + kMaxM * kWgPL;
 #pragma unroll
@@ -908,7 +771,7 @@ __global__ __launch_bounds__(2 * kThreads, 1) void s2k5_wgrad_kernel(S2wArgs a) 
         __syncthreads();  // A
         __syncthreads();  // B
         STAMP(2);
-        const int nq = (a.dbg & 1) ? 0 : kWgX / 4;
+        const int nq = kWgX / 4;
         for (int t = t0; t < t1; ++t) {
             const float* const Xs = s2w_lds + ((t - t0) & 1) * kWgLds;
             const float* const ab = Xs + kMaxM * kWgPL + pl * kWgDQ + wave * kWgX + kq;
@@ -1344,7 +1207,6 @@ int32_t isg_down_conv_fwd(const isg_conv_geom* g, const isg_vtensor* src, const 
         if (a.M <= 4) hipLaunchKernelGGL((down_conv_kernel<2, 4>), grid, dim3(kThreads), 0, st, a);
         else hipLaunchKernelGGL((down_conv_kernel<2, 16>), grid, dim3(kThreads), 0, st, a);
     }
-    if (out->fin_counter) isg_fin_note_handled();
     const int32_t e = isg_check_launch("down_conv_kernel");
     return e ? e : 1;
 }
@@ -1370,8 +1232,7 @@ int32_t isg_down_conv_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const
     a.ntiles = a.N * a.tiles_x * ((a.H + TY - 1) / TY);
     // ~2 tiles per workgroup (measured on the head's k8 s4: 4 tiles 74 us, 2 tiles 58 us,
     // 8 tiles 127 us — parallelism, not the dW atomics, bounds it)
-    static const int env_grid = getenv("ISG_DOWN_WG_GRID") ? atoi(getenv("ISG_DOWN_WG_GRID")) : 0;
-    const int grid = std::max(1, std::min(a.ntiles, env_grid ? env_grid : std::max(512, a.ntiles / 2)));
+    const int grid = std::max(1, std::min(a.ntiles, std::max(512, a.ntiles / 2)));
     if (S == 4) {
         if (a.M <= 4) hipLaunchKernelGGL((down_wgrad_kernel<4, 4, TY, TX>), dim3(grid), dim3(kThreads), 0, st, a);
         else hipLaunchKernelGGL((down_wgrad_kernel<4, 16, TY, TX>), dim3(grid), dim3(kThreads), 0, st, a);
@@ -1395,12 +1256,8 @@ int32_t isg_sub2_dgrad(const isg_conv_geom* g, const isg_vtensor* dy, const floa
     a.dy = *dy; a.out = *dx; a.w = w;
     a.N = g->N; a.M = g->Ci; a.C = g->Co; a.H = g->OH; a.W = g->OW;
     const dim3 grid((unsigned)((a.W + 63) / 64), (unsigned)((a.H + kRowsPB - 1) / kRowsPB), (unsigned)a.N);
-    static const bool direct = getenv("ISG_SUB2_DIRECT") != nullptr;  // the unstaged form (A/B)
-    if (!direct && a.W % 4 == 0 && down_src_ok(dy))
-        hipLaunchKernelGGL(sub2_dgrad_lds_kernel, grid, dim3(kThreads), 0, st, a);
-    else
-        hipLaunchKernelGGL((sub2_dgrad_mfma_kernel<5>), grid, dim3(kThreads), 0, st, a);
-    if (dx->fin_counter) isg_fin_note_handled();
+    if (a.W % 4 || !down_src_ok(dy)) return 0;  // tap_conv's stride-1 phases instead
+    hipLaunchKernelGGL(sub2_dgrad_lds_kernel, grid, dim3(kThreads), 0, st, a);
     const int32_t e = isg_check_launch("sub2_dgrad_kernel");
     return e ? e : 1;
 }
@@ -1413,15 +1270,14 @@ int32_t isg_s2k5_fwd(const isg_conv_geom* g, const isg_vtensor* x, const float* 
     if (off || g->groups != 1 || g->SH != 2 || g->SW != 2 || g->KH != 5 || g->KW != 5 ||
         g->PH != 2 || g->PW != 2 || g->DH != 1 || g->DW != 1 || g->H != 2 * g->OH ||
         g->W != 2 * g->OW || g->W % 4 || g->Co > kMaxM || g->Ci > kMaxM ||
-        (g->w_ci && g->w_ci < g->Ci) || !down_src_ok(x) || out->fin_counter)
+        (g->w_ci && g->w_ci < g->Ci) || !down_src_ok(x))
         return 0;
     for (int i = 0; i < x->nseg; ++i)  // the branch-free staging transform: PLAIN / BN_FWD
         if (x->s[i].xform == ISG_XF_BN_BWD) return 0;
     if ((int64_t)g->H * g->W >= (1ll << 31)) return 0;
     S2fArgs a{};
     a.x = *x; a.w = w; a.out = *out;
-    static const bool no16 = getenv("ISG_S2F_NO16") != nullptr;  // A/B: per-element sink epilogue
-    a.st16 = !no16 && out->nsink == 1 && out->s[0].mode == ISG_SINK_STORE && out->s[0].c0 == 0 &&
+    a.st16 = out->nsink == 1 && out->s[0].mode == ISG_SINK_STORE && out->s[0].c0 == 0 &&
              out->s[0].C == g->Co && g->OW % 4 == 0 && (uintptr_t)out->s[0].p % 16 == 0 &&
              out->s[0].n_stride % 4 == 0;
     a.N = g->N; a.M = g->Co; a.C = g->Ci; a.wc = g->w_ci ? g->w_ci : g->Ci; a.OH = g->OH; a.OW = g->OW;
@@ -1439,8 +1295,7 @@ int32_t isg_s2k5_fwd(const isg_conv_geom* g, const isg_vtensor* x, const float* 
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
             cus = 256;
     }
-    static const int env_wg = getenv("ISG_S2F_WGS") ? atoi(getenv("ISG_S2F_WGS")) : 0;
-    const int target = env_wg > 0 ? env_wg : cus;  // one 8-wave workgroup per CU (LDS 2 x 52 KB + 8 KB)
+    const int target = cus;  // one 8-wave workgroup per CU (LDS 2 x 52 KB + 8 KB)
     a.tpw = (int)std::max<int64_t>(1, (nt + target - 1) / target);
     const int grid = (int)((nt + a.tpw - 1) / a.tpw);
     // two bands + the four consumer waves' output rows (st16 epilogue)
@@ -1480,8 +1335,6 @@ int32_t isg_s2k5_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_
     a.rep_stride = nrep > 1 ? rep_stride : 0;
     a.nrep = nrep < 1 ? 1 : nrep;
     a.N = g->N; a.M = g->Co; a.C = g->Ci; a.wc = g->w_ci ? g->w_ci : g->Ci; a.OH = g->OH; a.OW = g->OW;
-    static const int dbg = getenv("ISG_S2W_DBG") ? atoi(getenv("ISG_S2W_DBG")) : 0;
-    a.dbg = dbg;
     a.tiles_x = (a.OW + kWgX - 1) / kWgX;
     a.tiles_y = (a.OH + kWgRows - 1) / kWgRows;
     const int64_t nt = (int64_t)a.N * a.tiles_x * a.tiles_y;
@@ -1494,8 +1347,7 @@ int32_t isg_s2k5_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
             cus = 256;
     }
-    static const int env_wg = getenv("ISG_S2W_WGS") ? atoi(getenv("ISG_S2W_WGS")) : 0;
-    const int target = env_wg > 0 ? env_wg : cus;  // one 8-wave workgroup per CU (LDS 2 x 60 KB)
+    const int target = cus;  // one 8-wave workgroup per CU (LDS 2 x 60 KB)
     a.tpw = (int)std::max<int64_t>(1, (nt + target - 1) / target);
     const int grid = (int)((nt + a.tpw - 1) / a.tpw);
     bool yb = false;

@@ -132,7 +132,6 @@ ISG_DEV bool sink1_needs_red(const isg_sink& k) {
 struct DwArgs {
     isg_vseg x;      // fwd: input; dgrad: dy
     isg_sink out;
-    uint32_t* fin_counter;  // fused BN finalisation ticket (isg_sinks.fin_counter)
     const float* w;  // [C][KH][KW]
     int N, C, H, W, OH, OW, KH, KW, PH, PW, DH, DW;
 };
@@ -209,10 +208,6 @@ __global__ __launch_bounds__(kThreads) void dw_kernel(DwArgs a) {
     if (sink1_needs_red(a.out)) {
         block_reduce<3>(red, sh);
         if (threadIdx.x == 0) sink1_flush(a.out, c, red);
-    }
-    if (a.fin_counter && fin_last_block(a.fin_counter)) {
-        fin_sink(a.out);
-        fin_reset(a.fin_counter);
     }
 }
 
@@ -342,7 +337,7 @@ __global__ __launch_bounds__(kThreads) void dw_tile_kernel(DwArgs a) {
 template <bool DGRAD>
 int dw_tile_try(const isg_conv_geom* g, const DwArgs& a, hipStream_t st) {
     static const bool off = getenv("ISG_NO_DW_TILE") != nullptr;
-    if (off || a.fin_counter || g->SH != 1 || g->SW != 1 || g->OH != g->H || g->OW != g->W || g->W % 4)
+    if (off || g->SH != 1 || g->SW != 1 || g->OH != g->H || g->OW != g->W || g->W % 4)
         return 0;
     const isg_sink& o = a.out;
     if (o.mode == ISG_SINK_NONE || ((uintptr_t)o.p & 15) || o.n_stride % 4 ||
@@ -519,35 +514,6 @@ __global__ __launch_bounds__(kThreads) void dw_wgrad_tile_kernel(DwWgArgs a) {
     dw_wgrad_tile_body<KH_, KW_>(a, blockIdx.x, blockIdx.y, blockIdx.z);
 }
 
-// up to kDwgGroup depthwise weight gradients of one tap shape in one launch (the
-// executor's side-stream batches, as pwg_group_kernel): flat block ranges per problem
-constexpr int kDwgGroup = 6;
-struct DwgGroup {
-    DwWgArgs p[kDwgGroup];
-    int start[kDwgGroup + 1];
-    int gx[kDwgGroup], gy[kDwgGroup];
-    int n;
-};
-
-template <int KH_, int KW_>
-__global__ __launch_bounds__(kThreads) void dw_wgrad_group_kernel(DwgGroup g) {
-    const int b = blockIdx.x;
-    int i = 0;
-#pragma unroll
-    for (int k = 1; k < kDwgGroup; ++k) i = (k < g.n && b >= g.start[k]) ? k : i;
-    const int l = b - g.start[i];
-    const int gxy = g.gx[i] * g.gy[i];
-    const unsigned bz = l / gxy, r = l - bz * gxy, by = r / g.gx[i], bx = r - by * g.gx[i];
-    switch (i) {  // one inlined body per slot: a selected copy of the record would go through scratch
-        case 0: dw_wgrad_tile_body<KH_, KW_>(g.p[0], bx, by, bz); break;
-        case 1: dw_wgrad_tile_body<KH_, KW_>(g.p[1], bx, by, bz); break;
-        case 2: dw_wgrad_tile_body<KH_, KW_>(g.p[2], bx, by, bz); break;
-        case 3: dw_wgrad_tile_body<KH_, KW_>(g.p[3], bx, by, bz); break;
-        case 4: dw_wgrad_tile_body<KH_, KW_>(g.p[4], bx, by, bz); break;
-        default: dw_wgrad_tile_body<KH_, KW_>(g.p[5], bx, by, bz); break;
-    }
-}
-
 // ---- transposed convolution, kernel 2S, stride S, pad S/2 --------------------------
 struct CtArgs {
     isg_vseg x;      // [N][Ci][H][W]
@@ -697,12 +663,11 @@ int32_t isg_depthwise_fwd(const isg_conv_geom* g, const isg_vtensor* x, const fl
                           const isg_sinks* out, hipStream_t st) {
     if (x->nseg != 1 || out->nsink != 1 || g->SH != 1 || g->SW != 1 || g->Ci != g->Co)
         return isg_set_error(ISG_ERR_UNSUPPORTED, "depthwise fwd: need 1 seg/sink, stride 1");
-    DwArgs a{x->s[0], out->s[0], out->fin_counter, w, g->N, g->Ci, g->H, g->W, g->OH, g->OW,
+    DwArgs a{x->s[0], out->s[0], w, g->N, g->Ci, g->H, g->W, g->OH, g->OW,
              g->KH, g->KW, g->PH, g->PW, g->DH, g->DW};
     if (dw_tile_try<false>(g, a, st)) return isg_check_launch("dw_tile_kernel<fwd>");
     dim3 grid((unsigned)(((int64_t)g->OH * g->OW + kThreads - 1) / kThreads), g->Ci, g->N);
     dw_launch<false>(g, a, grid, st);
-    if (a.fin_counter) isg_fin_note_handled();
     return isg_check_launch("dw_kernel<fwd>");
 }
 
@@ -710,12 +675,11 @@ int32_t isg_depthwise_dgrad(const isg_conv_geom* g, const isg_vtensor* dy, const
                             const isg_sinks* dx, hipStream_t st) {
     if (dy->nseg != 1 || dx->nsink != 1 || g->SH != 1 || g->SW != 1 || g->Ci != g->Co)
         return isg_set_error(ISG_ERR_UNSUPPORTED, "depthwise dgrad: need 1 seg/sink, stride 1");
-    DwArgs a{dy->s[0], dx->s[0], dx->fin_counter, w, g->N, g->Ci, g->H, g->W, g->OH, g->OW,
+    DwArgs a{dy->s[0], dx->s[0], w, g->N, g->Ci, g->H, g->W, g->OH, g->OW,
              g->KH, g->KW, g->PH, g->PW, g->DH, g->DW};
     if (dw_tile_try<true>(g, a, st)) return isg_check_launch("dw_tile_kernel<dgrad>");
     dim3 grid((unsigned)(((int64_t)g->H * g->W + kThreads - 1) / kThreads), g->Ci, g->N);
     dw_launch<true>(g, a, grid, st);
-    if (a.fin_counter) isg_fin_note_handled();
     return isg_check_launch("dw_kernel<dgrad>");
 }
 
@@ -774,10 +738,8 @@ int32_t isg_convT_fwd(const isg_conv_geom* g, const isg_vtensor* x, const float*
     const unsigned gx = (unsigned)(((int64_t)g->N * g->H * g->W + kThreads - 1) / kThreads);
     if (S != 2 && S != 4) return isg_set_error(ISG_ERR_UNSUPPORTED, "convT fwd: s=%d", S);
     // channels per thread: split the output channels until the grid has ~1024 blocks
-    static const int cob_env = getenv("ISG_CONVT_COB") ? atoi(getenv("ISG_CONVT_COB")) : 0;
     int cob = g->Co;
     while (cob > 1 && (int64_t)gx * (g->Co / cob) < 1024 && cob % 2 == 0) cob /= 2;
-    if (cob_env > 0 && g->Co % cob_env == 0) cob = cob_env;
     if (cob > 4 || g->Co % cob) cob = g->Co % 4 == 0 ? 4 : (g->Co % 2 == 0 ? 2 : 1);
     const dim3 grid(gx, (unsigned)(g->Co / cob));
     if (S == 2 && cob == 4) hipLaunchKernelGGL((convT_kernel<2, 4>), grid, dim3(kThreads), 0, st, a);
@@ -788,78 +750,3 @@ int32_t isg_convT_fwd(const isg_conv_geom* g, const isg_vtensor* x, const float*
     else hipLaunchKernelGGL((convT_kernel<4, 1>), grid, dim3(kThreads), 0, st, a);
     return isg_check_launch("convT_kernel");
 }
-
-// ---- executor hooks (api.cpp): the depthwise weight gradients of a side-stream batch,
-// grouped like the 1x1 ones (wgrad.hip isg_pwg_plan / isg_pwg_run) -----------------------
-namespace {
-struct DwgPlan {
-    DwWgArgs a;
-    unsigned gx, gy, gz;
-    int kh, kw;
-    int key() const { return 1000 + kh * 10 + kw; }
-};
-
-template <int KH_, int KW_>
-int32_t dwg_group_launch(const DwgPlan* const* pl, int n, hipStream_t st) {
-    DwgGroup g{};
-    int64_t total = 0;
-    for (int i = 0; i < n; ++i) {
-        g.p[i] = pl[i]->a;
-        g.start[i] = (int)total;
-        g.gx[i] = (int)pl[i]->gx;
-        g.gy[i] = (int)pl[i]->gy;
-        total += (int64_t)pl[i]->gx * pl[i]->gy * pl[i]->gz;
-    }
-    g.start[n] = (int)total;
-    g.n = n;
-    if (total >= (1ll << 31)) return isg_set_error(ISG_ERR_UNSUPPORTED, "dw wgrad group: grid");
-    hipLaunchKernelGGL((dw_wgrad_group_kernel<KH_, KW_>), dim3((unsigned)total), dim3(kThreads), 0, st, g);
-    return isg_check_launch("dw_wgrad_group_kernel");
-}
-}  // namespace
-
-extern "C" int32_t isg_dwg_plan_bytes() { return (int32_t)sizeof(DwgPlan); }
-extern "C" int32_t isg_dwg_group_max() { return kDwgGroup; }
-
-// > 0 (the tap-shape key) when isg_conv_wgrad_rep would run this op on dw_wgrad_tile_kernel
-extern "C" int32_t isg_dwg_plan(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x,
-                                double* dw, double* dbias, int64_t rep_stride, int32_t nrep, void* plan) {
-    if (!dw || nrep < 1 || (nrep > 1 && rep_stride <= 0)) return 0;
-    if (g->groups == 1 || g->groups != g->Ci || g->Ci != g->Co || (g->w_ci && g->w_ci != g->Ci)) return 0;
-    if (dy->nseg != 1 || x->nseg != 1 || g->KH * g->KW > kMaxTaps || x->s[0].xform == ISG_XF_BN_BWD) return 0;
-    if (dy->s[0].C != g->Co || x->s[0].C != g->Ci) return 0;
-    static const bool off = getenv("ISG_NO_DW_TILE") != nullptr;
-    const isg_vseg& d = dy->s[0];
-    const bool ok = !off && g->SH == 1 && g->SW == 1 && g->OH == g->H && g->OW == g->W && g->W % 4 == 0 &&
-                    !((uintptr_t)d.p & 15) && d.n_stride % 4 == 0 &&
-                    (d.xform != ISG_XF_BN_BWD || (!((uintptr_t)d.y & 15) && d.y_n_stride % 4 == 0)) &&
-                    (g->KH - 1) * g->DH <= 16 && (g->KW - 1) * g->DW <= 16;
-    const bool shape = (g->KH == 3 && g->KW == 3) || (g->KH == 5 && g->KW == 1) || (g->KH == 1 && g->KW == 5);
-    if (!ok || !shape) return 0;
-    DwgPlan& p = *static_cast<DwgPlan*>(plan);
-    p = DwgPlan{};
-    DwWgArgs& a = p.a;
-    a.dy = dy->s[0]; a.x = x->s[0]; a.dw = dw; a.dbias = dbias;
-    a.rep_stride = rep_stride; a.nrep = nrep;
-    a.N = g->N; a.C = g->Ci; a.H = g->H; a.W = g->W; a.OH = g->OH; a.OW = g->OW;
-    a.KH = g->KH; a.KW = g->KW; a.PH = g->PH; a.PW = g->PW; a.DH = g->DH; a.DW = g->DW;
-    p.gx = (unsigned)((g->W + kDtX - 1) / kDtX);
-    p.gy = (unsigned)((g->H + kDtY - 1) / kDtY);
-    p.gz = (unsigned)(g->Ci * g->N);
-    p.kh = g->KH;
-    p.kw = g->KW;
-    return p.key();
-}
-
-extern "C" int32_t isg_dwg_run(const void* const* plans, int32_t n, hipStream_t st) {
-    if (n < 1 || n > kDwgGroup) return isg_set_error(ISG_ERR_INVALID, "dw wgrad group of %d", n);
-    const DwgPlan* pl[kDwgGroup];
-    for (int i = 0; i < n; ++i) {
-        pl[i] = static_cast<const DwgPlan*>(plans[i]);
-        if (pl[i]->key() != pl[0]->key()) return isg_set_error(ISG_ERR_INVALID, "dw wgrad group: mixed shapes");
-    }
-    if (pl[0]->kh == 3) return dwg_group_launch<3, 3>(pl, n, st);
-    if (pl[0]->kh == 5) return dwg_group_launch<5, 1>(pl, n, st);
-    return dwg_group_launch<1, 5>(pl, n, st);
-}
-

@@ -898,8 +898,7 @@ int32_t isg_bn_finalize(const isg_bn* items, int32_t nitems, int32_t bwd, isg_st
     for (int i = 0; i < nitems; ++i)
         if (!items[i].coef || !items[i].stats || (((uintptr_t)items[i].coef) & 15))
             return isg_set_error(ISG_ERR_INVALID, "bn_finalize: item %d needs stats and a 16-B aligned coef", i);
-    static const bool list_only = getenv("ISG_BNF_LIST") != nullptr;
-    if (nitems == 1 && !list_only) {
+    if (nitems == 1) {
         hipLaunchKernelGGL(bn_finalize1_kernel, dim3(1), dim3(items[0].C > 64 ? 128 : 64), 0, st,
                            items[0], bwd ? 1 : 0);
         return isg_check_launch("bn_finalize1_kernel");

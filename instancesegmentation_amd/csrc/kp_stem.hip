@@ -50,7 +50,6 @@ struct KpArgs {
     float* out;
     int64_t out_ns;
     int tiles_x, FH, FW;
-    int dbg;  // ablation bits (ISG_KP_DBG, experiments only): 1 no maps, 2 no MACs, 4 no apply, 8 exit after the ballot
 };
 
 struct Win {
@@ -116,7 +115,7 @@ __global__ __launch_bounds__(kThreads) void kp_fwd_kernel(KpArgs a) {
     }
     __syncthreads();
     uint32_t mask = act_mask;
-    if (!mask || (a.dbg & 8)) return;  // block-uniform: no window reaches this tile
+    if (!mask) return;  // block-uniform: no window reaches this tile
     const int KK = a.KK;
     {
         float* const wf = reinterpret_cast<float*>(wl);
@@ -148,10 +147,9 @@ __global__ __launch_bounds__(kThreads) void kp_fwd_kernel(KpArgs a) {
         __syncthreads();  // previous part's map consumed (and wl / toff written, first time)
         for (int i = tid; i < a.FH * a.FW; i += kThreads) {
             const int r = i / a.FW, c = i - r * a.FW;
-            hl[i] = (a.dbg & 1) ? 0.f : heat(a, w, iy0 + r, ix0 + c);
+            hl[i] = heat(a, w, iy0 + r, ix0 + c);
         }
         __syncthreads();
-        if (a.dbg & 2) continue;
         const f32x4* wp = wl + s * KK * (kMaxCo / 4);
         int t = 0;
         for (; t + 5 <= KK; t += 5) {
@@ -171,7 +169,7 @@ __global__ __launch_bounds__(kThreads) void kp_fwd_kernel(KpArgs a) {
     }
     // apply + statistics change (sum, sum of squares) of the stored values
     const int oy = oy0 + py, ox = ox0 + px;
-    const bool in = oy < a.OH && ox < a.OW && !(a.dbg & 4);
+    const bool in = oy < a.OH && ox < a.OW;
     float d0[kMaxCo], d1[kMaxCo];
 #pragma unroll
     for (int c = 0; c < kMaxCo; ++c) {
@@ -365,8 +363,6 @@ int32_t isg_kp_stem_fwd(const isg_kp_stem* s, isg_stream_t st) {
     // the active parts' weights: Co x nact x KK floats in LDS
     if (kMaxCo * a.nparts * a.KK > kMaxWl)
         return isg_set_error(ISG_ERR_UNSUPPORTED, "kp_stem_fwd: %d parts x %d taps", a.nparts, a.KK);
-    static const int dbg = getenv("ISG_KP_DBG") ? atoi(getenv("ISG_KP_DBG")) : 0;
-    a.dbg = dbg;
     a.tiles_x = (a.OW + kTile - 1) / kTile;
     const int tiles_y = (a.OH + kTile - 1) / kTile;
     hipLaunchKernelGGL(kp_fwd_kernel, dim3((unsigned)(a.tiles_x * tiles_y), (unsigned)a.N),

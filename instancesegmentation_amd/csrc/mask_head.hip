@@ -192,207 +192,6 @@ __global__ __launch_bounds__(kThreads, 2) void head_fwd_kernel(isg_mask_head a) 
 
 // dT GEMM A operand in LDS: Wd[o = (co, r, s)][k = (a, b)][ci] = W1[ci][co][r + 4(1-a)][s + 4(1-b)]
 // (a lane reads word o * 64 + lane: conflict-free)
-ISG_DEV void stage_wd(const float* w1s, float* Wd) {
-    for (int e = threadIdx.x; e < kW1; e += kThreads) {
-        const int ci = e & 15, k = (e >> 4) & 3, o = e >> 6;
-        const int co = o >> 4, r = (o >> 2) & 3, s = o & 3, aa = k >> 1, bb = k & 1;
-        Wd[e] = w1s[((ci * kCm + co) * 8 + r + 4 * (1 - aa)) * 8 + s + 4 * (1 - bb)];
-    }
-}
-
-constexpr int XPP = NCELL;        // phase-split intermediate gradient: one (co, r, s) plane
-constexpr int XCF = kCm * 16 * XPP > kCm * IRP ? kCm * 16 * XPP : kCm * IRP;
-
-__global__ __launch_bounds__(kThreads, 2) void head_bwd_v1_kernel(isg_mask_head a, int ntx, int nty,
-                                                                  int ntiles) {
-    __shared__ float Ts[kCi][RY][RXS];
-    __shared__ float Ds[DY * DXS];
-    __shared__ __attribute__((aligned(16))) float Xc[XCF];  // intermediate, then its gradient
-    __shared__ float Wd[kW1];
-    __shared__ ChanCoef coef[kCi];
-    __shared__ SinkRow sk[kCi];
-    __shared__ float red[kCm * 4];
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane((int)(tid >> 6));
-    const int kq = lane >> 4, nl = lane & 15;
-    const int OH = 4 * a.Hi, OW = 4 * a.Wi;
-    const int64_t hw = (int64_t)a.Hi * a.Wi;
-    load_vt_coefs(a.x, coef, tid, kThreads);
-    copy_w1(a.w1, Xc);
-    __syncthreads();
-    stage_wd(Xc, Wd);
-    if (tid < kCi) {
-        SinkRow q = {};
-        q.mode = ISG_SINK_NONE;
-        if (a.dx.nsink > 0) q = sink_row(a.dx, tid, hw);
-        sk[tid] = q;
-    }
-    float wf[kCm][kCi];
-    cell_afrag(Xc, wf);
-    // convT weight gradient: this wave's 4 N-tiles of the [16 ci] x [256 (co, ky, kx)] GEMM
-    f32x4 dw1[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) dw1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // 3x3 weight / bias gradient: per-tile partials wave-reduced into LDS (acc2[37])
-    __shared__ float acc2[kCm * 9 + 1];
-    if (tid < kCm * 9 + 1) acc2[tid] = 0.f;
-    float db1[kCm];
-#pragma unroll
-    for (int co = 0; co < kCm; ++co) db1[co] = 0.f;
-
-    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const int n = tile / (ntx * nty), t2 = tile - n * ntx * nty;
-        const int Y0 = (t2 / ntx) * TY, X0 = (t2 % ntx) * TX;
-        __syncthreads();  // previous tile's LDS consumed (and the tables ready)
-        load_input(a, coef, n, Y0, X0, Ts);
-        for (int i = tid; i < DY * DX; i += kThreads) {
-            const int r = i / DX, q = i - r * DX;
-            const int oy = Y0 - 3 + r, ox = X0 - 3 + q;
-            float v = 0.f;
-            if (oy >= 0 && oy < OH && ox >= 0 && ox < OW)
-                v = a.dout[(int64_t)n * a.dout_n_stride + (int64_t)oy * OW + ox];
-            Ds[r * DXS + q] = v;
-        }
-        __syncthreads();
-        intermediate_mfma(a, Y0, X0, Ts, wf, Xc);  // origin (Y0 - 2, X0 - 2)
-        __syncthreads();
-        // ---- 3x3 weight / bias gradient over the tile's own logit pixels
-        {
-            const int lx = tid & 63, rb = tid >> 6;
-            float dl[8], dw2[kCm * 9], db2 = 0.f;
-#pragma unroll
-            for (int i = 0; i < kCm * 9; ++i) dw2[i] = 0.f;
-#pragma unroll
-            for (int o = 0; o < 8; ++o) {
-                dl[o] = Ds[(rb * 8 + o + 3) * DXS + lx + 3];  // zero outside the image
-                db2 += dl[o];
-            }
-#pragma unroll
-            for (int co = 0; co < kCm; ++co) {
-#pragma unroll
-                for (int rr = 0; rr < 10; ++rr) {
-                    const float* row = Xc + co * IRP + (rb * 8 + rr + 1) * IRS + lx + 1;
-                    const float v0 = row[0], v1 = row[1], v2 = row[2];
-#pragma unroll
-                    for (int dy = 0; dy < 3; ++dy) {
-                        const int o = rr - dy;
-                        if (o < 0 || o >= 8) continue;
-                        dw2[(co * 3 + dy) * 3 + 0] += dl[o] * v0;
-                        dw2[(co * 3 + dy) * 3 + 1] += dl[o] * v1;
-                        dw2[(co * 3 + dy) * 3 + 2] += dl[o] * v2;
-                    }
-                }
-            }
-#pragma unroll
-            for (int i = 0; i < kCm * 9; ++i) {
-                const float w = wave_sum(dw2[i]);
-                if (lane == 0) atomicAdd(&acc2[i], w);
-            }
-            const float b = wave_sum(db2);
-            if (lane == 0) atomicAdd(&acc2[kCm * 9], b);
-        }
-        __syncthreads();
-        // ---- intermediate gradient over the cell region (origin (Y0 - 2, X0 - 2)), stored
-        //      phase-split: Xc[((co * 4 + r) * 4 + s) * NCELL + cy * CX + cx]
-        for (int p = tid; p < GY * GX; p += kThreads) {
-            const int qy = p / GX, qx = p - qy * GX;
-            const int oy = Y0 - 2 + qy, ox = X0 - 2 + qx;
-            const bool in = oy >= 0 && oy < OH && ox >= 0 && ox < OW;
-            const bool own = qy >= 2 && qy < 2 + TY && qx >= 2 && qx < 2 + TX;
-            const float* d = Ds + qy * DXS + qx;  // d[(2 - dy) * DXS + 2 - dx] = dl[oy+1-dy][ox+1-dx]
-            const int dst = ((qy & 3) * 4 + (qx & 3)) * NCELL + (qy >> 2) * CX + (qx >> 2);
-#pragma unroll
-            for (int co = 0; co < kCm; ++co) {
-                float v = 0.f;
-#pragma unroll
-                for (int dy = 0; dy < 3; ++dy)
-#pragma unroll
-                    for (int dx = 0; dx < 3; ++dx)
-                        v += a.w2[(co * 3 + dy) * 3 + dx] * d[(2 - dy) * DXS + 2 - dx];
-                v = in ? v : 0.f;
-                if (own) db1[co] += v;
-                Xc[co * 16 * NCELL + dst] = v;
-            }
-        }
-        __syncthreads();
-        // ---- input gradient (MFMA): D[ci][px] = sum_{o, (a,b)} Wd[o][(a,b)][ci] *
-        //      dI[o][cell (ly + 1 - a, lx + 1 - b)]; wave w: own input rows w and w + 4
-        {
-            const int aa = kq >> 1, bb = kq & 1;
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int ly = wave + 4 * h;
-                f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-                const float* bp = Xc + (ly + 1 - aa) * CX + (nl + 1 - bb);
-                const float* ap = Wd + lane;
-#pragma unroll 8
-                for (int o = 0; o < 64; ++o)
-                    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ap[o * 64], bp[o * NCELL], acc, 0, 0, 0);
-                // D lane: ci = 4kq + i, px = (ly, nl)
-                const int iy = Y0 / 4 + ly, ix = X0 / 4 + nl;
-                if (iy < a.Hi && ix < a.Wi) {
-                    const int64_t pix = (int64_t)iy * a.Wi + ix;
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const SinkRow& q = sk[4 * kq + i];
-                        if (q.mode != ISG_SINK_STORE && q.mode != ISG_SINK_ACCUM) continue;
-                        float* p = q.p + (int64_t)n * q.ns + pix;
-                        *p = q.mode == ISG_SINK_ACCUM ? *p + acc[i] : acc[i];
-                    }
-                }
-            }
-        }
-        // ---- convT weight gradient (MFMA): K = the 128 own input pixels, 4 per step;
-        //      A[ci][px] = input, B[px][(co, ky, kx)] = dI under tap (ky, kx) of px
-        {
-#pragma unroll 2
-            for (int st = 0; st < (TY / 4) * (TX / 4) / 4; ++st) {
-                const int P = st * 4 + kq;
-                const int ly = P >> 4, lx = P & 15;
-                const float av = Ts[nl][ly + 1][lx + 1];
-#pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    const int col = (wave * 4 + t) * 16 + nl;  // (co, ky, kx), kx fastest
-                    const int co = col >> 6, ky = (col >> 3) & 7, kx = col & 7;
-                    const float bv = Xc[((co * 4 + (ky & 3)) * 4 + (kx & 3)) * NCELL +
-                                        (ly + (ky >> 2)) * CX + lx + (kx >> 2)];
-                    dw1[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, dw1[t], 0, 0, 0);
-                }
-            }
-        }
-    }
-    // ---- fold the partial weight gradients into this workgroup's replica
-    const int rep = blockIdx.x % a.nrep;
-    if (a.dw1) {
-        double* d = a.dw1 + (int64_t)rep * a.rep_stride;
-        // D lane: ci = 4kq + i, column (co, ky, kx) = (wave * 4 + t) * 16 + nl
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                atomicAdd(&d[(4 * kq + i) * (kCm * 64) + (wave * 4 + t) * 16 + nl], dw1[t][i]);
-    }
-    float v[kCm];
-#pragma unroll
-    for (int co = 0; co < kCm; ++co) v[co] = wave_sum(db1[co]);
-    constexpr int NV = kCm * 9 + 1 + kCm;
-    __syncthreads();
-    if (lane == 0)
-#pragma unroll
-        for (int co = 0; co < kCm; ++co) red[co * 4 + wave] = v[co];
-    __syncthreads();
-    if (tid < NV) {
-        const int j = tid - (kCm * 9 + 1);
-        const float s = tid <= kCm * 9 ? acc2[tid]
-                                       : (red[j * 4] + red[j * 4 + 1]) + (red[j * 4 + 2] + red[j * 4 + 3]);
-        const int64_t ro = (int64_t)rep * a.rep_stride;
-        double* dst = nullptr;
-        if (tid < kCm * 9) dst = a.dw2 ? a.dw2 + ro + tid : nullptr;
-        else if (tid == kCm * 9) dst = a.db2 ? a.db2 + ro : nullptr;
-        else dst = a.db1 ? a.db1 + ro + (tid - kCm * 9 - 1) : nullptr;
-        if (dst) atomicAdd(dst, s);
-    }
-}
 
 // ---- backward, round 4 (head_bwd_kernel) ----------------------------------------------
 // Per 32 x 64 logit tile (8 x 16 own input pixels), on a persistent grid:
@@ -994,14 +793,7 @@ extern "C" int32_t isg_mask_head_bwd(const isg_mask_head* a, isg_stream_t st) {
     const int OH = 4 * a->Hi, OW = 4 * a->Wi;
     const int ntx = (OW + TX - 1) / TX, nty = (OH + TY - 1) / TY;
     const int ntiles = ntx * nty * a->N;
-    static const int env = getenv("ISG_HEAD_BWD_GRID") ? atoi(getenv("ISG_HEAD_BWD_GRID")) : 0;
-    const int grid_v1 = std::min(ntiles, env > 0 ? env : 512);  // v1: 2 workgroups per CU
-    const int grid = std::min((ntiles + 1) / 2, env > 0 ? env : 256);  // 1 two-tile workgroup per CU
-    static const bool v1 = getenv("ISG_HEAD_BWD_V1") && atoi(getenv("ISG_HEAD_BWD_V1"));
-    if (v1) {
-        hipLaunchKernelGGL(head_bwd_v1_kernel, dim3(grid_v1), dim3(kThreads), 0, st, *a, ntx, nty, ntiles);
-        return isg_check_launch("head_bwd_v1_kernel");
-    }
+    const int grid = std::min((ntiles + 1) / 2, 256);  // 1 two-tile workgroup per CU
     if (head_bwd_vec(a))
         hipLaunchKernelGGL(head_bwd_kernel<true>, dim3(grid), dim3(2 * kThreads), 0, st, *a, ntx, nty, ntiles);
     else

@@ -261,7 +261,6 @@ __global__ __launch_bounds__(kThreads) void pw_kernel(PwArgs a) {
             }
         }
     }
-    sinks_finalize(a.out);
 }
 
 // ---- pwx: whole-K slab kernel (the path every aligned layer takes) ----------------------
@@ -277,7 +276,7 @@ __global__ __launch_bounds__(kThreads) void pw_kernel(PwArgs a) {
 //     16g + 4kk + j, for A and B alike (a permutation of the reduction order only).
 // Bank layout: As row stride = 8 mod 64 floats (conflict-free b128 fragment reads), Xs row
 // stride = 16 mod 32 (conflict-free b32 B reads).
-constexpr int kPxMaxLds = 160 * 1024 - 256;  // + the static LDS of sinks_finalize
+constexpr int kPxMaxLds = 160 * 1024 - 256;
 
 struct PwxArgs {
     isg_vtensor src;
@@ -593,16 +592,12 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
             sink_row_flush(a.out, m0 + rl, red[0][0][rl], red[0][1][rl], red[0][2][rl]);
         }
     }
-    sinks_finalize(a.out);
     STAMP(7);
 }
 
 int pwx_align16(int v) { return (v + 15) & ~15; }
 
-int pwx_min_blocks() {
-    static const int v = getenv("ISG_PWX_MINB") ? atoi(getenv("ISG_PWX_MINB")) : 512;
-    return v;
-}
+constexpr int kPwxMinBlocks = 512;
 
 // LDS bytes of a (BP, BM) configuration
 int pwx_lds(int K, int Kp, int BM, int BP, int& off_k, int& off_ri, int& off_a, int& off_x, int& AS,
@@ -835,19 +830,14 @@ bool sinks_aligned16(const isg_sinks& sk) {
 // 1: launched, 0: not applicable, < 0: error
 int32_t thin_pw(const PwArgs& a, hipStream_t st) {
     static const bool off = getenv("ISG_NO_THIN_PW") != nullptr;
-    if (off || a.HW % 4 || a.out.fin_counter || !pwx_src_ok(a.src, a.HW) || !sinks_aligned16(a.out))
+    if (off || a.HW % 4 || !pwx_src_ok(a.src, a.HW) || !sinks_aligned16(a.out))
         return 0;
     ThinPwArgs b{};
     b.src = a.src; b.out = a.out; b.w = a.w; b.rs = a.rs; b.cs = a.cs; b.HW = a.HW;
     b.Q = a.P / 4;
-    // opt-in: M = 32, 48, 64 as 16-row tiles on grid.y (the input quads re-read from L2).
-    // Measured slower in the step (r02h: 374 -> 362 images/s; the 128^2 16 -> 48 layers
-    // stay on the MFMA kernels)
-    static const bool tile_on = getenv("ISG_THIN_PW_TILE") != nullptr;
-    const int mt = tile_on && a.M > 16 && a.M % 16 == 0 && a.M <= 64 ? 16 : a.M;
-    const dim3 grid((unsigned)((b.Q + 64 * kThinWaves - 1) / (64 * kThinWaves)), (unsigned)(a.M / mt));
+    const dim3 grid((unsigned)((b.Q + 64 * kThinWaves - 1) / (64 * kThinWaves)));
 #define ISG_THIN_PW(KK, MM)                                                          \
-    if (a.K == KK && mt == MM) {                                                     \
+    if (a.K == KK && a.M == MM) {                                                     \
         hipLaunchKernelGGL((thin_pw_kernel<KK, MM>), grid, dim3(64 * kThinWaves), 0, st, b); \
         const int32_t e = isg_check_launch("thin_pw_kernel");                        \
         return e ? e : 1;                                                            \
@@ -897,14 +887,13 @@ int32_t isg_pw_gemm(const isg_conv_geom* g, const isg_vtensor* src, const float*
     // expansions' dgrads 17.1 -> 14.9 us, >= 512 workgroups); elsewhere its longer
     // per-workgroup phase chain loses to the chunked kernel (the 128 -> 48 dgrads
     // 12.2 -> 17.0 us, the 256 -> 128 resconv forward 27.6 -> 49.5 us)
-    static const bool slab_all = getenv("ISG_PW_SLAB_ALL") != nullptr;
     // (r02g per-op tables: the 64^2 128 -> 48 forwards 13.8 -> 12.5 us on the slab)
     static const bool fwd_small = getenv("ISG_NO_PW_FWD_SLAB_SMALL") == nullptr;
     // (round 3, after the single-segment prologue: the 48 -> 128 expansions and their
     // transposes, M = 128 rows over K = 48, on 32 x 64 tiles — kbench fwd 15.3 -> 14.8 us,
     // dgrad 18.4 -> 17.2 us against the chunked kernel)
     static const bool wide_rows = getenv("ISG_NO_PWX_WIDE_ROWS") == nullptr;
-    const bool slab_pays = slab_all || (!dgrad && a.P >= 65536) || (dgrad && a.M <= 64 && a.K <= 128) ||
+    const bool slab_pays = (!dgrad && a.P >= 65536) || (dgrad && a.M <= 64 && a.K <= 128) ||
                            (fwd_small && !dgrad && a.M <= 64 && a.K <= 128) ||
                            (wide_rows && a.M <= 128 && a.K <= 64);
     if (!slab_off && slab_pays && wmode && pwx_src_ok(*src, a.HW) && a.P < ((int64_t)1 << 31)) {
@@ -941,8 +930,6 @@ int32_t isg_pw_gemm(const isg_conv_geom* g, const isg_vtensor* src, const float*
         int best_bp = 0, best_bm = 0, best_lds = 0;
         int64_t best_blocks = -1;
         bool done = false;
-        static const int env_bm = getenv("ISG_PWX_BM") ? atoi(getenv("ISG_PWX_BM")) : 0;
-        static const int env_bp = getenv("ISG_PWX_BP") ? atoi(getenv("ISG_PWX_BP")) : 0;
         // more than 64 rows: the widest pixel tile first (fewer weight re-reads per pixel,
         // kbench (32, 64) beat (128, 16) on M = 128), else the most rows first
         const bool bp_first = a.M > 64;
@@ -950,9 +937,7 @@ int32_t isg_pw_gemm(const isg_conv_geom* g, const isg_vtensor* src, const float*
             const int bm = bp_first ? std::min(R, 8) * 16 - 16 * (it % 8) : std::min(R, 8) * 16 - 16 * (it / 3);
             const int bp = bp_first ? (64 >> (it / 8)) : (64 >> (it % 3));
             if (bm < 16) continue;
-            if (env_bm && bm != env_bm) continue;
             {
-                if (env_bp && bp != env_bp) continue;
                 const int wq = pwx_wrow_quads(wmode, bm, b.Kp) * (wmode == 1 ? bm : b.Kp);
                 if ((bm / 16) * (bp / 16) < 4 || wq > 8 * kThreads) continue;
                 if (b.Kp > 8 * (kThreads / (bp / 4))) continue;
@@ -963,7 +948,7 @@ int32_t isg_pw_gemm(const isg_conv_geom* g, const isg_vtensor* src, const float*
                 if (blocks > best_blocks) {
                     best_bp = bp; best_bm = bm; best_lds = lds; best_blocks = blocks;
                 }
-                if (blocks >= pwx_min_blocks()) { done = true; break; }
+                if (blocks >= kPwxMinBlocks) { done = true; break; }
             }
         }
         if (best_bp) {
@@ -984,7 +969,6 @@ int32_t isg_pw_gemm(const isg_conv_geom* g, const isg_vtensor* src, const float*
                                             : pwx_dispatch_seg<32, false>(b, grid, best_lds, tpw, seg1, st);
             else rc = hy ? pwx_dispatch_seg<16, true>(b, grid, best_lds, tpw, seg1, st)
                          : pwx_dispatch_seg<16, false>(b, grid, best_lds, tpw, seg1, st);
-            if (rc == 0 && out->fin_counter) isg_fin_note_handled();
             return rc;
         }
     }
@@ -1004,6 +988,5 @@ int32_t isg_pw_gemm(const isg_conv_geom* g, const isg_vtensor* src, const float*
         case 5: case 6: hipLaunchKernelGGL(pw_kernel<6>, grid, dim3(kThreads), 0, st, a); break;
         default: hipLaunchKernelGGL(pw_kernel<8>, grid, dim3(kThreads), 0, st, a); break;
     }
-    if (out->fin_counter) isg_fin_note_handled();
     return isg_check_launch("pw_kernel");
 }

@@ -56,7 +56,10 @@ ISG_DEV ChSrc ch_src(const VtLite& l, int c, int hw) {
         cl = c;
     }
     r.p += (int64_t)cl * hw;
-    r.y = (r.xf == ISG_XF_BN_BWD && y) ? y + (int64_t)cl * hw : r.p;
+    // no separate y: y is the input itself, with the input's image stride
+    const bool hy = r.xf == ISG_XF_BN_BWD && y;
+    r.y = hy ? y + (int64_t)cl * hw : r.p;
+    r.yns = hy ? r.yns : r.ns;
     return r;
 }
 
@@ -455,7 +458,9 @@ ISG_DEV ChSrc ch_addr(const VtSel vt, int c, int64_t hw) {
     r.xf = ISG_SEL3(s, xf, vt);
     r.act = ISG_SEL3(s, act, vt);
     const float* y = ISG_SEL3(s, y, vt);
-    r.y = (r.xf == ISG_XF_BN_BWD && y) ? y + (int64_t)cl * hw : r.p;
+    const bool hy = r.xf == ISG_XF_BN_BWD && y;
+    r.y = hy ? y + (int64_t)cl * hw : r.p;
+    r.yns = hy ? r.yns : r.ns;
     return r;
 }
 

@@ -390,7 +390,6 @@ __global__ __launch_bounds__(kThreads) void tap_conv_kernel(TapArgs a) {
             sink_row_flush(a.out, row, r3[0], r3[1], r3[2]);
         }
     }
-    sinks_finalize(a.out);
 }
 
 template <int MT, int G, bool YB, bool PAIR>
@@ -410,7 +409,6 @@ int32_t tap_launch(const TapArgs& a, size_t lds, hipStream_t st) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k, kThreads, lds) != hipSuccess || occ < 1) occ = 1;
     const int grid = std::max(1, std::min(a.ntiles, occ * cus));
     hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(kThreads), lds, st, a);
-    if (a.out.fin_counter) isg_fin_note_handled();
     return isg_check_launch("tap_conv_kernel");
 }
 
@@ -548,11 +546,6 @@ int32_t isg_tap_conv(const isg_conv_geom* g, const isg_vtensor* src, const float
     for (int i = 0; i < src->nseg; ++i) yb |= src->s[i].xform == ISG_XF_BN_BWD;
     const size_t lds = (size_t)(a.ws_floats + 4 * a.CHS) * sizeof(float);
     const bool pair = mx == 2;
-    static const bool log = getenv("ISG_TAP_LOG") != nullptr;  // debugging
-    if (log)
-        fprintf(stderr, "tap_conv %s C%d M%d %dx%d k%dx%d s%d: BX%d BY%d G%d HR%d HCu%d CHS%d tiles%d ph%d yb%d\n",
-                dgrad ? "dgrad" : "fwd", a.C, a.M, a.SrcH, a.SrcW, g->KH, g->KW, g->SH, BX, BY, G, a.HR,
-                a.HCu, a.CHS, a.ntiles, a.nph, (int)yb);
     int32_t e;
     if (mt == 1) e = tap_launch_g<1>(a, lds, G, yb, pair, st);
     else if (mt == 2) e = tap_launch_g<2>(a, lds, G, yb, pair, st);

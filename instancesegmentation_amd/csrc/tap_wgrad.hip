@@ -51,7 +51,6 @@ struct TwArgs {
     // reads the slot-0 tap's address, result discarded). Taps are grouped so that the 32
     // lanes of a ds_read_b32 group hit 32 distinct banks (host: tw_layout).
     int8_t gtap[8][4];
-    int dbg;  // ablation bits (ISG_TW_DBG, experiments only): 1 no MFMA loop, 2 no loads
 };
 
 template <int NT, bool YB, bool PAIR>
@@ -190,15 +189,15 @@ __global__ __launch_bounds__(kThreads) void tap_wgrad_kernel(TwArgs a) {
     float bsum = 0.f;  // dbias partial: sum of this lane's dy values (row co = pl)
 
     int tile = blockIdx.x;
-    if (tile < a.ntiles && !(a.dbg & 2)) load_tile(tile);
-    const int nstep = (a.dbg & 1) ? 0 : a.BX >> 2;
+    if (tile < a.ntiles) load_tile(tile);
+    const int nstep = a.BX >> 2;
     const int xrow = wave * a.SH * a.RS;  // halo row of this wave's tile row
     while (tile < a.ntiles) {
         __syncthreads();  // LDS free
         store_tile();
         __syncthreads();
         const int ntile = tile + gridDim.x;
-        if (ntile < a.ntiles && !(a.dbg & 2)) load_tile(ntile);
+        if (ntile < a.ntiles) load_tile(ntile);
         for (int s = 0; s < nstep; ++s) {
             const float av = Ds[aoff + 4 * s];
             bsum += av;
@@ -387,7 +386,6 @@ struct TwaArgs {
     int BX, tiles_x, tiles_y, ntiles;
     int HR, HRP, HCu, PS, RS, CHS, DQ, KPW;
     uint32_t m_tpi, m_tx, m_4bx, m_bx, m_hrp;
-    int dbg;  // ablation bits (ISG_TW_DBG): 1 no MFMA loop, 2 no global loads, 4 no LDS stores, 8 no dW atomics
     // tile t, lane pl: column id ci*KK + tap, or -1 - (a column id to read) for padding
     int16_t col[kTwaTiles][16];
 };
@@ -511,14 +509,14 @@ __global__ __launch_bounds__(kThreads, 2) void tap_wgrad_all_kernel(TwaArgs a) {
     float bsum = 0.f;  // dbias partial (wave 0): sum of this lane's dy values (row co = pl)
 
     int tile = blockIdx.x;
-    if (tile < a.ntiles && !(a.dbg & 2)) load_tile(tile);
-    const int nstep = (a.dbg & 1) ? 0 : a.BX >> 2;
+    if (tile < a.ntiles) load_tile(tile);
+    const int nstep = a.BX >> 2;
     while (tile < a.ntiles) {
         __syncthreads();  // LDS free
-        if (!(a.dbg & 4)) store_tile();
+        store_tile();
         __syncthreads();
         const int ntile = tile + gridDim.x;
-        if (ntile < a.ntiles && !(a.dbg & 2)) load_tile(ntile);
+        if (ntile < a.ntiles) load_tile(ntile);
         // kBY rows x nstep pixel quads, software-pipelined: the next quad's dy and halo
         // operands are read from LDS while this quad's MFMAs run
         const int nq = kBY * nstep;
@@ -553,7 +551,7 @@ __global__ __launch_bounds__(kThreads, 2) void tap_wgrad_all_kernel(TwaArgs a) {
     double* const dwr = a.dw + (int64_t)(blockIdx.x % a.nrep) * a.rep_stride;
 #pragma unroll
     for (int t = 0; t < NTW; ++t) {
-        if (!cval[t] || (a.dbg & 8)) continue;
+        if (!cval[t]) continue;
         const int c = a.col[wave * NTW + t][pl];
         const int ci = c / a.KK, tap = c - ci * a.KK;
 #pragma unroll
@@ -674,8 +672,7 @@ int32_t twa_try(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor
     const int KK = g->KH * g->KW;
     // measured (kbench): the stem layer1 (20 x 25 columns) 433 -> 308 us; the 16-channel
     // layer2 (400 columns, a 4x smaller map) is faster on the chunked kernel (71 vs ~100 us)
-    static const bool force = getenv("ISG_TWA_FORCE") != nullptr;
-    if (g->Ci * KK > 16 * kTwaTiles || (g->Ci * KK < 448 && !force)) return 0;
+    if (g->Ci * KK > 16 * kTwaTiles || g->Ci * KK < 448) return 0;
     TwaArgs a{};
     a.N = g->N; a.C = g->Ci; a.Co = g->Co; a.H = g->H; a.W = g->W; a.OH = g->OH; a.OW = g->OW;
     a.WC = g->w_ci > 0 ? g->w_ci : g->Ci;
@@ -732,8 +729,6 @@ int32_t twa_try(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor
     a.m_4bx = magic(4 * a.BX);
     a.m_bx = magic(a.BX);
     a.m_hrp = (uint32_t)(((1ull << 32) + a.HRP - 1) / a.HRP);  // k < 4*kTwaMaxPW: exact
-    static const int dbg = getenv("ISG_TW_DBG") ? atoi(getenv("ISG_TW_DBG")) : 0;
-    a.dbg = dbg;
     a.dy = *dy; a.x = *x; a.dw = dw; a.dbias = dbias;
     a.rep_stride = nrep > 1 ? rep_stride : 0;
     a.nrep = nrep < 1 ? 1 : nrep;
@@ -769,8 +764,6 @@ int32_t isg_tap_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_v
         if (x->s[i].xform == ISG_XF_BN_BWD) return 0;  // the gathered side never needs y
     if ((int64_t)g->H * g->W * 4 >= (1ll << 31) || (int64_t)g->OH * g->OW * 4 >= (1ll << 31)) return 0;
     TwArgs a{};
-    static const int dbg = getenv("ISG_TW_DBG") ? atoi(getenv("ISG_TW_DBG")) : 0;
-    a.dbg = dbg;
     a.dy = *dy; a.x = *x; a.dw = dw; a.dbias = dbias;
     a.rep_stride = nrep > 1 ? rep_stride : 0;
     a.nrep = nrep < 1 ? 1 : nrep;

@@ -504,7 +504,7 @@ __global__ __launch_bounds__(kThreads) void pwg_kernel(PwgArgs a) {
 
 // Up to kPwgGroup problems of one instantiation in one launch (the executor's side-stream
 // batches, api.cpp): measured, every side-stream node costs the step ~3 us even when it
-// does no work (ISG_DBG_NOP_WGRAD: 4.02 ms, 3.62 with the weight gradients as empty
+// does no work (a since-removed timing switch: 4.02 ms, 3.62 with the weight gradients as empty
 // launches, 3.35 with no launches), so the 1x1 weight gradients of a batch go out grouped.
 constexpr int kPwgGroup = 3;
 struct PwgGroupMeta {
@@ -595,7 +595,6 @@ struct PwkArgs {
     int nrep;
     int HW, R, C, ncb;
     int fast, stat_on;  // fast: always 1 here (pwk_try)
-    int dbg;            // experiments (ISG_DBG): 1 no slab loads, 2 no coefficient loads, 4 no MFMA
     int64_t P, ntiles, tiles_per_block;
 };
 
@@ -701,7 +700,6 @@ __global__ __launch_bounds__(kThreads) void pwk_kernel(PwkArgs a) {
 #pragma unroll
         for (int u = 0; u < NU; ++u) {
             const ChSrc& t = tabA[wave + 4 * u];
-            if (a.dbg & 1) { v[u] = f32x4{0.f, 0.f, 0.f, 0.f}; continue; }
             v[u] = gld4(t.p, (int64_t)n * t.ns + pix);
             if constexpr (HY)
                 if (u < NUY) yv[u < NUY ? u : 0] = gld4(t.y, (int64_t)n * t.yns + pix);
@@ -715,7 +713,7 @@ __global__ __launch_bounds__(kThreads) void pwk_kernel(PwkArgs a) {
         const ChSrc& e = tabA[ju];
         const int xf = e.xf, act = e.act;
         // finalised coefficients or training-mode statistics only (host check: a.fast)
-        ChanCoef k = (a.dbg & 2) ? ChanCoef{0.f, 1.f, 0.f, 0.f} : pwk_row_coef(vd, cdy, vx, cx, is_dy, a.stat_on != 0);
+        ChanCoef k = pwk_row_coef(vd, cdy, vx, cx, is_dy, a.stat_on != 0);
         if (xf == ISG_XF_PLAIN) k = ChanCoef{0.f, 1.f, 0.f, 0.f};
         tabK[ju] = k;
         const float neg = (xf != ISG_XF_BN_FWD || act == ISG_ACT_NONE) ? 1.f : act == ISG_ACT_RELU ? 0.f : k.c3;
@@ -760,7 +758,7 @@ __global__ __launch_bounds__(kThreads) void pwk_kernel(PwkArgs a) {
         if (tl == t0) STAMP(2);
         if (tl + 1 < t1) issue(tl + 1);  // under this super-tile's MFMAs
 #pragma unroll
-        for (int g = 0; g < ((a.dbg & 4) ? 0 : 64); g += 16) {
+        for (int g = 0; g < 64; g += 16) {
             f32x4 a4[RT], b4[CT];
 #pragma unroll
             for (int r = 0; r < RT; ++r) a4[r] = *reinterpret_cast<const f32x4*>(&S[(16 * r + pl) * kKS + kb + g]);
@@ -820,11 +818,10 @@ int32_t pwk_try(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor
     // workgroups leave them free — on the side streams a thin kernel beats a fast one
     const char* pe = getenv("ISG_PWK");  // read per call: the parity test runs both paths
     const int env = pe ? atoi(pe) : 0;
-    static const int max_rc = getenv("ISG_PWK_MAXRC") ? atoi(getenv("ISG_PWK_MAXRC")) : 65536;
     if (!env) return 0;
     const int HW = g->H * g->W;
     const int64_t P = (int64_t)g->N * HW;
-    if ((int64_t)g->Co * g->Ci > max_rc) return 0;
+    if ((int64_t)g->Co * g->Ci > 65536) return 0;
     for (int i = 0; i < x->nseg; ++i)  // the x rows' transform is loaded as BN_FWD / plain only
         if (x->s[i].xform == ISG_XF_BN_BWD) return 0;
     PwkArgs a{};
@@ -839,7 +836,6 @@ int32_t pwk_try(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor
             if ((q.xform == ISG_XF_BN_FWD || q.xform == ISG_XF_BN_BWD) && !q.bn.coef && q.bn.stats) a.stat_on = 1;
         }
     const bool hy = pwg_has_y(*dy);
-    { const char* e = getenv("ISG_DBG"); a.dbg = e ? atoi(e) : 0; }
     // block shape: the fewest slab rows loaded per super-tile over the whole dW
     static const int shapes[6][2] = {{1, 3}, {3, 1}, {2, 2}, {1, 2}, {2, 1}, {1, 1}};
     int best = -1;
@@ -849,14 +845,11 @@ int32_t pwk_try(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor
         const int64_t rows = (int64_t)((a.R + br - 1) / br) * ((a.C + bc - 1) / bc) * (br + bc);
         if (best < 0 || rows < best_rows) { best = i; best_rows = rows; }
     }
-    static const int env_shape = getenv("ISG_PWK_SHAPE") ? atoi(getenv("ISG_PWK_SHAPE")) : -1;
-    if (env_shape >= 0 && env_shape < 6) best = env_shape;
     const int RT = shapes[best][0], CT = shapes[best][1];
     a.ncb = (a.C + 16 * CT - 1) / (16 * CT);
     const int64_t gy = (int64_t)((a.R + 16 * RT - 1) / (16 * RT)) * a.ncb;
     a.ntiles = (P + kKTP - 1) / kKTP;
-    static const int env_wgs = getenv("ISG_PWK_WGS") ? atoi(getenv("ISG_PWK_WGS")) : 384;
-    a.tiles_per_block = std::max<int64_t>(1, (gy * a.ntiles) / env_wgs);
+    a.tiles_per_block = std::max<int64_t>(1, (gy * a.ntiles) / 384);
     const int64_t gx = (a.ntiles + a.tiles_per_block - 1) / a.tiles_per_block;
     if (gy > 65535) return 0;
     const dim3 grid((unsigned)gx, (unsigned)gy);
@@ -913,23 +906,16 @@ bool pwg_plan(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* 
     };
     // narrower column blocks while the grid would not cover the CUs
     while (bc > 32 && a.ntiles * gy_of(bc) < 256) bc = (bc / 2 + 15) / 16 * 16;
-    // experiments (tools/kbench): block shape overrides
-    static const int env_br = getenv("ISG_PWG_BR") ? atoi(getenv("ISG_PWG_BR")) : 0;
-    static const int env_bc = getenv("ISG_PWG_BC") ? atoi(getenv("ISG_PWG_BC")) : 0;
-    if (env_br >= 16 && env_br % 16 == 0 && env_br <= 64) br = std::min(env_br, (a.R + 15) / 16 * 16);
-    if (env_bc >= 16 && env_bc % 16 == 0) bc = std::min(std::min(env_bc, kGMaxRows - br), (a.C + 15) / 16 * 16);
     a.BR = br; a.BC = bc;
     a.ncb = (a.C + bc - 1) / bc;
     const int64_t gy = gy_of(bc);
-    static const int env_wgs = getenv("ISG_PWG_WGS") ? atoi(getenv("ISG_PWG_WGS")) : 512;
-    int64_t gx = std::max<int64_t>(1, env_wgs / gy);
+    int64_t gx = std::max<int64_t>(1, 512 / gy);
     if (gx > a.ntiles) gx = a.ntiles;
     a.tiles_per_block = (a.ntiles + gx - 1) / gx;
     // at least 2 tiles per workgroup: half the dW atomics, and — these kernels run on the
     // executor's side stream — half the workgroups competing with the input-gradient
     // chain (measured: 5.55 -> 5.43 ms/step; the 256->128 resconv wgrads 41 -> 35 us)
-    static const int env_tpb = getenv("ISG_PWG_TPB") ? atoi(getenv("ISG_PWG_TPB")) : 2;
-    if (env_tpb > a.tiles_per_block) a.tiles_per_block = env_tpb;
+    if (a.tiles_per_block < 2) a.tiles_per_block = 2;
     gx = (a.ntiles + a.tiles_per_block - 1) / a.tiles_per_block;
     if (gx * gy >= (1ll << 31)) return false;
     a.off_k = (kThreads * (int)sizeof(ChSrc) + 15) & ~15;

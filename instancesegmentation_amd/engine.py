@@ -369,11 +369,7 @@ class Graph:
         # finalised coefficients (isg_bn.coef): 8*C floats = 4*C doubles, 64-B aligned
         ref.coef_off = self.stats_size
         self.stats_size += (4 * bn.num_features + 7) // 8 * 8
-        # tickets of the fused finalisation (isg_sinks.fin_counter: 33 uint32 each),
-        # forward and backward, inside the forward's stats memset
-        ref.ctr_fwd = self.stats_size
-        ref.ctr_bwd = self.stats_size + 24
-        self.stats_size += 48
+        ref.coef_end = self.stats_size
         self.bns.append(ref)
         self.bn_by_mod[id(bn)] = ref
         return ref
@@ -587,17 +583,6 @@ _BN_FINAL = os.environ.get("ISG_BN_FINAL", "0") == "1"
 # one-wave workgroups whose statistics atomics and reads piled on the same lines; after its
 # four-wave form all-consumer-side measured 4.39 vs 4.41 ms/step, profiles/r03u_ab.txt.)
 _BN_FINAL_COUNT = int(os.environ.get("ISG_BN_FINAL_COUNT", str(1 << 62)))
-# finalise BN coefficients in the producing kernel's last workgroup (isg_sink.fin_*)
-# instead of a separate OP_BN_FINAL launch. Withdrawn in round 4: measured slower (5.43 vs
-# 5.17 ms/step fence-free, round 3; 7.16 vs 6.5 with a release fence) and, with the
-# memory-model fences in fin_last_block, still 1.4e-3 (relative to scale) from the default
-# plan's gradients on the 2x128^2 fixture, deterministically across replays — a plan-level
-# ordering fault (a BatchNorm finalised before all of its statistics are in), not a race.
-# The kernels keep the mechanism; ISG_BN_FUSE=1 is refused until that is found.
-if _BN_FINAL and os.environ.get("ISG_BN_FUSE", "0") == "1":
-    raise RuntimeError("ISG_BN_FUSE is withdrawn (engine.py: its gradients differ from the "
-                       "default plan's); use ISG_BN_FINAL=1 alone for finalisation launches")
-_BN_FUSE = False
 
 
 def _buf_range(buf):
@@ -683,17 +668,8 @@ def _fork_late_wgrads(recs, late):
 
 
 def sinks_spec(sinks):
-    """isg_sinks spec from sink specs; a sink's private '_fin_ctr' (the ticket of a fused
-    BN finalisation) becomes the launch's fin_counter."""
-    ctr = None
-    for sk in sinks:
-        c = sk.pop("_fin_ctr", None)
-        if c is not None and ctr is None:
-            ctr = c
-    out = {"s": sinks, "nsink": len(sinks)}
-    if ctr is not None:
-        out["fin_counter"] = ctr
-    return out
+    """isg_sinks spec from sink specs."""
+    return {"s": sinks, "nsink": len(sinks)}
 
 
 def bn_spec(bnr, train, coef=True):
@@ -781,13 +757,8 @@ class GradState:
                 s["slope"] = Ptr(val.slope.slot)
                 s["slope_grad"] = Ptr(S_STATS, val.slope.acc_off * 8)
                 val.slope.used_in_bwd = True
-            if val.bn is not None:
-                if train and _BN_FUSE:
-                    s["fin_bn"] = s["bn"]
-                    s["fin_mode"] = 2
-                    s["_fin_ctr"] = Ptr(S_STATS, val.bn.ctr_bwd * 8)
-                elif val.bn.fin:
-                    self.pending_final.append(val.bn)
+            if val.bn is not None and val.bn.fin:
+                self.pending_final.append(val.bn)
             return s
         d = self.dbuf(val.buf)
         first = self.mark(val.buf, val.c0, val.C)
@@ -849,14 +820,8 @@ class ConvOp:
                 "mode": L.SINK_STORE}
         if self.mod.bias is not None:
             sink["bias"] = g.tptr(self.mod, "bias")
-        self.fused_final = False
         if self.bnr is not None and g.train:
             sink["stats"] = Ptr(S_STATS, self.bnr.stats_off * 8)
-            if _BN_FUSE and self.kp is None:  # the keypoint stem finishes the statistics
-                sink["fin_bn"] = bn_spec(self.bnr, True)
-                sink["fin_mode"] = 1
-                sink["_fin_ctr"] = Ptr(S_STATS, self.bnr.ctr_fwd * 8)
-                self.fused_final = True
         ge = self.geom
         rec = {"g": ge, "a": vtensor(segs, g.N, ge["H"], ge["W"]), "w": g.tptr(self.mod, "weight"),
                "out": sinks_spec([sink])}
@@ -1054,8 +1019,8 @@ class HeadOp:
             s["db2"] = g.wrep_ptr(self.conv, "bias")
         fl, nb = self._cost()
         # algorithmic: input gradient + both weight gradients = 2x the forward (SURVEY
-        # §8d). The kernel also recomputes the intermediate (another 1x the forward) —
-        # implementation overhead, not counted as work in the roofline.
+        # §8d). The kernel does not recompute the 4-channel intermediate: the 3x3's weight
+        # gradient comes from W1·Z' plus the forward's border ring (isg.h ISG_HEAD_RING).
         ops.add(Record(L.OP_HEAD_BWD, L.MaskHead, s, label="d_" + self.out.name,
                        flops=2 * fl, nbytes=nb + 4 * 16 * g.N * self.x.H * self.x.W))
 
@@ -1218,12 +1183,12 @@ class Plan:
             op.fwd(fw)
             bnr = getattr(op, "bnr", None)
             for b in getattr(op, "bnrs", [bnr]):
-                if train and b is not None and b.fin and not getattr(op, "fused_final", False):
+                if train and b is not None and b.fin:
                     fw.add(bn_final_record([b], False))
             if getattr(op, "side", False):
                 rng = [_buf_range(op.out)]
                 if bnr is not None:
-                    rng.append((S_STATS, bnr.stats_off * 8, (bnr.ctr_fwd + 48) * 8))
+                    rng.append((S_STATS, bnr.stats_off * 8, bnr.coef_end * 8))
                 side_recs += [(r, rng) for r in fw.recs[i0:]]
         if train and g.bns:
             items = []
@@ -1280,7 +1245,7 @@ class Plan:
             if not g.mod_names[id(b.mod)].startswith(late):
                 n = (4 * b.C * L.STAT_REP + 7) // 8 * 8
                 early_stats.append((b.stats_off * 8, (b.stats_off + n) * 8))
-                early_stats.append((b.coef_off * 8, (b.ctr_bwd + 24) * 8))
+                early_stats.append((b.coef_off * 8, b.coef_end * 8))
         for sl in g.slopes.values():
             if not g.mod_names[id(sl.mod)].startswith(late):
                 early_stats.append((sl.acc_off * 8, (sl.acc_off + sl.C * L.STAT_REP) * 8))

@@ -377,6 +377,37 @@ def test_pw_wgrad_bn_bwd(cfg, xmode, pwk, monkeypatch):
     assert torch.all(OUT[nw + Co:] == 0)
 
 
+@pytest.mark.parametrize("cfg", [(48, 128, 16, 16), (128, 48, 12, 20)])
+def test_pw_bn_bwd_y_null(cfg):
+    """a BatchNorm-backward segment with y = NULL (and y_n_stride = 0) means
+    y = the segment's own input, at the input's image stride (isg.h isg_vseg). N = 2, so a
+    y addressed with the zero stride would read image 0 for image 1. Through the 1x1 input
+    gradient (pw_gemm.hip) and the 1x1 weight gradient (wgrad.hip), against fp64."""
+    Ci, Co, H, W = cfg
+    N = 2
+    ge, OH, OW = _geom(N, Ci, Co, H, W, 1, 1, 0, 1)
+    # g is also y: dy = gamma*rstd*(y - mean)*eps/(var + eps), so a spread near sqrt(eps)
+    # keeps dy O(g) instead of a 1e-5 cancellation residue
+    g = rnd(N, Co, H, W, seed=61, scale=0.003) + 0.2
+    gamma, beta, st, _ = _bn_train_state(g, g, 62)
+    dy = _bn_bwd_ref(g, g, gamma)
+    w = rnd(Co, Ci, 1, 1, seed=63, scale=0.3)
+    x = rnd(N, Ci, H, W, seed=64)
+    Gb, GA, BE, ST = cuda32(g), cuda32(gamma), cuda32(beta), rep_from(st)
+    dyseg = {"p": ptr(Gb), "y": 0, "n_stride": Co * H * W, "y_n_stride": 0,
+             "C": Co, "xform": L.XF_BN_BWD, "bn": bn_spec_train(GA, BE, ST, N * H * W)}
+    DX = torch.full((N, Ci, H, W), float("nan"), device=DEV)
+    sk = sinks([{"p": ptr(DX), "n_stride": Ci * H * W, "c0": 0, "C": Ci, "mode": L.SINK_STORE}])
+    call("isg_conv_dgrad", geom(**ge), vt([dyseg], N, H, W), ptr(cuda32(w)), sk, stream())
+    close(DX, torch.nn.grad.conv2d_input((N, Ci, H, W), w, dy), what="1x1 dgrad (y NULL)")
+    X = cuda32(x)
+    xseg = {"p": ptr(X), "n_stride": Ci * H * W, "C": Ci, "xform": L.XF_PLAIN}
+    DW = torch.zeros(Co, Ci, 1, 1, dtype=torch.float64, device=DEV)
+    call("isg_conv_wgrad", geom(**ge), vt([dyseg], N, H, W), vt([xseg], N, H, W), ptr(DW), 0,
+         stream())
+    close(DW.float(), torch.nn.grad.conv2d_weight(x, (Co, Ci, 1, 1), dy), what="1x1 wgrad (y NULL)")
+
+
 @pytest.mark.parametrize("cfg", [DENSE[0], DENSE[1], DENSE[4], (16, 16, 24, 40, 3, 1, 1, 0)])
 def test_conv_wgrad_replicated(cfg):
     """isg_conv_wgrad_rep adds into L.WREP replicas (the train plan's layout); folding them

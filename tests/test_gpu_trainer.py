@@ -292,7 +292,7 @@ def test_bn_final_launches_match_default(monkeypatch):
     OP_BN_FINAL per layer turns the statistics into coefficients) must give the gradients of
     the default plan (coefficients evaluated by the consumers). Three replays each. (The
     fused form, finalised by the producer's last workgroup, failed this check in round 4 —
-    1.4e-3 of scale, deterministic — and is withdrawn, engine.py _BN_FUSE.)"""
+    1.4e-3 of scale, deterministic — and was removed in round 5.)"""
     from instancesegmentation_amd import engine
     fx = SegmentFixture("segment20_n2_128.npz")
     xs, y = _inputs(fx.x), torch.from_numpy(fx.mask).to(DEV)
