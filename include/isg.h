@@ -79,11 +79,15 @@ typedef struct {
 /* A channel segment of a virtual tensor.
  *   PLAIN : v = p
  *   BN_FWD: v = act((p - mean) * gamma*rstd + beta)            (Conv.forward, segment.py:44-45)
+ *           with y non-NULL (a residual block's tail read by its consumer):
+ *           v = act((p - mean) * gamma*rstd + beta + y)        (segment.py:75-77: out += residual;
+ *           prelu) — accepted only by the 1x1 stride-1 conv forward, one segment
  *   BN_BWD: v = dL/d(conv output) rebuilt from g (= dL/d BN-output) and the forward
  *           raw y: A*g + B*(y - mean) + C                       (BatchNorm2d backward) */
 typedef struct {
     const float* p;
-    const float* y;        /* BN_BWD only; NULL: y = p (with p's n_stride) */
+    const float* y;        /* BN_BWD: saved raw output (NULL: y = p, with p's n_stride);
+                              BN_FWD: residual term or NULL */
     int64_t n_stride;      /* elements between images of p */
     int64_t y_n_stride;
     int32_t C;
@@ -98,13 +102,23 @@ typedef struct {
     isg_vseg s[ISG_MAX_SEGS];
     int32_t nseg;
     int32_t N, H, W;       /* C = sum of segment channels */
+    /* non-NULL: the consumer also writes the transformed values v here ([N][C][H][W] at
+     * mat_n_stride per image) — the materialised block output a residual tail would have
+     * written; 1x1 stride-1 conv forward with one segment only */
+    float* mat;
+    int64_t mat_n_stride;
 } isg_vtensor;
 
 /* Where a kernel writes channels [c0, c0+C) of its result.
  *   STORE : p = v + bias; optional BN sum/sumsq into stats   (forward conv outputs)
  *   ACCUM : p += v                                            (gradient of a consumed tensor)
  *   ACTBWD: v is dL/dz for z = act(BN(y)); writes g = v*act'(BN(y)) into p and
- *           accumulates bn.stats gsum/gxsum and the PReLU slope gradient. */
+ *           accumulates bn.stats gsum/gxsum and the PReLU slope gradient.
+ *           Residual form (r non-NULL; a block tail's backward folded into the input
+ *           gradient of the next block's first 1x1, segment.py:75-77): v' = v + old,
+ *           z = BN(y) + r, g = v'*act'(z) into p and, when p2 is non-NULL, also into p2
+ *           (the residual term's gradient, STORE); statistics as ACTBWD with v'. Accepted
+ *           only by the 1x1 stride-1 input gradient with one sink. */
 typedef struct {
     float* p;
     int64_t n_stride;
@@ -119,6 +133,12 @@ typedef struct {
     const float* slope;    /* ACTBWD + PRELU */
     double* slope_grad;    /* ACTBWD + PRELU, C doubles per replica */
     isg_bn bn;             /* ACTBWD; bn.stats==NULL means "no BN" (identity) */
+    const float* r;        /* ACTBWD residual form: the tail's residual term, or NULL */
+    int64_t r_n_stride;
+    const float* old;      /* ACTBWD residual form: gradient already accumulated for v, or NULL */
+    int64_t old_n_stride;
+    float* p2;             /* ACTBWD residual form: second output of g, or NULL */
+    int64_t p2_n_stride;
 } isg_sink;
 
 typedef struct {

@@ -20,7 +20,7 @@ SINK_STORE, SINK_ACCUM, SINK_ACTBWD, SINK_NONE = 0, 1, 2, 3
 MAX_SEGS = 3
 LIST_CHUNK = 32
 STAT_REP = int(os.environ.get("ISG_STAT_REP", "4"))  # accumulator replicas (isg.h ISG_STAT_REP)
-ABI_VERSION = 9
+ABI_VERSION = 10
 WREP = int(os.environ.get("ISG_WREP", "16"))  # weight-gradient replicas (isg.h ISG_WREP)
 
 
@@ -38,14 +38,16 @@ class VSeg(Structure):
 
 class VTensor(Structure):
     _fields_ = [("s", VSeg * MAX_SEGS), ("nseg", c_int32), ("N", c_int32), ("H", c_int32),
-                ("W", c_int32)]
+                ("W", c_int32), ("mat", c_void_p), ("mat_n_stride", c_int64)]
 
 
 class Sink(Structure):
     _fields_ = [("p", c_void_p), ("n_stride", c_int64), ("c0", c_int32), ("C", c_int32),
                 ("mode", c_int32), ("act", c_int32), ("bias", c_void_p), ("stats", c_void_p),
                 ("y", c_void_p), ("y_n_stride", c_int64), ("slope", c_void_p),
-                ("slope_grad", c_void_p), ("bn", Bn)]
+                ("slope_grad", c_void_p), ("bn", Bn), ("r", c_void_p), ("r_n_stride", c_int64),
+                ("old", c_void_p), ("old_n_stride", c_int64), ("p2", c_void_p),
+                ("p2_n_stride", c_int64)]
 
 
 class Sinks(Structure):

@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "../../include/isg.h"
+#include "residual.h"
 
 static thread_local std::string g_last_error;
 
@@ -67,6 +68,18 @@ static bool geom_ok(const isg_conv_geom* g) { return check_geom(g) == ISG_OK; }
 
 int32_t isg_tap_conv(const isg_conv_geom*, const isg_vtensor*, const float*, const isg_sinks*,
                      bool, hipStream_t);
+int32_t isg_pw_gemm(const isg_conv_geom*, const isg_vtensor*, const float*, const isg_sinks*, bool,
+                    hipStream_t);
+
+// the residual forms (isg.h) exist for the 1x1 stride-1 dense conv only
+static bool pointwise(const isg_conv_geom* g) {
+    return g->KH == 1 && g->KW == 1 && g->SH == 1 && g->SW == 1 && g->PH == 0 && g->PW == 0 &&
+           g->DH == 1 && g->DW == 1 && g->groups == 1 && g->w_ci == 0;
+}
+// one segment of `cin` channels in, one sink of all `cout` rows out
+static bool res_shape_ok(const isg_vtensor* v, int cin, const isg_sinks* k, int cout) {
+    return v->nseg == 1 && v->s[0].C == cin && k->nsink == 1 && k->s[0].c0 == 0 && k->s[0].C == cout;
+}
 int32_t isg_s2k5_fwd(const isg_conv_geom*, const isg_vtensor*, const float*, const isg_sinks*,
                      hipStream_t);
 int32_t isg_s2k5_wgrad(const isg_conv_geom*, const isg_vtensor*, const isg_vtensor*, double*, double*,
@@ -81,7 +94,9 @@ static bool partial_w(const isg_conv_geom* g) { return g->w_ci > 0 && g->w_ci !=
 // a BN_BWD segment without y (isg.h isg_vseg: y = p, at p's image stride), resolved once
 // here so no kernel has to know the convention
 static isg_vtensor resolve_y(const isg_vtensor* v) {
-    isg_vtensor r = *v;
+    isg_vtensor r{};
+    if (!v) return r;  // nseg 0: refused by the kernels' channel checks
+    r = *v;
     for (int i = 0; i < r.nseg && i < ISG_MAX_SEGS; ++i)
         if (r.s[i].xform == ISG_XF_BN_BWD && !r.s[i].y) {
             r.s[i].y = r.s[i].p;
@@ -93,12 +108,19 @@ static isg_vtensor resolve_y(const isg_vtensor* v) {
 extern "C" {
 
 const char* isg_last_error(void) { return g_last_error.c_str(); }
-int32_t isg_abi_version(void) { return 9; }
+int32_t isg_abi_version(void) { return 10; }
 int32_t isg_stat_replicas(void) { return ISG_STAT_REP; }
 
 int32_t isg_conv_fwd(const isg_conv_geom* g, const isg_vtensor* x_, const float* w,
                      const isg_sinks* out, isg_stream_t st) {
     if (int32_t e = check_geom(g)) return e;
+    if (!x_ || !out) return isg_set_error(ISG_ERR_INVALID, "conv fwd: NULL tensor");
+    if (isg_sinks_res(out)) return isg_set_error(ISG_ERR_UNSUPPORTED, "conv fwd: residual sink form");
+    if (isg_vt_res(x_)) {  // a folded residual tail: the slab 1x1 GEMM or nothing
+        if (!pointwise(g) || !res_shape_ok(x_, g->Ci, out, g->Co))
+            return isg_set_error(ISG_ERR_UNSUPPORTED, "conv fwd: residual input needs a 1x1 conv, one segment, one sink");
+        return isg_pw_gemm(g, x_, w, out, false, st);
+    }
     const isg_vtensor xr = resolve_y(x_);
     const isg_vtensor* x = &xr;
     if (partial_w(g)) {
@@ -116,8 +138,15 @@ int32_t isg_conv_fwd(const isg_conv_geom* g, const isg_vtensor* x_, const float*
 int32_t isg_conv_dgrad(const isg_conv_geom* g, const isg_vtensor* dy_, const float* w,
                        const isg_sinks* dx, isg_stream_t st) {
     if (int32_t e = check_geom(g)) return e;
+    if (!dy_ || !dx) return isg_set_error(ISG_ERR_INVALID, "conv dgrad: NULL tensor");
+    if (isg_vt_res(dy_)) return isg_set_error(ISG_ERR_UNSUPPORTED, "conv dgrad: residual input form");
     const isg_vtensor dyr = resolve_y(dy_);
     const isg_vtensor* dy = &dyr;
+    if (isg_sinks_res(dx)) {  // a folded residual tail's backward: the slab 1x1 GEMM or nothing
+        if (!pointwise(g) || !res_shape_ok(dy, g->Co, dx, g->Ci))
+            return isg_set_error(ISG_ERR_UNSUPPORTED, "conv dgrad: residual sink needs a 1x1 conv, one segment, one sink");
+        return isg_pw_gemm(g, dy, w, dx, true, st);
+    }
     if (partial_w(g)) return isg_set_error(ISG_ERR_UNSUPPORTED, "conv dgrad with w_ci != Ci");
     if (g->groups == 1) return isg_dense_conv_dgrad(g, dy, w, dx, st);
     return isg_depthwise_dgrad(g, dy, w, dx, st);
@@ -127,11 +156,14 @@ int32_t isg_conv_wgrad_rep(const isg_conv_geom* g, const isg_vtensor* dy_, const
                            double* dw, double* dbias, int64_t rep_stride, int32_t nrep,
                            isg_stream_t st) {
     if (int32_t e = check_geom(g)) return e;
+    if (isg_vt_res(dy_) || isg_vt_res(x_))
+        return isg_set_error(ISG_ERR_UNSUPPORTED, "conv wgrad: residual input form");
     const isg_vtensor dyr = resolve_y(dy_), xr = resolve_y(x_);
     const isg_vtensor *dy = &dyr, *x = &xr;
     if (nrep < 1 || (nrep > 1 && rep_stride <= 0))
         return isg_set_error(ISG_ERR_INVALID, "conv wgrad: bad replicas %d / stride %lld", nrep,
                              (long long)rep_stride);
+    if (!dy_ || !x_) return isg_set_error(ISG_ERR_INVALID, "conv wgrad: NULL tensor");
     if (partial_w(g)) {
         // the stem's RGB layer 1 (weight over w_ci = 20 channels): s2k5_wgrad_kernel
         const int32_t s = isg_s2k5_wgrad(g, dy, x, dw, dbias, rep_stride, nrep, st);

@@ -11,11 +11,13 @@
 #include <stdint.h>
 
 #include "../../include/isg.h"
+#include "residual.h"
 
 #define ISG_DEV __device__ __forceinline__
 #define ISG_DEV_HOST __host__ __device__ inline
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+
 
 // Global-address-space access through a generic pointer. Pointers that come out of LDS
 // tables (or any memory the compiler cannot trace to a kernel argument) otherwise turn

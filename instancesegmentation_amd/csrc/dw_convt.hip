@@ -728,6 +728,7 @@ int32_t isg_depthwise_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const
 
 int32_t isg_convT_fwd(const isg_conv_geom* g, const isg_vtensor* x, const float* w,
                       const isg_sinks* out, isg_stream_t st) {
+    if (isg_vt_res(x) || isg_sinks_res(out)) return isg_set_error(ISG_ERR_UNSUPPORTED, "convT fwd: residual form");
     if (x->nseg != 1 || out->nsink != 1 || out->s[0].mode != ISG_SINK_STORE || g->Ci > kCtMaxCi)
         return isg_set_error(ISG_ERR_UNSUPPORTED, "convT fwd: need 1 seg / 1 STORE sink, Ci <= %d", kCtMaxCi);
     const int S = g->SH;

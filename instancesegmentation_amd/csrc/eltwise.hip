@@ -826,6 +826,8 @@ extern "C" {
 int32_t isg_tail_fwd(const isg_tail* t, isg_stream_t st) {
     if ((t->H & 1) || (t->W & 1) || t->nterm < 1 || t->nterm > 3)
         return isg_set_error(ISG_ERR_UNSUPPORTED, "tail fwd: H, W must be even, 1..3 terms");
+    for (int i = 0; i < t->nterm; ++i)
+        if (isg_seg_res(t->term[i])) return isg_set_error(ISG_ERR_UNSUPPORTED, "tail fwd: residual term form");
     if (tail4_ok(*t, nullptr)) {
         dim3 grid4((unsigned)((((int64_t)t->H / 2) * (t->W / 4) + kThreads - 1) / kThreads), t->C, t->N);
         hipLaunchKernelGGL(tail_fwd4_kernel, grid4, dim3(kThreads), 0, st, *t);
@@ -840,6 +842,8 @@ int32_t isg_tail_bwd(const isg_tail_grad* t, isg_stream_t st) {
     const isg_tail& f = t->f;
     if ((f.H & 1) || (f.W & 1) || f.nterm < 1 || f.nterm > 3)
         return isg_set_error(ISG_ERR_UNSUPPORTED, "tail bwd: H, W must be even, 1..3 terms");
+    for (int i = 0; i < f.nterm; ++i)
+        if (isg_seg_res(f.term[i])) return isg_set_error(ISG_ERR_UNSUPPORTED, "tail bwd: residual term form");
     // the kernels load every accumulating term's old value before any write:
     // two terms accumulating into one destination would lose one contribution
     for (int i = 0; i < f.nterm; ++i)
@@ -859,6 +863,7 @@ int32_t isg_tail_bwd(const isg_tail_grad* t, isg_stream_t st) {
 int32_t isg_maxpool_fwd(const isg_vtensor* x, int32_t k, float* out, int64_t out_n_stride,
                         isg_stream_t st) {
     if (k < 1 || x->H % k || x->W % k) return isg_set_error(ISG_ERR_UNSUPPORTED, "maxpool: H,W %% k");
+    if (isg_vt_res(x)) return isg_set_error(ISG_ERR_UNSUPPORTED, "maxpool: residual input form");
     int C = 0;
     for (int i = 0; i < x->nseg; ++i) C += x->s[i].C;
     PoolArgs a{};
@@ -871,6 +876,7 @@ int32_t isg_maxpool_fwd(const isg_vtensor* x, int32_t k, float* out, int64_t out
 int32_t isg_maxpool_bwd(const isg_vtensor* x, int32_t k, const float* dout, int64_t dout_n_stride,
                         const isg_sinks* dx, isg_stream_t st) {
     if (k < 1 || x->H % k || x->W % k) return isg_set_error(ISG_ERR_UNSUPPORTED, "maxpool: H,W %% k");
+    if (isg_vt_res(x) || isg_sinks_res(dx)) return isg_set_error(ISG_ERR_UNSUPPORTED, "maxpool: residual form");
     int C = 0;
     for (int i = 0; i < x->nseg; ++i) C += x->s[i].C;
     for (int i = 0; i < dx->nsink; ++i)

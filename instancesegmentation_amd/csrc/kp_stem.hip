@@ -373,6 +373,7 @@ int32_t isg_kp_stem_fwd(const isg_kp_stem* s, isg_stream_t st) {
 int32_t isg_kp_stem_wgrad(const isg_kp_stem* s, isg_stream_t st) {
     KpArgs a;
     if (int32_t e = kp_args(s, a, true)) return e;
+    if (isg_vt_res(&s->dy)) return isg_set_error(ISG_ERR_UNSUPPORTED, "kp stem wgrad: residual form");
     if (!s->dw || s->dy.nseg != 1 || s->dy.s[0].C != a.Co)
         return isg_set_error(ISG_ERR_INVALID, "kp_stem_wgrad: dw / dy (one segment of Co channels)");
     if (s->nrep < 1 || (s->nrep > 1 && s->rep_stride <= 0))

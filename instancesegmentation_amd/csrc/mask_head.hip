@@ -738,6 +738,8 @@ __global__ __launch_bounds__(2 * kThreads, 1) void head_bwd_kernel(isg_mask_head
 int32_t check_head(const isg_mask_head* a, bool bwd) {
     if (!a || !a->w1 || !a->w2 || a->N < 1 || a->Hi < 1 || a->Wi < 1)
         return isg_set_error(ISG_ERR_INVALID, "mask head: NULL weights or bad size");
+    if (isg_vt_res(&a->x) || (bwd && isg_sinks_res(&a->dx)))
+        return isg_set_error(ISG_ERR_UNSUPPORTED, "mask head: residual form");
     int C = 0;
     for (int s = 0; s < a->x.nseg; ++s) C += a->x.s[s].C;
     if (a->x.nseg < 1 || a->x.nseg > ISG_MAX_SEGS || C != kCi || a->x.H != a->Hi || a->x.W != a->Wi)

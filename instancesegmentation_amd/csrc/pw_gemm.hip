@@ -291,6 +291,7 @@ struct PwxArgs {
     int wsh;                          // log2 of the weight quads per row, padded to a power of 2
     int stat_on;                      // some channel or sink row evaluates its BN statistics
     int pre_on;                       // some sink reads an operand (ACTBWD y / ACCUM old value)
+    int res_on;                       // the one sink is ACTBWD's residual form (isg.h isg_sink)
     int64_t P;
 };
 
@@ -390,16 +391,18 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
     // this same round trip instead of after the MFMA loop
     constexpr int CT_ = BP / 16;
     const int nt_ = (BM / 16) * CT_;
-    float pre[TPW][4];
+    float pre[TPW][4], pro[TPW][4], prr[TPW][4];  // sink operands: y / old value, + residual form
 #pragma unroll
     for (int i = 0; i < TPW; ++i)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) pre[i][r] = 0.f;
+        for (int r = 0; r < 4; ++r) pre[i][r] = pro[i][r] = prr[i][r] = 0.f;
     if (SEG1 && a.pre_on) {
         const SinkLite& k0 = ks.s0;
         const bool ab = k0.mode == ISG_SINK_ACTBWD;
         const float* base = ab ? k0.y : k0.p;
         const int bns = ab ? k0.yns : k0.ns;
+        const bool res = a.res_on != 0;  // lane-invariant; r is non-NULL then (host check)
+        const bool res_old = res && k0.old != nullptr;
 #pragma unroll
         for (int i = 0; i < TPW; ++i) {
             const int t = min(wave + 4 * i, nt_ - 1);
@@ -412,6 +415,8 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
             for (int r = 0; r < 4; ++r) {
                 const int cl = min(rt * 16 + kk * 4 + r, Mb - 1) + m0 - k0.c0;
                 pre[i][r] = gld(base, (int64_t)cl * a.HW + (int64_t)ne * bns + pixe);
+                if (res_old) pro[i][r] = gld(k0.old, (int64_t)cl * a.HW + (int64_t)ne * k0.ons + pixe);
+                if (res) prr[i][r] = gld(k0.r, (int64_t)cl * a.HW + (int64_t)ne * k0.rns + pixe);
             }
         }
     }
@@ -447,6 +452,9 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
     STAMP(2);
 
     // ---- phase 3: producer transform into Xs[k][p] --------------------------------------
+    // the materialised input (isg_vtensor.mat: a folded residual tail's block output),
+    // written once per pixel by the first row block
+    float* const mat = SEG1 && blockIdx.y == 0 ? a.src.mat : nullptr;
 #pragma unroll
     for (int u = 0; u < XU; ++u) {
         const int c = cr + u * CPP;
@@ -456,11 +464,18 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
             const ChSrc t = tabA[c];
             const XfLin l = xf_lin(t.xf, t.act, tabK[c]);
             f32x4 o;
+            if constexpr (HY) {  // BN_FWD with a residual term (isg_vseg): y is the residual
+                const float isr = t.xf == ISG_XF_BN_FWD && t.y != t.p ? 1.f : 0.f;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) o[e] = xf_lin_apply(l, xv[u][e], HY ? yv[u][e] : xv[u][e]);
+                for (int e = 0; e < 4; ++e) o[e] = xf_lin_apply_r(l, xv[u][e], yv[u][e], isr);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) o[e] = xf_lin_apply(l, xv[u][e], xv[u][e]);
+            }
 #pragma unroll
             for (int e = 0; e < 4; ++e) o[e] = live ? o[e] : 0.f;
             *reinterpret_cast<f32x4*>(&Xs[c * XS + 4 * q]) = o;
+            if (mat && live) gst4(mat, (int64_t)n * a.src.mat_n_stride + (int64_t)c * a.HW + pix, o);
         }
     }
     __syncthreads();
@@ -554,7 +569,11 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
                 s1[r] = v * v;
             } else {
                 const float y = pre[i][r];
-                const float z = (y - qi.f.mean) * qi.f.scale + qi.f.beta;
+                float z = (y - qi.f.mean) * qi.f.scale + qi.f.beta;
+                if (SEG1 && a.res_on) {  // residual form: + old gradient, + residual term
+                    v = pro[i][r] + v;
+                    z = z + prr[i][r];
+                }
                 float gv = v;
                 if (qi.act == ISG_ACT_RELU) {
                     gv = z > 0.f ? v : 0.f;
@@ -563,6 +582,8 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
                     s2[r] = z > 0.f ? 0.f : z * v;
                 }
                 gst(qi.p, off, gv);
+                if (SEG1 && a.res_on && ks.s0.p2)
+                    gst(ks.s0.p2, (int64_t)(rl + m0 - ks.s0.c0) * a.HW + (int64_t)ne * ks.s0.p2ns + pixe, gv);
                 s0[r] = gv;
                 s1[r] = gv * (y - qi.f.mean);
             }
@@ -675,8 +696,11 @@ bool pwx_src_ok(const isg_vtensor& v, int HW) {
     for (int s = 0; s < v.nseg; ++s) {
         const isg_vseg& g = v.s[s];
         if (!aligned16(g.p) || g.n_stride % 4) return false;
-        if (g.xform == ISG_XF_BN_BWD && g.y && (!aligned16(g.y) || g.y_n_stride % 4)) return false;
+        if ((g.xform == ISG_XF_BN_BWD || g.xform == ISG_XF_BN_FWD) && g.y &&
+            (!aligned16(g.y) || g.y_n_stride % 4))
+            return false;
     }
+    if (v.mat && (!aligned16(v.mat) || v.mat_n_stride % 4)) return false;
     return true;
 }
 
@@ -872,7 +896,21 @@ int32_t isg_pw_gemm(const isg_conv_geom* g, const isg_vtensor* src, const float*
         return isg_set_error(ISG_ERR_UNSUPPORTED, "pw gemm: K = %d channels > %d", a.K, kMaxK);
     if (a.M > 2 * kMaxBM)
         return isg_set_error(ISG_ERR_UNSUPPORTED, "pw gemm: M = %d rows", a.M);
-    {  // thin layers (K, M <= 16) on the VALU
+    // a folded residual tail (isg.h: BN_FWD segment with y / vtensor.mat in the forward,
+    // ACTBWD sink's residual form in the input gradient) runs on the slab kernel only
+    bool res_in = src->mat != nullptr, res_out = false;
+    for (int s = 0; s < src->nseg; ++s) res_in |= src->s[s].xform == ISG_XF_BN_FWD && src->s[s].y;
+    for (int s = 0; s < out->nsink; ++s) {
+        const isg_sink& k = out->s[s];
+        res_out |= k.r || k.old || k.p2;
+    }
+    const bool res = res_in || res_out;
+    if (res && ((res_in && dgrad) ||
+                (res_out && (!dgrad || out->s[0].mode != ISG_SINK_ACTBWD || !out->s[0].r)) ||
+                src->nseg != 1 || out->nsink != 1))
+        return isg_set_error(ISG_ERR_UNSUPPORTED, "pw gemm: residual forms need one segment and one "
+                             "sink (input residual in the forward, ACTBWD residual in the input gradient)");
+    if (!res) {  // thin layers (K, M <= 16) on the VALU
         const int32_t t = thin_pw(a, st);
         if (t != 0) return t < 0 ? t : 0;
     }
@@ -893,16 +931,17 @@ int32_t isg_pw_gemm(const isg_conv_geom* g, const isg_vtensor* src, const float*
     // transposes, M = 128 rows over K = 48, on 32 x 64 tiles — kbench fwd 15.3 -> 14.8 us,
     // dgrad 18.4 -> 17.2 us against the chunked kernel)
     static const bool wide_rows = getenv("ISG_NO_PWX_WIDE_ROWS") == nullptr;
-    const bool slab_pays = (!dgrad && a.P >= 65536) || (dgrad && a.M <= 64 && a.K <= 128) ||
+    const bool slab_pays = res || (!dgrad && a.P >= 65536) || (dgrad && a.M <= 64 && a.K <= 128) ||
                            (fwd_small && !dgrad && a.M <= 64 && a.K <= 128) ||
                            (wide_rows && a.M <= 128 && a.K <= 64);
-    if (!slab_off && slab_pays && wmode && pwx_src_ok(*src, a.HW) && a.P < ((int64_t)1 << 31)) {
+    if ((!slab_off || res) && slab_pays && wmode && pwx_src_ok(*src, a.HW) && a.P < ((int64_t)1 << 31)) {
         PwxArgs b{};
         b.src = a.src; b.out = a.out; b.w = w; b.rs = a.rs; b.cs = a.cs;
         b.HW = a.HW; b.M = a.M; b.K = a.K; b.Kp = (a.K + 15) / 16 * 16; b.P = a.P;
         b.wmode = wmode;
         b.fast = host_vt_fast(*src) && host_sinks_fast(*out);
         b.pre_on = 0;
+        b.res_on = res_out ? 1 : 0;
         for (int s = 0; s < out->nsink; ++s)
             if (out->s[s].mode == ISG_SINK_ACTBWD || out->s[s].mode == ISG_SINK_ACCUM) b.pre_on = 1;
         b.stat_on = 0;
@@ -917,11 +956,14 @@ int32_t isg_pw_gemm(const isg_conv_geom* g, const isg_vtensor* src, const float*
         // HY also selects the 4-group statistics loads (coef_issue<4>): a BN_BWD segment
         // finalised by the consumer needs them even when its y is its own input (ADVICE r03:
         // the 2-group form would apply identity coefficients there)
+        // HY also loads a BN_FWD segment's residual term (isg_vseg residual form)
         bool hy = false;
-        for (int s = 0; s < src->nseg; ++s)
+        for (int s = 0; s < src->nseg; ++s) {
             if (src->s[s].xform == ISG_XF_BN_BWD &&
                 ((src->s[s].y && src->s[s].y != src->s[s].p) || (!src->s[s].bn.coef && src->s[s].bn.stats)))
                 hy = true;
+            if (src->s[s].xform == ISG_XF_BN_FWD && src->s[s].y) hy = true;
+        }
         // (BM, BP): rows first (fewer row blocks = fewer slab re-reads), then pixels; the
         // first configuration that fits the LDS and the per-lane load budget (8 weight and
         // 8 activation loads of 16 B), keeps >= 4 MFMA tiles per workgroup and gives >= 256
@@ -972,6 +1014,9 @@ int32_t isg_pw_gemm(const isg_conv_geom* g, const isg_vtensor* src, const float*
             return rc;
         }
     }
+    if (res)
+        return isg_set_error(ISG_ERR_UNSUPPORTED, "pw gemm: residual form off the slab kernel "
+                             "(16-B aligned rows and weights, HW %% 4 == 0)");
     const int64_t pblocks = (a.P + kBP - 1) / kBP;
     // rows per block: up to 128, halved while that keeps more workgroups in flight
     int bm = std::min(kMaxBM, (a.M + 15) / 16 * 16);

@@ -1,0 +1,19 @@
+#pragma once
+#include "../../include/isg.h"
+
+// Host checks of the residual forms (isg.h: a BN_FWD segment with y, vtensor.mat, the
+// ACTBWD sink's r / old / p2): only the 1x1 stride-1 GEMM (pw_gemm.hip) implements them,
+// every other entry point refuses them instead of silently dropping the residual.
+inline bool isg_seg_res(const isg_vseg& s) { return s.xform == ISG_XF_BN_FWD && s.y; }
+inline bool isg_vt_res(const isg_vtensor* v) {
+    if (!v) return false;
+    bool r = v->mat != nullptr;
+    for (int i = 0; i < v->nseg && i < ISG_MAX_SEGS; ++i) r |= isg_seg_res(v->s[i]);
+    return r;
+}
+inline bool isg_sinks_res(const isg_sinks* k) {
+    if (!k) return false;
+    bool r = false;
+    for (int i = 0; i < k->nsink && i < ISG_MAX_SEGS; ++i) r |= k->s[i].r || k->s[i].old || k->s[i].p2;
+    return r;
+}

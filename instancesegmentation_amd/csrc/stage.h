@@ -12,7 +12,7 @@
 // One channel of a vtensor (c must be wave-uniform so this stays in SGPRs).
 struct ChSrc {
     const float* p;  // channel base, image 0
-    const float* y;  // BN_BWD: saved forward output of the channel (else == p)
+    const float* y;  // BN_BWD: saved forward output; BN_FWD: residual term (else == p)
     int ns, yns;     // elements between images
     int xf, act;
 };
@@ -57,7 +57,7 @@ ISG_DEV ChSrc ch_src(const VtLite& l, int c, int hw) {
     }
     r.p += (int64_t)cl * hw;
     // no separate y: y is the input itself, with the input's image stride
-    const bool hy = r.xf == ISG_XF_BN_BWD && y;
+    const bool hy = (r.xf == ISG_XF_BN_BWD || r.xf == ISG_XF_BN_FWD) && y;
     r.y = hy ? y + (int64_t)cl * hw : r.p;
     r.yns = hy ? r.yns : r.ns;
     return r;
@@ -149,6 +149,17 @@ ISG_DEV XfLin xf_lin(int xf, int act, const ChanCoef& k) {
 
 ISG_DEV float xf_lin_apply(const XfLin& l, float x, float y) {
     float zf = (x - l.k.c0) * l.k.c1 + l.k.c2;
+    zf = zf > 0.f ? zf : zf * l.neg;
+    const float zb = l.k.c0 * x + l.k.c1 * (y - l.k.c2) + l.k.c3;
+    return l.isb != 0.f ? zb : zf;
+}
+
+// the same with a BN_FWD channel's residual term y added before the activation when
+// isr = 1 (isg_vseg residual form; a block tail's BN(y3) + x, then PReLU): the tail's own
+// order of operations, (BN value) + residual
+ISG_DEV float xf_lin_apply_r(const XfLin& l, float x, float y, float isr) {
+    float zf = (x - l.k.c0) * l.k.c1 + l.k.c2;
+    zf = zf + isr * y;
     zf = zf > 0.f ? zf : zf * l.neg;
     const float zb = l.k.c0 * x + l.k.c1 * (y - l.k.c2) + l.k.c3;
     return l.isb != 0.f ? zb : zf;
@@ -458,17 +469,17 @@ ISG_DEV ChSrc ch_addr(const VtSel vt, int c, int64_t hw) {
     r.xf = ISG_SEL3(s, xf, vt);
     r.act = ISG_SEL3(s, act, vt);
     const float* y = ISG_SEL3(s, y, vt);
-    const bool hy = r.xf == ISG_XF_BN_BWD && y;
+    const bool hy = (r.xf == ISG_XF_BN_BWD || r.xf == ISG_XF_BN_FWD) && y;
     r.y = hy ? y + (int64_t)cl * hw : r.p;
     r.yns = hy ? r.yns : r.ns;
     return r;
 }
 
 struct SinkLite {
-    float *p;
-    const float *y, *coef, *bias, *slope, *gamma, *beta;
+    float *p, *p2;
+    const float *y, *coef, *bias, *slope, *gamma, *beta, *r, *old;
     const double* stats;
-    int ns, yns, mode, act, c0, bnC;
+    int ns, yns, mode, act, c0, bnC, rns, ons, p2ns;
     float count, eps;
 };
 ISG_DEV SinkLite sink_lite(const isg_sink& k) {
@@ -480,6 +491,9 @@ ISG_DEV SinkLite sink_lite(const isg_sink& k) {
     l.ns = sgpr_i((int)k.n_stride); l.yns = sgpr_i((int)k.y_n_stride);
     l.mode = sgpr_i(k.mode); l.act = sgpr_i(k.act); l.c0 = sgpr_i(k.c0); l.bnC = sgpr_i(k.bn.C);
     l.count = sgpr_f(k.bn.count); l.eps = sgpr_f(k.bn.eps);
+    l.r = sgpr_p(k.r); l.old = sgpr_p(k.old); l.p2 = sgpr_p(k.p2);
+    l.rns = sgpr_i((int)k.r_n_stride); l.ons = sgpr_i((int)k.old_n_stride);
+    l.p2ns = sgpr_i((int)k.p2_n_stride);
     return l;
 }
 struct SkSel {

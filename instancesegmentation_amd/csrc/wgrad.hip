@@ -1124,6 +1124,7 @@ extern "C" int32_t isg_pwg_group_max() { return kPwgGroup; }
 
 extern "C" int32_t isg_pwg_plan(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, double* dw,
                      double* dbias, int64_t rep_stride, int32_t nrep, void* plan) {
+    if (isg_vt_res(dy) || isg_vt_res(x)) return 0;  // isg_conv_wgrad_rep refuses it
     const char* pe = getenv("ISG_PWK");
     if (pe && atoi(pe)) return 0;  // the opt-in pwk path stays on the per-op route
     if (!dw || nrep < 1 || (nrep > 1 && rep_stride <= 0) || g->groups != 1) return 0;

@@ -667,6 +667,51 @@ def _fork_late_wgrads(recs, late):
             recs[i], recs[i + 1] = b, a
 
 
+def _fold_tails(g):
+    """Residual tails folded into their first consumer: a tail
+    out = act(BN(y) + x) (segment.py:75-77, 107-109, 259: BatchNorm'd raw conv output plus a
+    materialised value, no upsampling) whose output is read FIRST by the very next op, a
+    1x1 stride-1 conv on exactly that value, stops being a launch of its own:
+      forward  — the conv reads act(BN(y) + x) on load (isg_vseg residual form) and its
+                 first row block writes the materialised output on the way (vtensor.mat),
+                 which every later reader (the next tail's residual term, skips, the
+                 weight gradient) still finds in the tail's buffer;
+      backward — the conv's input gradient, the last contribution to dL/d out, carries the
+                 tail's backward in its sink (ACTBWD residual form: + the gradient already
+                 accumulated for out, act' at BN(y) + x, BatchNorm-backward sums of y, the
+                 PReLU slope gradient, and the residual term's gradient as a second
+                 output), decided in ConvOp.bwd (falls back to the tail's own launch when
+                 the gradient bookkeeping does not allow it).
+    Train mode only (batch statistics); ISG_NO_TAIL_FOLD=1 off."""
+    if os.environ.get("ISG_NO_TAIL_FOLD", "0") == "1" or not g.train:
+        return
+    for t, c in zip(g.ops, g.ops[1:]):
+        if not isinstance(t, TailOp) or not isinstance(c, ConvOp) or len(t.terms) != 2:
+            continue
+        (y, upy), (r, upr) = t.terms
+        C = t.out.C
+        if upy or upr or y.bn is None or y.act != "none" or r.virtual or t.c0 != 0:
+            continue
+        if t.out.slot != S_ACT or y.C != C or r.C != C or y.c0 != 0 or y.buf.C != C:
+            continue
+        ge = c.geom
+        if not (c.kind == "conv" and c.kp is None and not getattr(c, "side", False)
+                and ge["KH"] == 1 and ge["KW"] == 1 and ge["SH"] == 1 and ge["SW"] == 1
+                and ge["PH"] == 0 and ge["PW"] == 0 and ge["DH"] == 1 and ge["DW"] == 1
+                and ge["groups"] == 1 and "w_ci" not in ge):
+            continue
+        if len(c.x.segs) != 1:
+            continue
+        xv = c.x.segs[0]
+        if xv.buf is not t.out or xv.c0 != 0 or xv.C != C or xv.virtual:
+            continue
+        # the slab kernel's shapes (pw_gemm.hip isg_pw_gemm): 16-B rows, K and M <= 128
+        if (t.out.H * t.out.W) % 4 or C % 4 or C > 128 or ge["Co"] > 128 or ge["Co"] % 4:
+            continue
+        t.fwd_folded = True
+        c.res_tail = t
+
+
 def sinks_spec(sinks):
     """isg_sinks spec from sink specs."""
     return {"s": sinks, "nsink": len(sinks)}
@@ -791,6 +836,57 @@ class ConvOp:
     def __init__(self, g, kind, mod, geom, x, out, bnr):
         self.g, self.kind, self.mod, self.geom, self.x, self.out, self.bnr = g, kind, mod, geom, x, out, bnr
         self.kp = None
+        self.res_tail = None  # a residual tail folded into this conv (_fold_tails)
+
+    def _res_input(self):
+        """The forward input of a folded tail act(BN(y) + x): one BN_FWD segment of y with
+        the residual x and the tail's activation, and the tail's buffer as `mat`."""
+        g, t = self.g, self.res_tail
+        (y, _), (r, _) = t.terms
+        seg = fwd_seg(Val(y.buf, y.c0, y.C, y.bn, t.act, t.slope), g.train)
+        seg["y"] = r.buf.ptr(r.c0)
+        seg["y_n_stride"] = r.buf.n_stride
+        vt = vtensor([seg], g.N, self.geom["H"], self.geom["W"])
+        vt["mat"] = t.out.ptr()
+        vt["mat_n_stride"] = t.out.n_stride
+        return vt
+
+    def _res_sink(self, gs):
+        """The input-gradient sink that also runs the folded tail's backward (isg.h ACTBWD
+        residual form), or None when the gradient bookkeeping does not allow it (then the
+        tail runs its own backward): dL/d out must be this conv's input gradient plus at
+        most what later consumers accumulated over the whole buffer, and the residual
+        term's gradient buffer must not hold anything yet (the second output STOREs)."""
+        g, t = self.g, self.res_tail
+        (y, _), (r, _) = t.terms
+        C = t.out.C
+        ini = gs.inited.get(id(t.out), set())
+        if id(t.out) in gs.external or ini - {(0, C)} or id(y.buf) in gs.G:
+            return None
+        if r.grad and (r.c0, r.C) in gs.inited.get(id(r.buf), set()):
+            return None  # the residual term's gradient already has a value: no STORE
+        gb = gs.alloc(y.buf, "g_" + y.buf.name)
+        gs.G[id(y.buf)] = gb
+        s = {"p": gb.ptr(), "n_stride": gb.n_stride, "c0": 0, "C": C, "mode": L.SINK_ACTBWD,
+             "act": L.ACT[t.act], "y": y.buf.ptr(), "y_n_stride": y.buf.n_stride,
+             "bn": bn_spec(y.bn, g.train), "r": r.buf.ptr(r.c0), "r_n_stride": r.buf.n_stride}
+        if t.slope is not None:
+            s["slope"] = Ptr(t.slope.slot)
+            s["slope_grad"] = Ptr(S_STATS, t.slope.acc_off * 8)
+            t.slope.used_in_bwd = True
+        if (0, C) in ini:
+            d = gs.dbuf(t.out)
+            s["old"] = d.ptr()
+            s["old_n_stride"] = d.n_stride
+        if r.grad:
+            db = gs.dbuf(r.buf)
+            gs.mark(r.buf, r.c0, r.C)
+            s["p2"] = db.ptr(r.c0)
+            s["p2_n_stride"] = db.n_stride
+        if y.bn.fin:
+            gs.pending_final.append(y.bn)
+        t.bwd_folded = True
+        return s
 
     def _kp_spec(self):
         """isg_kp_stem fields shared by the forward and weight-gradient records."""
@@ -823,10 +919,12 @@ class ConvOp:
         if self.bnr is not None and g.train:
             sink["stats"] = Ptr(S_STATS, self.bnr.stats_off * 8)
         ge = self.geom
-        rec = {"g": ge, "a": vtensor(segs, g.N, ge["H"], ge["W"]), "w": g.tptr(self.mod, "weight"),
-               "out": sinks_spec([sink])}
+        a = self._res_input() if self.res_tail is not None else vtensor(segs, g.N, ge["H"], ge["W"])
+        rec = {"g": ge, "a": a, "w": g.tptr(self.mod, "weight"), "out": sinks_spec([sink])}
         kind = L.OP_CONVT_FWD if self.kind == "convT" else L.OP_CONV_FWD
         fl, xb, yb, wb = self._cost()
+        if self.res_tail is not None:
+            xb *= 3  # BN'd y and the residual read, the materialised output written
         ops.add(Record(kind, L.ConvRec, rec, label=self.out.name, flops=fl, nbytes=xb + yb + wb))
         if self.kp is not None:
             ks = dict(self._kp_spec(), w=g.tptr(self.mod, "weight"), y=self.out.ptr(),
@@ -847,9 +945,10 @@ class ConvOp:
         dyv = vtensor([dy], g.N, ge["OH"], ge["OW"])
         # ---- input gradient
         if self.x.grad:
-            sinks = []
+            rs = self._res_sink(gs) if self.res_tail is not None else None
+            sinks = [rs] if rs is not None else []
             c = 0
-            for v in self.x.segs:
+            for v in ([] if rs is not None else self.x.segs):
                 sinks.append(gs.sink_for(v, c, g.train))
                 c += v.C
             sk = sinks_spec(sinks)
@@ -1097,11 +1196,15 @@ class TailOp:
         return t
 
     def fwd(self, ops):
+        if getattr(self, "fwd_folded", False):
+            return  # the next 1x1 conv computes and writes the output (_fold_tails)
         ops.add(Record(L.OP_TAIL_FWD, L.Tail, self.spec(), label=self.out.name))
 
     def bwd(self, ops, gs):
         g = self.g
         C = self.terms[0][0].C
+        if getattr(self, "bwd_folded", False):
+            return  # done in the consumer's input-gradient sink (ConvOp._res_sink)
         if not gs.has_grad(self.out, self.c0, C):
             return
         d = gs.dbuf(self.out)
@@ -1167,6 +1270,7 @@ class Plan:
                 self._emit_output(g, o, ob)
             self.out_bufs.append(ob)
         self.out_shapes = [(N, b.C, b.H, b.W) for b in self.out_bufs]
+        _fold_tails(g)
         # a training step's loss accumulator (one double): in the statistics arena, so the
         # forward's memset zeroes it (no separate fill launch before the loss kernel)
         self.loss_off = None

@@ -7,7 +7,7 @@ import torch.nn.functional as F
 
 from instancesegmentation_amd import _lib as L
 from tests.isg_helpers import (bn_spec_eval, bn_spec_train, call, geom, ptr, rep_fold, rep_from,
-                               rep_zeros, sinks, stream, vt)
+                               rep_zeros, sinks, stream, struct, vt)
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -406,6 +406,135 @@ def test_pw_bn_bwd_y_null(cfg):
     call("isg_conv_wgrad", geom(**ge), vt([dyseg], N, H, W), vt([xseg], N, H, W), ptr(DW), 0,
          stream())
     close(DW.float(), torch.nn.grad.conv2d_weight(x, (Co, Ci, 1, 1), dy), what="1x1 wgrad (y NULL)")
+
+
+# folded residual tails (engine._fold_tails; isg.h residual forms): the fold's shapes
+# (128^2 48 -> 16, 64^2 128 -> 48 and their input gradients) plus a ragged pixel count
+RES = [(48, 16, 32, 32), (128, 48, 16, 16), (48, 16, 20, 12)]
+
+
+def _res_state(C, N, H, W, seed):
+    """raw y, residual x, BN parameters and train statistics [sum | sumsq | 0 | 0] of y."""
+    y = rnd(N, C, H, W, seed=seed) + 0.3
+    xr = rnd(N, C, H, W, seed=seed + 1)
+    gamma, beta, _, _, slope = bn_eval_params(C, seed + 2)
+    st = torch.cat([y.sum((0, 2, 3)), (y * y).sum((0, 2, 3)), torch.zeros(2 * C, dtype=torch.float64)])
+    mean = y.mean((0, 2, 3))
+    rstd = 1 / torch.sqrt(y.var((0, 2, 3), unbiased=False) + 1e-5)
+    z = (y - mean[None, :, None, None]) * (gamma * rstd)[None, :, None, None] \
+        + beta[None, :, None, None] + xr
+    return y, xr, gamma, beta, slope, st, mean, z
+
+
+@pytest.mark.parametrize("act", ["prelu", "relu"])
+@pytest.mark.parametrize("cfg", RES)
+def test_pw_residual_fwd(cfg, act):
+    """Folded residual tail, forward: a 1x1 conv reading act(BN(y) + x) on load (BN_FWD
+    segment with a residual y, statistics finalised by the consumer) that also writes the
+    materialised act(BN(y) + x) to vtensor.mat — segment.py:75-77 then the next block's
+    first conv — against fp64."""
+    C, Co, H, W = cfg
+    N = 2
+    ge, _, _ = _geom(N, C, Co, H, W, 1, 1, 0, 1)
+    y, xr, gamma, beta, slope, st, _, z = _res_state(C, N, H, W, 71)
+    v = torch.where(z > 0, z, z * slope[None, :, None, None]) if act == "prelu" else z.clamp_min(0)
+    w = rnd(Co, C, 1, 1, seed=74, scale=(2.0 / C) ** 0.5)
+    b = rnd(Co, seed=75, scale=0.1)
+    ref = F.conv2d(v, w, b)
+    Y, XR, GA, BE, SL, ST = cuda32(y), cuda32(xr), cuda32(gamma), cuda32(beta), cuda32(slope), rep_from(st)
+    seg = {"p": ptr(Y), "y": ptr(XR), "n_stride": C * H * W, "y_n_stride": C * H * W, "C": C,
+           "xform": L.XF_BN_FWD, "act": L.ACT[act], "bn": bn_spec_train(GA, BE, ST, N * H * W)}
+    if act == "prelu":
+        seg["slope"] = ptr(SL)
+    MAT = torch.full((N, C, H, W), float("nan"), device=DEV)
+    OUT = torch.full((N, Co, H, W), float("nan"), device=DEV)
+    OST = rep_zeros(4 * Co)
+    B, Wt = cuda32(b), cuda32(w)  # kept alive: the call only sees their addresses
+    a = struct(L.VTensor, {"s": [seg], "nseg": 1, "N": N, "H": H, "W": W, "mat": ptr(MAT),
+                           "mat_n_stride": C * H * W})
+    sk = sinks([{"p": ptr(OUT), "n_stride": Co * H * W, "c0": 0, "C": Co, "mode": L.SINK_STORE,
+                 "bias": ptr(B), "stats": ptr(OST)}])
+    call("isg_conv_fwd", geom(**ge), a, ptr(Wt), sk, stream())
+    close(MAT, v, what="materialised block output")
+    close(OUT, ref, what="1x1 on the folded tail")
+    ost = rep_fold(OST, 4 * Co)
+    close(ost[:Co], ref.sum((0, 2, 3)), tol=4e-6, what="sum")
+    close(ost[Co:2 * Co], (ref * ref).sum((0, 2, 3)), tol=4e-6, what="sumsq")
+
+
+@pytest.mark.parametrize("parts", ["old+p2", "old", "p2", "none"])
+@pytest.mark.parametrize("cfg", RES)
+def test_pw_residual_dgrad(cfg, parts):
+    """Folded residual tail, backward: the 1x1 input gradient's ACTBWD sink in residual
+    form — v' = dx + old (what later consumers accumulated), g = v' * PReLU'(BN(y) + x)
+    into p and p2, BatchNorm-backward sums of y and the PReLU slope gradient — the tail
+    backward of segment.py:75-77 — against fp64."""
+    C, Co, H, W = cfg
+    N = 2
+    ge, _, _ = _geom(N, C, Co, H, W, 1, 1, 0, 1)
+    y, xr, gamma, beta, slope, st, mean, z = _res_state(C, N, H, W, 81)
+    dz = rnd(N, Co, H, W, seed=85)
+    w = rnd(Co, C, 1, 1, seed=86, scale=(2.0 / C) ** 0.5)
+    old = rnd(N, C, H, W, seed=87) if "old" in parts else torch.zeros(N, C, H, W, dtype=torch.float64)
+    tot = torch.nn.grad.conv2d_input((N, C, H, W), w, dz) + old
+    sl = slope[None, :, None, None]
+    g = torch.where(z > 0, tot, tot * sl)
+    Y, XR, GA, BE, SL, ST = cuda32(y), cuda32(xr), cuda32(gamma), cuda32(beta), cuda32(slope), rep_from(st)
+    SG = rep_zeros(C)
+    GB = torch.full((N, C, H, W), float("nan"), device=DEV)
+    P2 = torch.full((N, C, H, W), float("nan"), device=DEV)
+    OLD = cuda32(old)
+    sk = {"p": ptr(GB), "n_stride": C * H * W, "c0": 0, "C": C, "mode": L.SINK_ACTBWD,
+          "act": L.ACT["prelu"], "y": ptr(Y), "y_n_stride": C * H * W, "slope": ptr(SL),
+          "slope_grad": ptr(SG), "bn": bn_spec_train(GA, BE, ST, N * H * W),
+          "r": ptr(XR), "r_n_stride": C * H * W}
+    if "old" in parts:
+        sk["old"], sk["old_n_stride"] = ptr(OLD), C * H * W
+    if "p2" in parts:
+        sk["p2"], sk["p2_n_stride"] = ptr(P2), C * H * W
+    DZ, Wt = cuda32(dz), cuda32(w)  # kept alive: the call only sees their addresses
+    dyseg = {"p": ptr(DZ), "n_stride": Co * H * W, "C": Co, "xform": L.XF_PLAIN}
+    call("isg_conv_dgrad", geom(**ge), vt([dyseg], N, H, W), ptr(Wt), sinks([sk]), stream())
+    close(GB, g, what="g (BN-output gradient of y)")
+    if "p2" in parts:
+        assert torch.equal(P2, GB), "p2 must hold the same g"
+    else:
+        assert torch.isnan(P2).all()
+    stf = rep_fold(ST, 4 * C).double().cpu()
+    for got, terms, what in ((stf[2 * C:3 * C], g, "gsum"),
+                             (stf[3 * C:], g * (y - mean[None, :, None, None]), "gxsum"),
+                             (rep_fold(SG, C).double().cpu(), torch.where(z > 0, 0 * z, z * tot),
+                              "slope grad")):
+        err = (got - terms.sum((0, 2, 3))).abs().max().item()
+        assert err <= 2e-6 * terms.abs().sum((0, 2, 3)).max().item() + 1e-9, (what, err)
+
+
+def test_residual_forms_refused_elsewhere():
+    """Every entry point but the 1x1 GEMM refuses the residual forms (isg.h) instead of
+    silently dropping the residual: a 3x3 forward with a residual input, a 3x3 input
+    gradient with a residual sink, a weight gradient with a residual input."""
+    N, C, H, W = 2, 16, 8, 8
+    ge, _, _ = _geom(N, C, C, H, W, 3, 1, 1, 1)
+    X = torch.zeros(N, C, H, W, device=DEV)
+    ST = rep_zeros(4 * C)
+    G1 = torch.ones(C, device=DEV)
+    seg = {"p": ptr(X), "y": ptr(X), "n_stride": C * H * W, "y_n_stride": C * H * W, "C": C,
+           "xform": L.XF_BN_FWD, "bn": bn_spec_train(G1, G1, ST, N * H * W)}
+    plain = {"p": ptr(X), "n_stride": C * H * W, "C": C, "xform": L.XF_PLAIN}
+    out = sinks([{"p": ptr(X), "n_stride": C * H * W, "c0": 0, "C": C, "mode": L.SINK_STORE}])
+    res_sink = sinks([{"p": ptr(X), "n_stride": C * H * W, "c0": 0, "C": C, "mode": L.SINK_ACTBWD,
+                       "y": ptr(X), "y_n_stride": C * H * W, "r": ptr(X), "r_n_stride": C * H * W,
+                       "bn": bn_spec_train(G1, G1, ST, N * H * W)}])
+    W_ = torch.zeros(C, C, 3, 3, device=DEV)
+    DW = torch.zeros(C * C * 9, dtype=torch.float64, device=DEV)
+    lib = L.lib()
+    import ctypes
+    by = ctypes.byref
+    assert lib.isg_conv_fwd(by(geom(**ge)), by(vt([seg], N, H, W)), ptr(W_), by(out), stream()) == -2  # ISG_ERR_UNSUPPORTED
+    assert lib.isg_conv_dgrad(by(geom(**ge)), by(vt([plain], N, H, W)), ptr(W_), by(res_sink),
+                              stream()) == -2  # ISG_ERR_UNSUPPORTED
+    assert lib.isg_conv_wgrad(by(geom(**ge)), by(vt([plain], N, H, W)), by(vt([seg], N, H, W)),
+                              ptr(DW), None, stream()) == -2  # ISG_ERR_UNSUPPORTED
 
 
 @pytest.mark.parametrize("cfg", [DENSE[0], DENSE[1], DENSE[4], (16, 16, 24, 40, 3, 1, 1, 0)])

@@ -239,6 +239,38 @@ def test_forward_side_branches_fork_and_join():
                and r.kind in (L.OP_CONV_WGRAD, L.OP_KP_STEM_WGRAD))
 
 
+def test_residual_tails_fold_into_the_next_1x1(monkeypatch):
+    """engine._fold_tails: every Bottleneck3x3/5x5 tail act(BN(y) + x) whose output is read
+    first by the next block's 1x1 conv is no launch of its own — forward: the conv record
+    reads a BN_FWD segment with the residual and writes the tail's buffer (vtensor.mat);
+    backward: the conv's input gradient carries the tail's backward (ACTBWD residual sink),
+    except where the residual term's gradient already holds a skip connection's part
+    (bottle1_x.0, bottle2_x.0: their tails keep their own backward). ISG_NO_TAIL_FOLD=1 off."""
+    m = Segment(20)
+    p = Plan(m, [(2, 3, 128, 128), (2, 17, 3)], True, True, (False, False))
+    ops = p.graph.ops
+    fwd = {t.out.name for t in ops if getattr(t, "fwd_folded", False)}
+    bwd = {t.out.name for t in ops if getattr(t, "bwd_folded", False)}
+    chain = [f"bottle1_x.{i}" for i in range(3)] + [f"bottle{s}_x.{i}" for s in (2, 3) for i in range(4)]
+    assert fwd == set(chain)
+    assert bwd == set(chain) - {"bottle1_x.0", "bottle2_x.0"}
+    tails_f = [r for r in p.fwd.recs if r.kind == L.OP_TAIL_FWD]
+    tails_b = [r for r in p.bwd.recs if r.kind == L.OP_TAIL_BWD]
+    assert not any(r.label in fwd for r in tails_f)
+    assert not any(r.label[2:] in bwd for r in tails_b)
+    # the folded conv writes the tail's buffer: its record holds a pointer into it
+    for t in ops:
+        if getattr(t, "fwd_folded", False):
+            c = next(op for op in ops if getattr(op, "res_tail", None) is t)
+            r = next(r for r in p.fwd.recs if r.label == c.out.name)
+            o = t.out.ptr()
+            assert any(fs == o.slot and off == o.off for _, fs, off in r.fix)
+    monkeypatch.setenv("ISG_NO_TAIL_FOLD", "1")
+    q = Plan(Segment(20), [(2, 3, 128, 128), (2, 17, 3)], True, True, (False, False))
+    assert len([r for r in q.fwd.recs if r.kind == L.OP_TAIL_FWD]) == len(tails_f) + len(fwd)
+    assert len([r for r in q.bwd.recs if r.kind == L.OP_TAIL_BWD]) == len(tails_b) + len(bwd)
+
+
 @pytest.mark.parametrize("n", [1, 2])
 def test_forked_pools_join_before_any_reader_of_their_buffer(n):
     """engine._fork_pools at batch 1 and 2: the keypoint heatmaps' pool
