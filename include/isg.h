@@ -117,7 +117,8 @@ typedef struct {
  *           Residual form (r non-NULL; a block tail's backward folded into the input
  *           gradient of the next block's first 1x1, segment.py:75-77): v' = v + old,
  *           z = BN(y) + r, g = v'*act'(z) into p and, when p2 is non-NULL, also into p2
- *           (the residual term's gradient, STORE); statistics as ACTBWD with v'. Accepted
+ *           (the residual term's gradient; STORE, or ACCUM with p2_accum); statistics as
+ *           ACTBWD with v'. Accepted
  *           only by the 1x1 stride-1 input gradient with one sink. */
 typedef struct {
     float* p;
@@ -139,6 +140,8 @@ typedef struct {
     int64_t old_n_stride;
     float* p2;             /* ACTBWD residual form: second output of g, or NULL */
     int64_t p2_n_stride;
+    int32_t p2_accum;      /* p2 += g instead of p2 = g */
+    int32_t pad2_;
 } isg_sink;
 
 typedef struct {

@@ -391,11 +391,13 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
     // this same round trip instead of after the MFMA loop
     constexpr int CT_ = BP / 16;
     const int nt_ = (BM / 16) * CT_;
-    float pre[TPW][4], pro[TPW][4], prr[TPW][4];  // sink operands: y / old value, + residual form
+    // sink operands: y / old value, + the residual form's old gradient, residual term and
+    // p2's old value
+    float pre[TPW][4], pro[TPW][4], prr[TPW][4], pp2[TPW][4];
 #pragma unroll
     for (int i = 0; i < TPW; ++i)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) pre[i][r] = pro[i][r] = prr[i][r] = 0.f;
+        for (int r = 0; r < 4; ++r) pre[i][r] = pro[i][r] = prr[i][r] = pp2[i][r] = 0.f;
     if (SEG1 && a.pre_on) {
         const SinkLite& k0 = ks.s0;
         const bool ab = k0.mode == ISG_SINK_ACTBWD;
@@ -403,6 +405,7 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
         const int bns = ab ? k0.yns : k0.ns;
         const bool res = a.res_on != 0;  // lane-invariant; r is non-NULL then (host check)
         const bool res_old = res && k0.old != nullptr;
+        const bool res_p2a = res && k0.p2 != nullptr && k0.p2acc != 0;
 #pragma unroll
         for (int i = 0; i < TPW; ++i) {
             const int t = min(wave + 4 * i, nt_ - 1);
@@ -417,6 +420,7 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
                 pre[i][r] = gld(base, (int64_t)cl * a.HW + (int64_t)ne * bns + pixe);
                 if (res_old) pro[i][r] = gld(k0.old, (int64_t)cl * a.HW + (int64_t)ne * k0.ons + pixe);
                 if (res) prr[i][r] = gld(k0.r, (int64_t)cl * a.HW + (int64_t)ne * k0.rns + pixe);
+                if (res_p2a) pp2[i][r] = gld(k0.p2, (int64_t)cl * a.HW + (int64_t)ne * k0.p2ns + pixe);
             }
         }
     }
@@ -583,7 +587,8 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
                 }
                 gst(qi.p, off, gv);
                 if (SEG1 && a.res_on && ks.s0.p2)
-                    gst(ks.s0.p2, (int64_t)(rl + m0 - ks.s0.c0) * a.HW + (int64_t)ne * ks.s0.p2ns + pixe, gv);
+                    gst(ks.s0.p2, (int64_t)(rl + m0 - ks.s0.c0) * a.HW + (int64_t)ne * ks.s0.p2ns + pixe,
+                        ks.s0.p2acc ? pp2[i][r] + gv : gv);
                 s0[r] = gv;
                 s1[r] = gv * (y - qi.f.mean);
             }

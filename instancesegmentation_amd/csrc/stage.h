@@ -479,7 +479,7 @@ struct SinkLite {
     float *p, *p2;
     const float *y, *coef, *bias, *slope, *gamma, *beta, *r, *old;
     const double* stats;
-    int ns, yns, mode, act, c0, bnC, rns, ons, p2ns;
+    int ns, yns, mode, act, c0, bnC, rns, ons, p2ns, p2acc;
     float count, eps;
 };
 ISG_DEV SinkLite sink_lite(const isg_sink& k) {
@@ -494,6 +494,7 @@ ISG_DEV SinkLite sink_lite(const isg_sink& k) {
     l.r = sgpr_p(k.r); l.old = sgpr_p(k.old); l.p2 = sgpr_p(k.p2);
     l.rns = sgpr_i((int)k.r_n_stride); l.ons = sgpr_i((int)k.old_n_stride);
     l.p2ns = sgpr_i((int)k.p2_n_stride);
+    l.p2acc = sgpr_i(k.p2_accum);
     return l;
 }
 struct SkSel {

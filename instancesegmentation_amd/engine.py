@@ -855,16 +855,15 @@ class ConvOp:
         """The input-gradient sink that also runs the folded tail's backward (isg.h ACTBWD
         residual form), or None when the gradient bookkeeping does not allow it (then the
         tail runs its own backward): dL/d out must be this conv's input gradient plus at
-        most what later consumers accumulated over the whole buffer, and the residual
-        term's gradient buffer must not hold anything yet (the second output STOREs)."""
+        most what later consumers accumulated over the whole buffer (`old`); the residual
+        term's gradient goes out as the second output (p2: STORE when it is the first
+        contribution, else ACCUM)."""
         g, t = self.g, self.res_tail
         (y, _), (r, _) = t.terms
         C = t.out.C
         ini = gs.inited.get(id(t.out), set())
         if id(t.out) in gs.external or ini - {(0, C)} or id(y.buf) in gs.G:
             return None
-        if r.grad and (r.c0, r.C) in gs.inited.get(id(r.buf), set()):
-            return None  # the residual term's gradient already has a value: no STORE
         gb = gs.alloc(y.buf, "g_" + y.buf.name)
         gs.G[id(y.buf)] = gb
         s = {"p": gb.ptr(), "n_stride": gb.n_stride, "c0": 0, "C": C, "mode": L.SINK_ACTBWD,
@@ -880,9 +879,10 @@ class ConvOp:
             s["old_n_stride"] = d.n_stride
         if r.grad:
             db = gs.dbuf(r.buf)
-            gs.mark(r.buf, r.c0, r.C)
+            first = gs.mark(r.buf, r.c0, r.C)
             s["p2"] = db.ptr(r.c0)
             s["p2_n_stride"] = db.n_stride
+            s["p2_accum"] = 0 if first else 1
         if y.bn.fin:
             gs.pending_final.append(y.bn)
         t.bwd_folded = True

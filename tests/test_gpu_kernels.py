@@ -462,7 +462,7 @@ def test_pw_residual_fwd(cfg, act):
     close(ost[Co:2 * Co], (ref * ref).sum((0, 2, 3)), tol=4e-6, what="sumsq")
 
 
-@pytest.mark.parametrize("parts", ["old+p2", "old", "p2", "none"])
+@pytest.mark.parametrize("parts", ["old+p2", "old", "p2", "none", "old+p2acc"])
 @pytest.mark.parametrize("cfg", RES)
 def test_pw_residual_dgrad(cfg, parts):
     """Folded residual tail, backward: the 1x1 input gradient's ACTBWD sink in residual
@@ -490,13 +490,19 @@ def test_pw_residual_dgrad(cfg, parts):
           "r": ptr(XR), "r_n_stride": C * H * W}
     if "old" in parts:
         sk["old"], sk["old_n_stride"] = ptr(OLD), C * H * W
+    P2OLD = rnd(N, C, H, W, seed=88)
+    if "p2acc" in parts:  # the residual term's gradient already holds a part: p2 += g
+        P2.copy_(cuda32(P2OLD))
+        sk["p2_accum"] = 1
     if "p2" in parts:
         sk["p2"], sk["p2_n_stride"] = ptr(P2), C * H * W
     DZ, Wt = cuda32(dz), cuda32(w)  # kept alive: the call only sees their addresses
     dyseg = {"p": ptr(DZ), "n_stride": Co * H * W, "C": Co, "xform": L.XF_PLAIN}
     call("isg_conv_dgrad", geom(**ge), vt([dyseg], N, H, W), ptr(Wt), sinks([sk]), stream())
     close(GB, g, what="g (BN-output gradient of y)")
-    if "p2" in parts:
+    if "p2acc" in parts:
+        close(P2, g + P2OLD, what="p2 += g")
+    elif "p2" in parts:
         assert torch.equal(P2, GB), "p2 must hold the same g"
     else:
         assert torch.isnan(P2).all()
