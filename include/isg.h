@@ -226,6 +226,15 @@ int32_t isg_conv_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_
 int32_t isg_conv_wgrad_rep(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x,
                            double* dw, double* dbias, int64_t rep_stride, int32_t nrep,
                            isg_stream_t stream);
+/* Both backward halves of one depthwise layer (segment.py:63-64 groups=planes, the
+ * Bottleneck blocks' 3x3 / 5x1 / 1x5): dx through the one sink `dx` (as isg_conv_dgrad;
+ * NULL or nsink 0 skips it) and dw / dbias accumulated into replicas (as
+ * isg_conv_wgrad_rep; dw NULL skips it), in ONE launch when both tile kernels apply
+ * (same-size layer, W % 4 == 0, 16-B aligned sink rows): the dy tile is staged once. Same
+ * partials and reduction order as the two calls, so the results are bitwise theirs. */
+int32_t isg_depthwise_bwd(const isg_conv_geom* g, const isg_vtensor* dy, const float* w,
+                          const isg_sinks* dx, const isg_vtensor* x, double* dw, double* dbias,
+                          int64_t rep_stride, int32_t nrep, isg_stream_t stream);
 /* dst[i] = (float) sum_{r<nrep} src[r*stride + i] for i < n (fp64, fixed order). */
 int32_t isg_sum_replicas(float* dst, const double* src, int64_t n, int32_t nrep, int64_t stride,
                          isg_stream_t stream);
@@ -480,7 +489,7 @@ int32_t isg_exec_ms2(const void* ops, int32_t nops, void* const* table, isg_stre
 /* sizeof() of the ABI structs and executor records (0 vtensor, 1 sinks, 2 conv record,
  * 3 wgrad record, 4 pool record, 5 tail, 6 tail_grad, 7 bn_update, 8 grad_final,
  * 9 bce record, 10 conv_geom, 11 bn, 12 vseg, 13 sink, 14 sum_rep record, 15 kp_stem,
- * 16 mask_head) so
+ * 16 mask_head, 17 stamp record, 18 depthwise-backward record) so
  * bindings can verify layouts. */
 int32_t isg_record_size(int32_t which);
 

@@ -144,6 +144,12 @@ class StampRec(Structure):
     _fields_ = [("buf", c_void_p), ("slot", c_int32), ("sign", c_int32)]
 
 
+class DwBwdRec(Structure):
+    _fields_ = [("g", Geom), ("dy", VTensor), ("w", c_void_p), ("dx", Sinks), ("x", VTensor),
+                ("dw", c_void_p), ("dbias", c_void_p), ("rep_stride", c_int64), ("nrep", c_int32),
+                ("pad_", c_int32)]
+
+
 OP_CONV_FWD, OP_CONV_DGRAD, OP_CONV_WGRAD, OP_CONVT_FWD = 1, 2, 3, 4
 OP_MAXPOOL_FWD, OP_MAXPOOL_BWD, OP_TAIL_FWD, OP_TAIL_BWD = 5, 6, 7, 8
 OP_BN_UPDATE, OP_GRAD_FINAL, OP_BCE, OP_MEMSET = 9, 10, 11, 12
@@ -151,11 +157,12 @@ OP_SUM_REP, OP_BN_FINAL = 13, 14
 OP_KP_STEM_FWD, OP_KP_STEM_WGRAD, OP_KP_POOL = 15, 16, 17
 OP_HEAD_FWD, OP_HEAD_BWD = 18, 19
 OP_STAMP = 20
+OP_DW_BWD = 21
 
 _RECORD_CHECK = [(0, VTensor), (1, Sinks), (2, ConvRec), (3, WgradRec), (4, PoolRec), (5, Tail),
                  (6, TailGrad), (7, BnUpdate), (8, GradFinal), (9, BceRec), (10, Geom), (11, Bn),
                  (12, VSeg), (13, Sink), (14, SumRepRec), (15, KpStem), (16, MaskHead),
-                 (17, StampRec)]
+                 (17, StampRec), (18, DwBwdRec)]
 
 # exported symbol -> (restype, argtypes)
 SIGNATURES = {
@@ -166,6 +173,8 @@ SIGNATURES = {
     "isg_conv_wgrad_rep": (c_int32, [POINTER(Geom), POINTER(VTensor), POINTER(VTensor), c_void_p,
                                      c_void_p, c_int64, c_int32, c_void_p]),
     "isg_sum_replicas": (c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_int64, c_void_p]),
+    "isg_depthwise_bwd": (c_int32, [POINTER(Geom), POINTER(VTensor), c_void_p, POINTER(Sinks),
+                                    POINTER(VTensor), c_void_p, c_void_p, c_int64, c_int32, c_void_p]),
     "isg_convT_fwd": (c_int32, [POINTER(Geom), POINTER(VTensor), c_void_p, POINTER(Sinks), c_void_p]),
     "isg_maxpool_fwd": (c_int32, [POINTER(VTensor), c_int32, c_void_p, c_int64, c_void_p]),
     "isg_maxpool_bwd": (c_int32, [POINTER(VTensor), c_int32, c_void_p, c_int64, POINTER(Sinks),

@@ -207,6 +207,7 @@ enum {
     OP_HEAD_FWD = 18,
     OP_HEAD_BWD = 19,
     OP_STAMP = 20,
+    OP_DW_BWD = 21,
 };
 
 struct ConvRec {
@@ -259,6 +260,17 @@ struct BceRec {
 struct MemsetRec {
     void* p;
     int64_t bytes;
+};
+struct DwBwdRec {  // OP_DW_BWD: isg_depthwise_bwd
+    isg_conv_geom g;
+    isg_vtensor dy;
+    const float* w;
+    isg_sinks dx;
+    isg_vtensor x;
+    double* dw;
+    double* dbias;
+    int64_t rep_stride;
+    int32_t nrep, pad_;
 };
 struct StampRec {  // OP_STAMP: isg_stamp(buf, slot, sign)
     uint64_t* buf;
@@ -382,6 +394,12 @@ static int32_t run_op(int32_t kind, char* buf, isg_stream_t st) {
         case OP_HEAD_BWD:
             rc = isg_mask_head_bwd((const isg_mask_head*)buf, st);
             break;
+        case OP_DW_BWD: {
+            auto* r = (DwBwdRec*)buf;
+            rc = isg_depthwise_bwd(&r->g, &r->dy, r->w, &r->dx, &r->x, r->dw, r->dbias, r->rep_stride,
+                                   r->nrep, st);
+            break;
+        }
         case OP_STAMP: {
             auto* r = (StampRec*)buf;
             rc = isg_stamp(r->buf, r->slot, r->sign, st);
@@ -589,6 +607,7 @@ int32_t isg_record_size(int32_t which) {
         case 15: return (int32_t)sizeof(isg_kp_stem);
         case 16: return (int32_t)sizeof(isg_mask_head);
         case 17: return (int32_t)sizeof(StampRec);
+        case 18: return (int32_t)sizeof(DwBwdRec);
         default: return -1;
     }
 }

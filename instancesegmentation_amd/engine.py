@@ -943,6 +943,23 @@ class ConvOp:
         fl, xb, yb, wb = self._cost()
         dyb = yb * (2 if dy["xform"] == L.XF_BN_BWD else 1)  # g and y for BN backward
         dyv = vtensor([dy], g.N, ge["OH"], ge["OW"])
+        if (self.kind == "conv" and ge["groups"] > 1 and self.x.grad and self.kp is None
+                and len(self.x.segs) == 1 and os.environ.get("ISG_NO_DW_FUSE", "0") != "1"):
+            # a depthwise layer's input and weight gradients as ONE op on the main stream
+            # (isg_depthwise_bwd: the dy tile staged once; the weight gradient is no
+            # side-stream node of its own)
+            sk = sinks_spec([gs.sink_for(self.x.segs[0], 0, g.train)])
+            xv = vtensor([fwd_seg(self.x.segs[0], g.train)], g.N, ge["H"], ge["W"])
+            rec = {"g": ge, "dy": dyv, "w": g.tptr(self.mod, "weight"), "dx": sk, "x": xv,
+                   "dw": g.wrep_ptr(self.mod, "weight"), "rep_stride": g.pgrad_size,
+                   "nrep": L.WREP}
+            if self.mod.bias is not None and self.bnr is None:
+                rec["dbias"] = g.wrep_ptr(self.mod, "bias")
+            ops.add(Record(L.OP_DW_BWD, L.DwBwdRec, rec, label="dx_" + self.out.name,
+                           flops=2 * fl, nbytes=2 * dyb + 2 * xb + wb))
+            if self.mod.bias is not None and self.bnr is not None:
+                gs.bias_from_bn.append((self.mod, self.bnr))
+            return
         # ---- input gradient
         if self.x.grad:
             rs = self._res_sink(gs) if self.res_tail is not None else None

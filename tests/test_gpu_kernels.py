@@ -634,6 +634,63 @@ def test_depthwise(cfg):
     close(DB, dy.sum((0, 2, 3)), what="dw dbias")
 
 
+@pytest.mark.parametrize("cfg", DW_CFG)
+def test_depthwise_bwd_fused(cfg):
+    """isg_depthwise_bwd (one launch, the dy tile staged once) against the two calls it
+    replaces, bit for bit — dx through an ACTBWD sink with its BatchNorm-backward and PReLU
+    slope sums, the weight/bias-gradient replicas — with dy the BatchNorm backward of the
+    layer's output and x a BatchNorm + PReLU view; and the weight gradient against fp64."""
+    C, H, W, kh, kw, ph, pw, d = cfg
+    N = 2
+    ge = dict(N=N, Ci=C, H=H, W=W, Co=C, OH=H, OW=W, KH=kh, KW=kw, SH=1, SW=1, PH=ph, PW=pw,
+              DH=d, DW=d, groups=C)
+    yraw = rnd(N, C, H, W, seed=41) + 0.3
+    gbn = rnd(N, C, H, W, seed=42)
+    og, ob, st, _ = _bn_train_state(yraw, gbn, 43)
+    dy = _bn_bwd_ref(yraw, gbn, og)
+    x = rnd(N, C, H, W, seed=44)
+    gamma, beta, rm, rv, slope = bn_eval_params(C, 45)
+    xt = fwd_xform_ref(x, gamma, beta, rm, rv, slope, "prelu")
+    w = rnd(C, 1, kh, kw, seed=46, scale=0.4)
+    Yr, Gb, GA, BE, X, Wt = (cuda32(t) for t in (yraw, gbn, og, ob, x, w))
+    G = [cuda32(t) for t in (gamma, beta, rm, rv, slope)]
+    nw = C * kh * kw
+    stride_ = nw + C + 3
+
+    def run(fused):
+        ST = rep_from(st)
+        dyseg = {"p": ptr(Gb), "y": ptr(Yr), "n_stride": C * H * W, "y_n_stride": C * H * W,
+                 "C": C, "xform": L.XF_BN_BWD, "bn": bn_spec_train(GA, BE, ST, N * H * W)}
+        xseg = {"p": ptr(X), "n_stride": C * H * W, "C": C, "xform": L.XF_BN_FWD,
+                "act": L.ACT["prelu"], "slope": ptr(G[4]), "bn": bn_spec_eval(*G[:4])}
+        DX = torch.full((N, C, H, W), float("nan"), device=DEV)
+        IST, SG = rep_zeros(4 * C), rep_zeros(C)
+        bn_in = bn_spec_eval(*G[:4])
+        bn_in["stats"] = ptr(IST)
+        sk = sinks([{"p": ptr(DX), "n_stride": C * H * W, "c0": 0, "C": C, "mode": L.SINK_ACTBWD,
+                     "act": L.ACT["prelu"], "y": ptr(X), "y_n_stride": C * H * W,
+                     "slope": ptr(G[4]), "slope_grad": ptr(SG), "bn": bn_in}])
+        REP = torch.zeros(L.WREP * stride_, dtype=torch.float64, device=DEV)
+        if fused:
+            call("isg_depthwise_bwd", geom(**ge), vt([dyseg], N, H, W), ptr(Wt), sk,
+                 vt([xseg], N, H, W), ptr(REP), ptr(REP[nw:]), stride_, L.WREP, stream())
+        else:
+            call("isg_conv_dgrad", geom(**ge), vt([dyseg], N, H, W), ptr(Wt), sk, stream())
+            call("isg_conv_wgrad_rep", geom(**ge), vt([dyseg], N, H, W), vt([xseg], N, H, W),
+                 ptr(REP), ptr(REP[nw:]), stride_, L.WREP, stream())
+        return DX, IST, SG, REP
+
+    a, b = run(True), run(False)
+    for u, v, what in zip(a, b, ("dx", "BN-backward sums", "slope gradient", "dW replicas")):
+        assert not torch.isnan(u).any(), what
+        assert torch.equal(u, v), f"fused {what} differs from the separate calls"
+    OUT = torch.full((stride_,), float("nan"), device=DEV)
+    call("isg_sum_replicas", ptr(OUT), ptr(a[3]), stride_, L.WREP, stride_, stream())
+    wref = torch.nn.grad.conv2d_weight(xt, (C, 1, kh, kw), dy, padding=(ph, pw), dilation=d,
+                                       groups=C)
+    close(OUT[:nw].view(C, 1, kh, kw), wref, what="fused dw wgrad")
+
+
 @pytest.mark.parametrize("cfg", [(16, 16, 2, 16, 16), (4, 4, 2, 32, 24), (16, 4, 4, 16, 16)])
 def test_convT_fwd(cfg):
     Ci, Co, S, H, W = cfg

@@ -272,6 +272,25 @@ def test_residual_tails_fold_into_the_next_1x1(monkeypatch):
     assert len([r for r in q.bwd.recs if r.kind == L.OP_TAIL_BWD]) == len(tails_b) + len(bwd)
 
 
+def test_depthwise_backward_is_one_main_stream_op(monkeypatch):
+    """Every depthwise layer's backward is one OP_DW_BWD record (isg_depthwise_bwd: input
+    and weight gradient in one launch) on the main stream, with no depthwise weight gradient
+    left on the side streams; ISG_NO_DW_FUSE=1 restores the dgrad + side-stream wgrad pair."""
+    from instancesegmentation_amd.engine import ConvOp, Record
+    m = Segment(20)
+    p = Plan(m, [(2, 3, 128, 128), (2, 17, 3)], True, True, (False, False))
+    dws = [op for op in p.graph.ops if isinstance(op, ConvOp) and op.geom["groups"] > 1]
+    recs = [r for r in p.bwd.recs if r.kind == L.OP_DW_BWD]
+    assert len(recs) == len(dws) > 0
+    assert not any(r.flags & Record.OPF_SIDE for r in recs)
+    names = {"dw_" + op.out.name for op in dws}
+    assert not any(r.label in names for r in p.bwd.recs if r.kind == L.OP_CONV_WGRAD)
+    monkeypatch.setenv("ISG_NO_DW_FUSE", "1")
+    q = Plan(Segment(20), [(2, 3, 128, 128), (2, 17, 3)], True, True, (False, False))
+    assert not any(r.kind == L.OP_DW_BWD for r in q.bwd.recs)
+    assert sum(r.label in names for r in q.bwd.recs if r.kind == L.OP_CONV_WGRAD) == len(dws)
+
+
 @pytest.mark.parametrize("n", [1, 2])
 def test_forked_pools_join_before_any_reader_of_their_buffer(n):
     """engine._fork_pools at batch 1 and 2: the keypoint heatmaps' pool
