@@ -453,10 +453,20 @@ typedef struct {
     int32_t N, Hi, Wi;
     int32_t pad_;
     float* ring;                 /* [N][4][ISG_HEAD_RING(Hi, Wi)] (fwd: written if non-NULL; bwd: read) */
+    /* bwd: non-NULL = each workgroup STORES its fp32 dW1 partial here ([blocks][4096],
+     * isg_mask_head_part_floats) instead of adding it into dw1, and isg_mask_head_fold
+     * adds the partials into dw1's replicas later (off the critical path: the end-of-
+     * workgroup fp64 atomics of the 4096 dW1 values were the kernel's tail) */
+    float* dw1_part;
 } isg_mask_head;
 
 int32_t isg_mask_head_fwd(const isg_mask_head* a, isg_stream_t stream);
 int32_t isg_mask_head_bwd(const isg_mask_head* a, isg_stream_t stream);
+/* floats of the backward's dW1 partial slab for an N x 16 x Hi x Wi input */
+int64_t isg_mask_head_part_floats(int32_t N, int32_t Hi, int32_t Wi);
+/* dw1 replicas += the partial slab (fp64 sums of the fp32 partials: exact, so the result
+ * is the one of the in-kernel atomics, bit for bit) */
+int32_t isg_mask_head_fold(const isg_mask_head* a, isg_stream_t stream);
 
 /* ---- plan executor ------------------------------------------------------ */
 

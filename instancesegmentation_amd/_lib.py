@@ -99,7 +99,15 @@ class MaskHead(Structure):
                 ("b2", c_void_p), ("out", c_void_p), ("out_n_stride", c_int64), ("dout", c_void_p),
                 ("dout_n_stride", c_int64), ("dx", Sinks), ("dw1", c_void_p), ("db1", c_void_p),
                 ("dw2", c_void_p), ("db2", c_void_p), ("rep_stride", c_int64), ("nrep", c_int32),
-                ("N", c_int32), ("Hi", c_int32), ("Wi", c_int32), ("pad_", c_int32), ("ring", c_void_p)]
+                ("N", c_int32), ("Hi", c_int32), ("Wi", c_int32), ("pad_", c_int32), ("ring", c_void_p),
+                ("dw1_part", c_void_p)]
+
+
+def head_part_floats(N, Hi, Wi):
+    """isg_mask_head_part_floats: the backward's dW1 partial slab, [workgroups][4096] with one
+    workgroup per two 32 x 64 logit tiles, at most 256 (mask_head.hip head_bwd_blocks)."""
+    ntiles = N * -(-4 * Hi // 32) * -(-4 * Wi // 64)
+    return min((ntiles + 1) // 2, 256) * 4096
 
 
 def head_ring_floats(Hi, Wi):
@@ -158,6 +166,7 @@ OP_KP_STEM_FWD, OP_KP_STEM_WGRAD, OP_KP_POOL = 15, 16, 17
 OP_HEAD_FWD, OP_HEAD_BWD = 18, 19
 OP_STAMP = 20
 OP_DW_BWD = 21
+OP_HEAD_FOLD = 22
 
 _RECORD_CHECK = [(0, VTensor), (1, Sinks), (2, ConvRec), (3, WgradRec), (4, PoolRec), (5, Tail),
                  (6, TailGrad), (7, BnUpdate), (8, GradFinal), (9, BceRec), (10, Geom), (11, Bn),
@@ -210,6 +219,8 @@ SIGNATURES = {
     "isg_kp_pool": (c_int32, [POINTER(KpStem), c_void_p]),
     "isg_mask_head_fwd": (c_int32, [POINTER(MaskHead), c_void_p]),
     "isg_mask_head_bwd": (c_int32, [POINTER(MaskHead), c_void_p]),
+    "isg_mask_head_fold": (c_int32, [POINTER(MaskHead), c_void_p]),
+    "isg_mask_head_part_floats": (c_int64, [c_int32, c_int32, c_int32]),
     "isg_exec": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p]),
     "isg_exec_ms": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p]),
     "isg_exec_ms2": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p]),

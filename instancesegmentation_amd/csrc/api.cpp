@@ -208,6 +208,7 @@ enum {
     OP_HEAD_BWD = 19,
     OP_STAMP = 20,
     OP_DW_BWD = 21,
+    OP_HEAD_FOLD = 22,
 };
 
 struct ConvRec {
@@ -394,6 +395,9 @@ static int32_t run_op(int32_t kind, char* buf, isg_stream_t st) {
         case OP_HEAD_BWD:
             rc = isg_mask_head_bwd((const isg_mask_head*)buf, st);
             break;
+        case OP_HEAD_FOLD:
+            rc = isg_mask_head_fold((const isg_mask_head*)buf, st);
+            break;
         case OP_DW_BWD: {
             auto* r = (DwBwdRec*)buf;
             rc = isg_depthwise_bwd(&r->g, &r->dy, r->w, &r->dx, &r->x, r->dw, r->dbias, r->rep_stride,
@@ -441,13 +445,18 @@ int32_t isg_exec_ms2(const void* ops, int32_t nops, void* const* table, isg_stre
     std::vector<std::pair<int32_t, std::string>> pending;
     int pool_next = 0;
     int deal = 0;  // weight gradients alternate between the side streams across batches too
+    bool side_serial = false;  // a side-only batch ran on `side` since side 2 last waited for it
     auto launch = [&](Batch& bt) -> int32_t {
         // a batch of weight gradients only (independent accumulations into the replica
         // buffers) is dealt over both side streams: their grids (128-512 workgroups) leave
         // most of the chip idle one at a time; anything else keeps its order on stream 0
         bool spread = side2 != nullptr;
         for (auto& op : bt.ops)
-            spread = spread && (op.first == OP_CONV_WGRAD || op.first == OP_KP_STEM_WGRAD);
+            spread = spread && (op.first == OP_CONV_WGRAD || op.first == OP_KP_STEM_WGRAD ||
+                                op.first == OP_HEAD_FOLD || op.first == OP_GRAD_FINAL);
+        // a batch behind a side-only one (the gradient finalisation lists behind the replica
+        // fold at ISG_SIDE_CLOSE=1) may read what that one writes: it stays on `side`, in order
+        if (spread && side_serial) spread = false;
         if (hipStreamWaitEvent(side, bt.ev, 0) != hipSuccess ||
             (spread && hipStreamWaitEvent(side2, bt.ev, 0) != hipSuccess))
             return isg_check_launch("exec: fork side stream");
@@ -459,6 +468,7 @@ int32_t isg_exec_ms2(const void* ops, int32_t nops, void* const* table, isg_stre
             if (hipEventRecord(ev_join2, side2) != hipSuccess || hipStreamWaitEvent(side, ev_join2, 0) != hipSuccess)
                 return isg_check_launch("exec: order side stream after side stream 2");
         }
+        side_serial = side_serial || (!spread && side2 != nullptr);
         forked = true;
         forked2 = forked2 || spread;
         alignas(16) char pb[8192];
@@ -466,7 +476,9 @@ int32_t isg_exec_ms2(const void* ops, int32_t nops, void* const* table, isg_stre
         // its input-gradient chain) land on different side streams and overlap
         auto next_st = [&]() { return spread && (deal++ & 1) ? side2 : side; };
         bool all_wgrad = true;
-        for (auto& op : bt.ops) all_wgrad = all_wgrad && (op.first == OP_CONV_WGRAD || op.first == OP_KP_STEM_WGRAD);
+        for (auto& op : bt.ops)
+            all_wgrad = all_wgrad && (op.first == OP_CONV_WGRAD || op.first == OP_KP_STEM_WGRAD ||
+                                      op.first == OP_HEAD_FOLD);
         if (!pwg_group_on || !all_wgrad) {
             for (auto& op : bt.ops) {
                 std::memcpy(pb, op.second.data(), op.second.size());
@@ -519,6 +531,7 @@ int32_t isg_exec_ms2(const void* ops, int32_t nops, void* const* table, isg_stre
     };
     auto join = [&]() -> int32_t {
         if (int32_t e = close_batch()) return e;
+        side_serial = false;  // later forks start from the main stream, which waits for both
         if (forked) {
             forked = false;
             if (hipEventRecord(ev_join, side) != hipSuccess || hipStreamWaitEvent(main_st, ev_join, 0) != hipSuccess)

@@ -658,6 +658,47 @@ __global__ void grad_final_kernel(GradFinalList items, int nitems) {
 }
 
 // ---- sigmoid + BCE ----------------------------------------------------------------
+// the per-element arithmetic of bce_kernel below, one 16-B quad per thread: both loads in
+// flight at once and one pass (the strided loop waited out one load round trip per
+// element group: 21 us for the 2 x 1024^2 logits of the bench step)
+ISG_DEV float bce_elem(float x, float t, float grad_scale, float& g) {
+#pragma clang fp contract(off)
+    const float p = 1.f / (1.f + expf(-x));
+    float lp = logf(p);
+    float l1p = logf(1.f - p);
+    lp = lp < -100.f ? -100.f : lp;
+    l1p = l1p < -100.f ? -100.f : l1p;
+    float den = (1.f - p) * p;
+    den = den < 1e-12f ? 1e-12f : den;
+    const float gp = grad_scale * (p - t) / den;
+    g = gp * (1.f - p) * p;
+    return -(t * lp + (1.f - t) * l1p);
+}
+
+__global__ __launch_bounds__(kThreads) void bce4_kernel(const float* logits, const float* target,
+                                                         int64_t nq, double* loss_acc, float* dlogits,
+                                                         float grad_scale) {
+    __shared__ double sh[4];
+    const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    const bool ok = i < nq;
+    const f32x4 x = gld4(logits, 4 * (ok ? i : 0)), t = gld4(target, 4 * (ok ? i : 0));
+    double acc = 0.0;
+    f32x4 g;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        float ge;
+        const float l = bce_elem(x[e], t[e], grad_scale, ge);
+        g[e] = ge;
+        acc += ok ? (double)l : 0.0;
+    }
+    if (ok && dlogits) gst4(dlogits, 4 * i, g);
+    acc = wave_sum_d(acc);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) sh[wave] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(loss_acc, sh[0] + sh[1] + sh[2] + sh[3]);
+}
+
 __global__ __launch_bounds__(kThreads) void bce_kernel(const float* logits, const float* target,
                                                         int64_t n, double* loss_acc, float* dlogits,
                                                         float grad_scale) {
@@ -788,6 +829,27 @@ __global__ void fill_f64_kernel(double* p, int64_t n, double v) {
 
 // Fold the ISG_WREP weight-gradient replicas: dst[i] = sum_r src[r*stride + i] (fixed
 // order), 4 elements per lane with 16-B loads where the layout allows.
+// NREP replicas known at compile time: every replica's load of the thread's 2 elements is
+// issued before the first add (the runtime-count loop waited one round trip per replica:
+// 23 us for the 16 x 266k fp64 replicas of the bench step); summed in replica order
+template <int NREP>
+__global__ __launch_bounds__(kThreads) void sum_rep_n_kernel(float* __restrict__ dst,
+                                                             const double* __restrict__ src, int64_t n2,
+                                                             int64_t stride) {
+    typedef double f64x2 __attribute__((ext_vector_type(2)));
+    typedef const f64x2 __attribute__((address_space(1)))* gc2p;
+    const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (i >= n2) return;
+    f64x2 v[NREP];
+#pragma unroll
+    for (int r = 0; r < NREP; ++r) v[r] = *(gc2p)((const double __attribute__((address_space(1)))*)src + r * stride + 2 * i);
+    f64x2 a = v[0];
+#pragma unroll
+    for (int r = 1; r < NREP; ++r) a += v[r];
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    *(f32x2 __attribute__((address_space(1)))*)((gfloat_p)dst + 2 * i) = f32x2{(float)a[0], (float)a[1]};
+}
+
 __global__ __launch_bounds__(kThreads) void sum_rep_kernel(float* __restrict__ dst,
                                                             const double* __restrict__ src,
                                                             int64_t n, int nrep, int64_t stride) {
@@ -932,6 +994,13 @@ int32_t isg_grad_finalize(const isg_grad_final* items, int32_t nitems, isg_strea
 
 int32_t isg_bce_sigmoid(const float* logits, const float* target, int64_t n, double* loss_acc,
                         float* dlogits, float grad_scale, isg_stream_t st) {
+    auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+    if (n % 4 == 0 && n / 4 < ((int64_t)1 << 31) && al16(logits) && al16(target) && (!dlogits || al16(dlogits))) {
+        const int64_t q = n / 4;
+        hipLaunchKernelGGL(bce4_kernel, dim3((unsigned)((q + kThreads - 1) / kThreads)), dim3(kThreads), 0, st,
+                           logits, target, q, loss_acc, dlogits, grad_scale);
+        return isg_check_launch("bce4_kernel");
+    }
     hipLaunchKernelGGL(bce_kernel, dim3(grid_for(n, 1024)), dim3(kThreads), 0, st, logits, target, n,
                        loss_acc, dlogits, grad_scale);
     return isg_check_launch("bce_kernel");
@@ -976,6 +1045,14 @@ int32_t isg_sum_replicas(float* dst, const double* src, int64_t n, int32_t nrep,
     if (n <= 0) return 0;
     if (!dst || !src || nrep < 1 || (nrep > 1 && stride < n))
         return isg_set_error(ISG_ERR_INVALID, "sum_replicas: bad arguments");
+    if (n % 2 == 0 && (nrep == 1 || stride % 2 == 0) && ((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 7) == 0 &&
+        (nrep == 16 || nrep == 8 || nrep == 4)) {
+        const int64_t n2 = n / 2, b2 = (n2 + kThreads - 1) / kThreads;
+        if (nrep == 16) hipLaunchKernelGGL(sum_rep_n_kernel<16>, dim3((unsigned)b2), dim3(kThreads), 0, st, dst, src, n2, stride);
+        else if (nrep == 8) hipLaunchKernelGGL(sum_rep_n_kernel<8>, dim3((unsigned)b2), dim3(kThreads), 0, st, dst, src, n2, stride);
+        else hipLaunchKernelGGL(sum_rep_n_kernel<4>, dim3((unsigned)b2), dim3(kThreads), 0, st, dst, src, n2, stride);
+        return isg_check_launch("sum_rep_n_kernel");
+    }
     const int64_t blocks = ((n + 3) / 4 + kThreads - 1) / kThreads;
     hipLaunchKernelGGL(sum_rep_kernel, dim3((unsigned)blocks), dim3(kThreads), 0, st, dst, src, n,
                        nrep, stride);

@@ -679,7 +679,13 @@ __global__ __launch_bounds__(2 * kThreads, 1) void head_bwd_kernel(isg_mask_head
         STAMP(7);
         return;
     }
-    if (a.dw1) {
+    if (a.dw1_part) {  // the partial slab, folded later by isg_mask_head_fold (plain stores)
+        float* d = a.dw1_part + (int64_t)blockIdx.x * kW1;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) d[dw1_idx(t, i)] = dw1[t][i] + P1[dw1_idx(t, i)];
+    } else if (a.dw1) {
         double* d = a.dw1 + ro;
 #pragma unroll
         for (int t = 0; t < 4; ++t)
@@ -790,12 +796,48 @@ extern "C" int32_t isg_mask_head_fwd(const isg_mask_head* a, isg_stream_t st) {
     return isg_check_launch("head_fwd_kernel");
 }
 
+// the backward's workgroup count (1 two-tile workgroup per CU at most)
+static int head_bwd_blocks(int N, int Hi, int Wi) {
+    const int OH = 4 * Hi, OW = 4 * Wi;
+    const int ntiles = ((OW + TX - 1) / TX) * ((OH + TY - 1) / TY) * N;
+    return std::min((ntiles + 1) / 2, 256);
+}
+
+extern "C" int64_t isg_mask_head_part_floats(int32_t N, int32_t Hi, int32_t Wi) {
+    if (N < 1 || Hi < 1 || Wi < 1) return 0;
+    return (int64_t)head_bwd_blocks(N, Hi, Wi) * kW1;
+}
+
+// dw1[replica r][e] += sum of the rows of its row chunk r' (r = r' % nrep): a thread per
+// (element, 16-row chunk), fp64 sums of fp32 partials (exact, order-free)
+__global__ __launch_bounds__(256) void head_fold_kernel(const float* __restrict__ part, int rows,
+                                                        double* dw1, int64_t rep_stride, int nrep) {
+    const int e = blockIdx.x * 256 + threadIdx.x;  // < kW1 (grid.x = kW1 / 256)
+    const int r0 = blockIdx.y * 16;
+    double s = 0.0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s += r0 + r < rows ? (double)part[(int64_t)(r0 + r) * kW1 + e] : 0.0;
+    atomicAdd(&dw1[(int64_t)(blockIdx.y % (unsigned)nrep) * rep_stride + e], s);
+}
+
+extern "C" int32_t isg_mask_head_fold(const isg_mask_head* a, isg_stream_t st) {
+    if (!a || !a->dw1_part || !a->dw1 || a->N < 1 || a->Hi < 1 || a->Wi < 1)
+        return isg_set_error(ISG_ERR_INVALID, "mask head fold: NULL slab / dw1 or bad size");
+    if (a->nrep < 1 || (a->nrep > 1 && a->rep_stride <= 0))
+        return isg_set_error(ISG_ERR_INVALID, "mask head fold: bad replicas");
+    const int rows = head_bwd_blocks(a->N, a->Hi, a->Wi);
+    static_assert(kW1 % 256 == 0, "fold grid");
+    hipLaunchKernelGGL(head_fold_kernel, dim3(kW1 / 256, (rows + 15) / 16), dim3(256), 0, st, a->dw1_part,
+                       rows, a->dw1, a->nrep > 1 ? a->rep_stride : 0, a->nrep);
+    return isg_check_launch("head_fold_kernel");
+}
+
 extern "C" int32_t isg_mask_head_bwd(const isg_mask_head* a, isg_stream_t st) {
     if (int32_t e = check_head(a, true)) return e;
     const int OH = 4 * a->Hi, OW = 4 * a->Wi;
     const int ntx = (OW + TX - 1) / TX, nty = (OH + TY - 1) / TY;
     const int ntiles = ntx * nty * a->N;
-    const int grid = std::min((ntiles + 1) / 2, 256);  // 1 two-tile workgroup per CU
+    const int grid = head_bwd_blocks(a->N, a->Hi, a->Wi);
     if (head_bwd_vec(a))
         hipLaunchKernelGGL(head_bwd_kernel<true>, dim3(grid), dim3(2 * kThreads), 0, st, *a, ntx, nty, ntiles);
     else

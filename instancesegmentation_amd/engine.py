@@ -667,6 +667,9 @@ def _fork_late_wgrads(recs, late):
             recs[i], recs[i + 1] = b, a
 
 
+_GF_MAIN = os.environ.get("ISG_GRAD_FINAL_MAIN", "0") == "1"  # A/B: finalisation on the main stream
+
+
 def _fold_tails(g):
     """Residual tails folded into their first consumer: a tail
     out = act(BN(y) + x) (segment.py:75-77, 107-109, 259: BatchNorm'd raw conv output plus a
@@ -1133,12 +1136,21 @@ class HeadOp:
             s["db1"] = g.wrep_ptr(self.ct, "bias")
         if self.conv.bias is not None:
             s["db2"] = g.wrep_ptr(self.conv, "bias")
+        # the convT weight gradient's per-workgroup partials go to a slab folded into the
+        # replicas by a side-stream op (isg.h isg_mask_head.dw1_part): the kernel's tail was
+        # its 4096 fp64 atomics per workgroup
+        nslab = L.head_part_floats(g.N, self.x.H, self.x.W)
+        if nslab > 0 and os.environ.get("ISG_NO_HEAD_FOLD", "0") != "1":
+            part = gs.alloc(Buf(S_GRAD, 1, 1, 1, nslab, "head_dw1_part"), "head_dw1_part")
+            s["dw1_part"] = part.ptr()
         fl, nb = self._cost()
         # algorithmic: input gradient + both weight gradients = 2x the forward (SURVEY
         # §8d). The kernel does not recompute the 4-channel intermediate: the 3x3's weight
         # gradient comes from W1·Z' plus the forward's border ring (isg.h ISG_HEAD_RING).
         ops.add(Record(L.OP_HEAD_BWD, L.MaskHead, s, label="d_" + self.out.name,
                        flops=2 * fl, nbytes=nb + 4 * 16 * g.N * self.x.H * self.x.W))
+        if "dw1_part" in s:
+            ops.add(Record(L.OP_HEAD_FOLD, L.MaskHead, s, label="fold_" + self.out.name))
 
 
 class KpPoolOp:
@@ -1298,6 +1310,16 @@ class Plan:
         fw = OpList()
         if g.stats_size:
             fw.add(Record(L.OP_MEMSET, L.MemsetRec, {"p": Ptr(S_STATS), "bytes": g.stats_size * 8}))
+        self.wrep_zero_fwd = need_grad and os.environ.get("ISG_WREP_ZERO_BWD", "0") != "1"
+        if self.wrep_zero_fwd:
+            # the weight-gradient replicas (L.WREP fp64 copies of the flat gradient, 34 MB for
+            # Segment(20)) are zeroed on the side stream under the forward instead of at the
+            # head of the backward's critical path; the forward's final join covers it
+            r = Record(L.OP_MEMSET, L.MemsetRec, {"p": Ptr(S_WREP),
+                                                  "bytes": L.WREP * g.pgrad_size * 8},
+                       label="zero_wgrad_replicas")
+            r.flags |= Record.OPF_SIDE | Record.OPF_FORK_NOW
+            fw.add(r)
         side_recs = []
         for op in g.ops:
             i0 = len(fw.recs)
@@ -1408,10 +1430,12 @@ class Plan:
                 gs.external[id(b)] = Buf(S_DIN[i], b.N, b.C, b.H, b.W, f"din{i}")
         bw = OpList()
         # weight gradients accumulate (fp64 atomics of fp32 workgroup partials: exact, so
-        # order-independent, isg.h ISG_WREP) into L.WREP replicas, folded into S_PGRAD by
-        # OP_SUM_REP before the BN/PReLU finalisation overwrites its own entries
-        bw.add(Record(L.OP_MEMSET, L.MemsetRec, {"p": Ptr(S_WREP),
-                                                 "bytes": L.WREP * g.pgrad_size * 8}))
+        # order-independent, isg.h ISG_WREP) into L.WREP replicas — zeroed by the forward
+        # (its side-stream memset) — folded into S_PGRAD by OP_SUM_REP before the BN/PReLU
+        # finalisation overwrites its own entries
+        if not self.wrep_zero_fwd:  # A/B: the replicas zeroed at the head of the backward
+            bw.add(Record(L.OP_MEMSET, L.MemsetRec, {"p": Ptr(S_WREP),
+                                                     "bytes": L.WREP * g.pgrad_size * 8}))
         body = OpList()
         gs.pending_final = []
         for op in reversed(g.ops):
@@ -1420,7 +1444,7 @@ class Plan:
                 body.add(bn_final_record(gs.pending_final, True))
                 gs.pending_final = []
         for r in body.recs:
-            if r.kind in (L.OP_CONV_WGRAD, L.OP_KP_STEM_WGRAD):
+            if r.kind in (L.OP_CONV_WGRAD, L.OP_KP_STEM_WGRAD, L.OP_HEAD_FOLD):
                 r.flags |= Record.OPF_SIDE  # nothing later in the list reads a weight gradient
         _fork_late_wgrads(body.recs, self._late_prefix(g))
         self.din_written = [isinstance(v, Value) and v.grad and
@@ -1473,7 +1497,11 @@ class Plan:
                 recs.append(Record(L.OP_GRAD_FINAL, L.ListRec, {"n": len(chunk)}, L.GradFinal,
                                    chunk))
             for r in recs:
-                if side:
+                if side or (r.kind == L.OP_GRAD_FINAL and not _GF_MAIN):
+                    # the finalisation lists are independent of each other: forked behind
+                    # the fold, dealt over both side streams (api.cpp), joined at the end
+                    # of the list (5 launches of ~5 us each ran back to back on the main
+                    # stream at the very end of the step)
                     r.flags |= Record.OPF_SIDE | Record.OPF_FORK_NOW
                 ol.add(r)
 
@@ -1482,7 +1510,8 @@ class Plan:
         # backward runs last). The Trainer all-reduces bucket 1 on RCCL's stream while the
         # stem backward (body[split:]) runs. split == len(body): one bucket at the end.
         part1, part2 = OpList(), OpList()
-        part1.add(bw.recs[0])  # the replica memset
+        if bw.recs:
+            part1.add(bw.recs[0])  # the replica memset (ISG_WREP_ZERO_BWD=1)
         for r in body.recs[:split]:
             part1.add(r)
         if split < len(body.recs):
@@ -1495,7 +1524,7 @@ class Plan:
         else:
             cut = 0
             close(part1, 0, g.pgrad_size, [it for _, it in items])
-        for r in part1.recs[1:] + part2.recs:
+        for r in part1.recs[len(bw.recs):] + part2.recs:
             bw.add(r)
         self.bucket_cut = cut
         self.bwd_parts = [part1.compile()] + ([part2.compile()] if part2.recs else [])

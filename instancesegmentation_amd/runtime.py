@@ -98,10 +98,16 @@ class Runner:
                                    "device (call .to(device))")
         act = _arena(max(p.act_size, 1), torch.float32, dev)
         stats = _arena(p.stats_size, torch.float64, dev)
+        # the weight-gradient replicas: zeroed by the forward's side-stream memset (Plan), so
+        # they belong to this forward's saved state
+        wrep = _arena(L.WREP * max(p.graph.pgrad_size, 1), torch.float64, dev) \
+            if p.bwd is not None else None
         outs = [torch.empty(s, dtype=torch.float32, device=dev) for s in p.out_shapes]
         tab = self.table()
         tab[S_ACT] = act.data_ptr()
         tab[S_STATS] = stats.data_ptr()
+        if wrep is not None:
+            tab[S_WREP] = wrep.data_ptr()
         for i, x in enumerate(xs):
             tab[S_IN[i]] = x.data_ptr()
         for i, o in enumerate(outs):
@@ -110,15 +116,14 @@ class Runner:
             tab[S_TENSOR0 + j] = t.data_ptr()
         with torch.cuda.device(dev):
             p.fwd.run(tab, L.stream_ptr(dev))
-        return outs, (act, stats, xs, tensors)
+        return outs, (act, stats, xs, tensors, wrep)
 
     def backward(self, saved, douts, in_grad):
         p = self.plan
-        act, stats, xs, tensors = saved
+        act, stats, xs, tensors, wrep = saved
         dev = act.device
         grad = _arena(max(p.grad_size, 1), torch.float32, dev)
         pgrad = _arena(max(p.graph.pgrad_size, 1), torch.float32, dev)
-        wrep = _arena(L.WREP * max(p.graph.pgrad_size, 1), torch.float64, dev)
         dins = []
         for i, x in enumerate(xs):
             if in_grad[i]:

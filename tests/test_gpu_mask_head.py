@@ -87,3 +87,46 @@ def test_mask_head_fwd_bwd(N, Hi, Wi):
             "db2": _rel(tot[4136:4137], ref_g[4])}
     print({k: f"{v:.1e}" for k, v in errs.items()})
     assert all(v < 2e-5 for v in errs.values()), errs
+
+
+@pytest.mark.parametrize("N,Hi,Wi", [(2, 8, 16), (1, 17, 33), (2, 64, 64)])
+def test_mask_head_bwd_slab_fold_matches_atomics(N, Hi, Wi):
+    """The convT weight gradient through the per-workgroup slab (isg_mask_head.dw1_part)
+    and the later fold (isg_mask_head_fold, the train plan's side-stream op) equals the
+    in-kernel fp64 atomics bit for bit (both are exact fp64 sums of the same fp32
+    partials), and every other output is unchanged."""
+    x, w1, b1, w2, b2, dl = _case(N, Hi, Wi, 7 * Hi + Wi)
+    d = {k: v.to(DEV).contiguous() for k, v in dict(x=x, w1=w1, b1=b1, w2=w2, b2=b2, dl=dl).items()}
+    OH, OW = 4 * Hi, 4 * Wi
+    ring = torch.zeros(N, L.head_ring_floats(Hi, Wi), device=DEV)
+    base = {"x": {"s": [{"p": d["x"].data_ptr(), "n_stride": 16 * Hi * Wi, "C": 16,
+                         "xform": L.XF_PLAIN}], "nseg": 1, "N": N, "H": Hi, "W": Wi},
+            "w1": d["w1"].data_ptr(), "b1": d["b1"].data_ptr(), "w2": d["w2"].data_ptr(),
+            "b2": d["b2"].data_ptr(), "N": N, "Hi": Hi, "Wi": Wi, "ring": ring.data_ptr()}
+    out = torch.zeros(N, 1, OH, OW, device=DEV)
+    call("isg_mask_head_fwd", struct(L.MaskHead, dict(base, out=out.data_ptr(), out_n_stride=OH * OW)),
+         L.stream_ptr())
+    nslab = L.head_part_floats(N, Hi, Wi)
+    assert nslab == L.lib().isg_mask_head_part_floats(N, Hi, Wi)
+    R, nrep = 4096 + 4 + 36 + 1, L.WREP
+
+    def run(slab):
+        dx = torch.full((N, 16, Hi, Wi), float("nan"), device=DEV)
+        rep = torch.zeros(nrep * R, dtype=torch.float64, device=DEV)
+        part = torch.full((nslab,), float("nan"), device=DEV)
+        rp = rep.data_ptr()
+        sk = [{"p": dx.data_ptr(), "n_stride": 16 * Hi * Wi, "c0": 0, "C": 16, "mode": L.SINK_STORE}]
+        b = struct(L.MaskHead, dict(base, dout=d["dl"].data_ptr(), dout_n_stride=OH * OW,
+                                    dx={"s": sk, "nsink": 1}, dw1=rp, db1=rp + 8 * 4096,
+                                    dw2=rp + 8 * 4100, db2=rp + 8 * 4136, rep_stride=R, nrep=nrep,
+                                    dw1_part=part.data_ptr() if slab else None))
+        call("isg_mask_head_bwd", b, L.stream_ptr())
+        if slab:
+            call("isg_mask_head_fold", b, L.stream_ptr())
+        return dx, rep.view(nrep, R).sum(0)
+
+    (dxa, ta), (dxb, tb) = run(True), run(False)
+    assert torch.equal(dxa, dxb)
+    assert torch.equal(ta, tb), (ta - tb).abs().max().item()
+    ref_y, ref_g = _ref(x, w1, b1, w2, b2, dl)
+    assert _rel(ta[:4096].float().view(16, 4, 8, 8), ref_g[1]) < 2e-5

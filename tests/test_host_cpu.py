@@ -38,6 +38,14 @@ def test_library_exports_every_declared_symbol():
     assert lib.isg_stat_replicas() == L.STAT_REP
 
 
+def test_head_slab_size_matches_library():
+    """engine sizes the mask head's dW1 partial slab with _lib.head_part_floats, the Python
+    mirror of isg_mask_head_part_floats (mask_head.hip head_bwd_blocks)."""
+    lib = L.lib()
+    for n, h, w in [(2, 256, 256), (1, 5, 7), (2, 17, 33), (1, 120, 120), (4, 200, 336)]:
+        assert lib.isg_mask_head_part_floats(n, h, w) == L.head_part_floats(n, h, w), (n, h, w)
+
+
 def test_library_error_path_without_gpu():
     # an invalid geometry is rejected before any device work
     g = L.Geom()

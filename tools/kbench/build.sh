@@ -14,7 +14,7 @@ fi
 SRC=../../instancesegmentation_amd/csrc
 OUT=$PWD/_build
 mkdir -p $OUT
-FL="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -DISG_STAMPS -Wno-unused-function"
+FL="--offload-arch=gfx950 -O2 -fno-unroll-loops -std=c++17 -fPIC -DISG_STAMPS -Wno-unused-function"
 objs=""
 for s in $SRC/*.hip; do
   f=$(basename $s .hip)

@@ -77,7 +77,7 @@ def gpu_forward(params, fx):
     plan = Plan(m, [tuple(t.shape) for t in xs], True, False, tuple(False for _ in xs))
     run = Runner(m, plan)
     with torch.no_grad():
-        outs, (act, _, _, _) = run.forward(xs, module_tensors(m))
+        outs, (act, _, _, _, _) = run.forward(xs, module_tensors(m))
     torch.cuda.synchronize()
     return outs[0].double().cpu(), act.double().cpu(), plan
 
