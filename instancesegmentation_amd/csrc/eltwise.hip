@@ -675,23 +675,37 @@ ISG_DEV float bce_elem(float x, float t, float grad_scale, float& g) {
     return -(t * lp + (1.f - t) * l1p);
 }
 
+// kBceQ quads per thread (all loads in flight): the loss sum is one fp64 atomic per
+// workgroup on ONE address, which serialises — with a quad per thread (2048 workgroups at
+// the bench size) those atomics alone took ~30 us
+constexpr int kBceQ = 8;
 __global__ __launch_bounds__(kThreads) void bce4_kernel(const float* logits, const float* target,
                                                          int64_t nq, double* loss_acc, float* dlogits,
                                                          float grad_scale) {
     __shared__ double sh[4];
-    const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-    const bool ok = i < nq;
-    const f32x4 x = gld4(logits, 4 * (ok ? i : 0)), t = gld4(target, 4 * (ok ? i : 0));
-    double acc = 0.0;
-    f32x4 g;
+    const int64_t i0 = (int64_t)blockIdx.x * kThreads * kBceQ + threadIdx.x;
+    f32x4 x[kBceQ], t[kBceQ];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-        float ge;
-        const float l = bce_elem(x[e], t[e], grad_scale, ge);
-        g[e] = ge;
-        acc += ok ? (double)l : 0.0;
+    for (int u = 0; u < kBceQ; ++u) {
+        const int64_t i = i0 + (int64_t)u * kThreads;
+        x[u] = gld4(logits, 4 * (i < nq ? i : 0));
+        t[u] = gld4(target, 4 * (i < nq ? i : 0));
     }
-    if (ok && dlogits) gst4(dlogits, 4 * i, g);
+    double acc = 0.0;
+#pragma unroll
+    for (int u = 0; u < kBceQ; ++u) {
+        const int64_t i = i0 + (int64_t)u * kThreads;
+        const bool ok = i < nq;
+        f32x4 g;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            float ge;
+            const float l = bce_elem(x[u][e], t[u][e], grad_scale, ge);
+            g[e] = ge;
+            acc += ok ? (double)l : 0.0;
+        }
+        if (ok && dlogits) gst4(dlogits, 4 * i, g);
+    }
     acc = wave_sum_d(acc);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (lane == 0) sh[wave] = acc;
@@ -834,20 +848,17 @@ __global__ void fill_f64_kernel(double* p, int64_t n, double v) {
 // 23 us for the 16 x 266k fp64 replicas of the bench step); summed in replica order
 template <int NREP>
 __global__ __launch_bounds__(kThreads) void sum_rep_n_kernel(float* __restrict__ dst,
-                                                             const double* __restrict__ src, int64_t n2,
+                                                             const double* __restrict__ src, int64_t n,
                                                              int64_t stride) {
-    typedef double f64x2 __attribute__((ext_vector_type(2)));
-    typedef const f64x2 __attribute__((address_space(1)))* gc2p;
     const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-    if (i >= n2) return;
-    f64x2 v[NREP];
+    if (i >= n) return;
+    double v[NREP];
 #pragma unroll
-    for (int r = 0; r < NREP; ++r) v[r] = *(gc2p)((const double __attribute__((address_space(1)))*)src + r * stride + 2 * i);
-    f64x2 a = v[0];
+    for (int r = 0; r < NREP; ++r) v[r] = gld_d(src, r * stride + i);
+    double a = v[0];
 #pragma unroll
     for (int r = 1; r < NREP; ++r) a += v[r];
-    typedef float f32x2 __attribute__((ext_vector_type(2)));
-    *(f32x2 __attribute__((address_space(1)))*)((gfloat_p)dst + 2 * i) = f32x2{(float)a[0], (float)a[1]};
+    gst(dst, i, (float)a);
 }
 
 __global__ __launch_bounds__(kThreads) void sum_rep_kernel(float* __restrict__ dst,
@@ -997,7 +1008,8 @@ int32_t isg_bce_sigmoid(const float* logits, const float* target, int64_t n, dou
     auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
     if (n % 4 == 0 && n / 4 < ((int64_t)1 << 31) && al16(logits) && al16(target) && (!dlogits || al16(dlogits))) {
         const int64_t q = n / 4;
-        hipLaunchKernelGGL(bce4_kernel, dim3((unsigned)((q + kThreads - 1) / kThreads)), dim3(kThreads), 0, st,
+        hipLaunchKernelGGL(bce4_kernel, dim3((unsigned)((q + kThreads * kBceQ - 1) / (kThreads * kBceQ))),
+                           dim3(kThreads), 0, st,
                            logits, target, q, loss_acc, dlogits, grad_scale);
         return isg_check_launch("bce4_kernel");
     }
@@ -1045,12 +1057,11 @@ int32_t isg_sum_replicas(float* dst, const double* src, int64_t n, int32_t nrep,
     if (n <= 0) return 0;
     if (!dst || !src || nrep < 1 || (nrep > 1 && stride < n))
         return isg_set_error(ISG_ERR_INVALID, "sum_replicas: bad arguments");
-    if (n % 2 == 0 && (nrep == 1 || stride % 2 == 0) && ((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 7) == 0 &&
-        (nrep == 16 || nrep == 8 || nrep == 4)) {
-        const int64_t n2 = n / 2, b2 = (n2 + kThreads - 1) / kThreads;
-        if (nrep == 16) hipLaunchKernelGGL(sum_rep_n_kernel<16>, dim3((unsigned)b2), dim3(kThreads), 0, st, dst, src, n2, stride);
-        else if (nrep == 8) hipLaunchKernelGGL(sum_rep_n_kernel<8>, dim3((unsigned)b2), dim3(kThreads), 0, st, dst, src, n2, stride);
-        else hipLaunchKernelGGL(sum_rep_n_kernel<4>, dim3((unsigned)b2), dim3(kThreads), 0, st, dst, src, n2, stride);
+    if (nrep == 16 || nrep == 8 || nrep == 4) {
+        const int64_t b1 = (n + kThreads - 1) / kThreads;
+        if (nrep == 16) hipLaunchKernelGGL(sum_rep_n_kernel<16>, dim3((unsigned)b1), dim3(kThreads), 0, st, dst, src, n, stride);
+        else if (nrep == 8) hipLaunchKernelGGL(sum_rep_n_kernel<8>, dim3((unsigned)b1), dim3(kThreads), 0, st, dst, src, n, stride);
+        else hipLaunchKernelGGL(sum_rep_n_kernel<4>, dim3((unsigned)b1), dim3(kThreads), 0, st, dst, src, n, stride);
         return isg_check_launch("sum_rep_n_kernel");
     }
     const int64_t blocks = ((n + 3) / 4 + kThreads - 1) / kThreads;
