@@ -107,6 +107,10 @@ typedef struct {
      * written; 1x1 stride-1 conv forward with one segment only */
     float* mat;
     int64_t mat_n_stride;
+    /* the residual term's own BatchNorm (a tail of two BatchNorm'd conv outputs,
+     * segment.py:147-148, 202-207): when rbn.stats or rbn.coef is set the residual form
+     * reads act(BN(p) + BN2(y)) */
+    isg_bn rbn;
 } isg_vtensor;
 
 /* Where a kernel writes channels [c0, c0+C) of its result.
@@ -142,6 +146,8 @@ typedef struct {
     int64_t p2_n_stride;
     int32_t p2_accum;      /* p2 += g instead of p2 = g */
     int32_t pad2_;
+    isg_bn rbn;            /* ACTBWD residual form: the residual's own BatchNorm (stats or coef
+                              set): z = BN(y) + BN2(r); rbn.stats receives Σg and Σg(r - mean2) */
 } isg_sink;
 
 typedef struct {

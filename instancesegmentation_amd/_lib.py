@@ -38,7 +38,7 @@ class VSeg(Structure):
 
 class VTensor(Structure):
     _fields_ = [("s", VSeg * MAX_SEGS), ("nseg", c_int32), ("N", c_int32), ("H", c_int32),
-                ("W", c_int32), ("mat", c_void_p), ("mat_n_stride", c_int64)]
+                ("W", c_int32), ("mat", c_void_p), ("mat_n_stride", c_int64), ("rbn", Bn)]
 
 
 class Sink(Structure):
@@ -47,7 +47,7 @@ class Sink(Structure):
                 ("y", c_void_p), ("y_n_stride", c_int64), ("slope", c_void_p),
                 ("slope_grad", c_void_p), ("bn", Bn), ("r", c_void_p), ("r_n_stride", c_int64),
                 ("old", c_void_p), ("old_n_stride", c_int64), ("p2", c_void_p),
-                ("p2_n_stride", c_int64), ("p2_accum", c_int32), ("pad2_", c_int32)]
+                ("p2_n_stride", c_int64), ("p2_accum", c_int32), ("pad2_", c_int32), ("rbn", Bn)]
 
 
 class Sinks(Structure):

@@ -292,6 +292,7 @@ struct PwxArgs {
     int stat_on;                      // some channel or sink row evaluates its BN statistics
     int pre_on;                       // some sink reads an operand (ACTBWD y / ACCUM old value)
     int res_on;                       // the one sink is ACTBWD's residual form (isg.h isg_sink)
+    int rbn_in, rbn_out;              // ... with a BatchNorm'd residual (vtensor.rbn / sink rbn)
     int64_t P;
 };
 
@@ -305,12 +306,39 @@ struct PwxArgs {
 // SEG1: one source segment and one sink — the per-lane segment selection folds away (the
 // prologue's address arithmetic was the first phase's cost: ~1,250 instructions per wave
 // before the first barrier with three-way selects, 64-bit and runtime-divisor integer math)
-template <int TPW, int BP, bool HY, bool SEG1>
+// The residual term's own BatchNorm (isg.h vtensor.rbn / sink rbn) for one channel: its
+// coefficient or statistics loads in the caller's round trip (`on` lane-invariant: no
+// load at all on the common path), then (mean, gamma*rstd, beta)
+struct RbnLoad {
+    f32x4 f;
+    StatLoad<2> st;
+};
+ISG_DEV RbnLoad rbn_issue(const isg_bn& bn, int cl, const float* any, bool on) {
+    RbnLoad r;
+    const float* coef = sgpr_p((const float*)bn.coef);
+    r.f = f32x4{0.f, 1.f, 0.f, 0.f};
+    if (on && coef) r.f = gld4(coef, 4 * (int64_t)cl);
+    r.st = stat_issue<2>(coef ? nullptr : sgpr_p((const double*)bn.stats), sgpr_p(bn.gamma),
+                         sgpr_p(bn.beta), sgpr_i(bn.C), cl, any, on && !coef);
+    return r;
+}
+ISG_DEV ChanCoef rbn_finish(const isg_bn& bn, const RbnLoad& l) {
+    if (bn.coef) return ChanCoef{l.f[0], l.f[1], l.f[2], 0.f};
+    double mean, rstd;
+    mean_rstd_of(stat_sum(l.st, 0), stat_sum(l.st, 1), sgpr_f(bn.count), sgpr_f(bn.eps), mean, rstd);
+    return fwd_coef_of(mean, rstd, l.st.gamma, l.st.beta, 0.f);
+}
+
+// RES (SEG1 only): the one sink is ACTBWD's residual form — its extra operands and
+// reductions exist only in these instantiations (kept out of the common kernels, where
+// their live registers cost occupancy)
+template <int TPW, int BP, bool HY, bool SEG1, bool RES>
 __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
     extern __shared__ f32x4 pwx_smem[];
     char* const smem = reinterpret_cast<char*>(pwx_smem);
     ChSrc* const tabA = reinterpret_cast<ChSrc*>(smem);  // kThreads entries (clamped past K)
     ChanCoef* const tabK = reinterpret_cast<ChanCoef*>(smem + a.off_k);
+    ChanCoef* const tabK2 = tabK + a.K;  // residual BatchNorm: per channel (fwd) / per row (dgrad)
     RowInfo* const ri = reinterpret_cast<RowInfo*>(smem + a.off_ri);
     float* const As = reinterpret_cast<float*>(smem + a.off_a);
     float* const Xs = reinterpret_cast<float*>(smem + a.off_x);
@@ -370,6 +398,13 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
     const CoefLoad<HY ? 4 : 2> cfl = coef_issue<HY ? 4 : 2>(vs, tc, stat_on);
     const int trow = min(tid, Mb - 1);
     const SinkLoad skl = sink_issue(ks, m0 + trow, w, stat_on);
+    // the residual's BatchNorm: forward per input channel, input gradient per output row
+#ifdef ISG_NO_RBN_KERNEL  // A/B build (tools/build_variant.sh): the residual-BN code compiled out
+    const bool rbn_in = false, rbn_out = false;
+#else
+    const bool rbn_in = SEG1 && HY && a.rbn_in != 0, rbn_out = RES && a.rbn_out != 0;
+#endif
+
     // weight slot i -> (row, quad): quads per row padded to 2^wsh, so the split is a shift
     // and a mask; forward rows are m with k contiguous, dgrad rows are k with m contiguous.
     // Padding slots load a clamped duplicate and are dropped at the LDS store.
@@ -393,19 +428,24 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
     const int nt_ = (BM / 16) * CT_;
     // sink operands: y / old value, + the residual form's old gradient, residual term and
     // p2's old value
-    float pre[TPW][4], pro[TPW][4], prr[TPW][4], pp2[TPW][4];
+    constexpr int TR = RES ? TPW : 1;
+    float pre[TPW][4], pro[TR][4], prr[TR][4], pp2[TR][4];
 #pragma unroll
     for (int i = 0; i < TPW; ++i)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) pre[i][r] = pro[i][r] = prr[i][r] = pp2[i][r] = 0.f;
+        for (int r = 0; r < 4; ++r) pre[i][r] = 0.f;
+#pragma unroll
+    for (int i = 0; i < TR; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pro[i][r] = prr[i][r] = pp2[i][r] = 0.f;
     if (SEG1 && a.pre_on) {
         const SinkLite& k0 = ks.s0;
         const bool ab = k0.mode == ISG_SINK_ACTBWD;
         const float* base = ab ? k0.y : k0.p;
         const int bns = ab ? k0.yns : k0.ns;
-        const bool res = a.res_on != 0;  // lane-invariant; r is non-NULL then (host check)
-        const bool res_old = res && k0.old != nullptr;
-        const bool res_p2a = res && k0.p2 != nullptr && k0.p2acc != 0;
+        // lane-invariant; r is non-NULL in the residual form (host check)
+        const bool res_old = RES && k0.old != nullptr;
+        const bool res_p2a = RES && k0.p2 != nullptr && k0.p2acc != 0;
 #pragma unroll
         for (int i = 0; i < TPW; ++i) {
             const int t = min(wave + 4 * i, nt_ - 1);
@@ -418,15 +458,26 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
             for (int r = 0; r < 4; ++r) {
                 const int cl = min(rt * 16 + kk * 4 + r, Mb - 1) + m0 - k0.c0;
                 pre[i][r] = gld(base, (int64_t)cl * a.HW + (int64_t)ne * bns + pixe);
-                if (res_old) pro[i][r] = gld(k0.old, (int64_t)cl * a.HW + (int64_t)ne * k0.ons + pixe);
-                if (res) prr[i][r] = gld(k0.r, (int64_t)cl * a.HW + (int64_t)ne * k0.rns + pixe);
-                if (res_p2a) pp2[i][r] = gld(k0.p2, (int64_t)cl * a.HW + (int64_t)ne * k0.p2ns + pixe);
+                if constexpr (RES) {
+                    if (res_old) pro[i][r] = gld(k0.old, (int64_t)cl * a.HW + (int64_t)ne * k0.ons + pixe);
+                    prr[i][r] = gld(k0.r, (int64_t)cl * a.HW + (int64_t)ne * k0.rns + pixe);
+                    if (res_p2a) pp2[i][r] = gld(k0.p2, (int64_t)cl * a.HW + (int64_t)ne * k0.p2ns + pixe);
+                }
             }
         }
     }
     __syncthreads();
     STAMP(1);
     // phase-1 results -> LDS (waits for phase-1 loads only)
+    // the residual's own BatchNorm (two-BN tails only, 4 launches per step): its own round
+    // trip inside a uniform branch, so no state of it stays live in the common kernels
+    if (rbn_in) {
+        const RbnLoad rbl = rbn_issue(a.src.rbn, tc, w, true);
+        if (tid < K) tabK2[tid] = rbn_finish(a.src.rbn, rbl);
+    } else if (rbn_out) {
+        const RbnLoad rbl = rbn_issue(a.out.s[0].rbn, trow + m0 - a.out.s[0].c0, w, true);
+        if (tid < Mb) tabK2[tid] = rbn_finish(a.out.s[0].rbn, rbl);
+    }
     if (a.fast) {
         if (tid < K) tabK[tid] = coef_finish(vs, tid, cfl);
         if (tid < Mb) {
@@ -470,8 +521,14 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
             f32x4 o;
             if constexpr (HY) {  // BN_FWD with a residual term (isg_vseg): y is the residual
                 const float isr = t.xf == ISG_XF_BN_FWD && t.y != t.p ? 1.f : 0.f;
+                f32x4 rv = yv[u];
+                if (rbn_in) {  // the residual's own BatchNorm, the tail's (x - mean) * k + beta
+                    const ChanCoef k2 = tabK2[c < K ? c : K - 1];
 #pragma unroll
-                for (int e = 0; e < 4; ++e) o[e] = xf_lin_apply_r(l, xv[u][e], yv[u][e], isr);
+                    for (int e = 0; e < 4; ++e) rv[e] = (rv[e] - k2.c0) * k2.c1 + k2.c2;
+                }
+#pragma unroll
+                for (int e = 0; e < 4; ++e) o[e] = xf_lin_apply_r(l, xv[u][e], rv[e], isr);
             } else {
 #pragma unroll
                 for (int e = 0; e < 4; ++e) o[e] = xf_lin_apply(l, xv[u][e], xv[u][e]);
@@ -536,10 +593,10 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
         }
     }
     const bool need_red = sinks_need_red(a.out);
-    float (*red)[3][kMaxBM] = reinterpret_cast<float (*)[3][kMaxBM]>(Xs);
+    float (*red)[4][kMaxBM] = reinterpret_cast<float (*)[4][kMaxBM]>(Xs);
     if (need_red) {
         __syncthreads();  // every wave is past its Xs reads
-        for (int i = tid; i < 4 * 3 * kMaxBM; i += kThreads) (&red[0][0][0])[i] = 0.f;
+        for (int i = tid; i < 4 * 4 * kMaxBM; i += kThreads) (&red[0][0][0])[i] = 0.f;
         __syncthreads();
     }
     STAMP(5);
@@ -553,10 +610,10 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
         const bool pve = pe < a.P;
         const int ne = pve ? (int)((uint32_t)pe / (uint32_t)a.HW) : 0;
         const int pixe = pve ? (int)pe - ne * a.HW : 0;
-        float s0[4], s1[4], s2[4];
+        float s0[4], s1[4], s2[4], s3[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            s0[r] = s1[r] = s2[r] = 0.f;
+            s0[r] = s1[r] = s2[r] = s3[r] = 0.f;
             const int rl = rt * 16 + kk * 4 + r;
             const RowInfo& qi = ri[rl];
             if (!pve || qi.mode < 0 || qi.mode == ISG_SINK_NONE) continue;
@@ -574,9 +631,15 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
             } else {
                 const float y = pre[i][r];
                 float z = (y - qi.f.mean) * qi.f.scale + qi.f.beta;
-                if (SEG1 && a.res_on) {  // residual form: + old gradient, + residual term
+                ChanCoef k2 = {0.f, 1.f, 0.f, 0.f};
+                if constexpr (RES) {  // residual form: + old gradient, + residual term
                     v = pro[i][r] + v;
-                    z = z + prr[i][r];
+                    float rv = prr[i][r];
+                    if (rbn_out) {  // the residual's own BatchNorm (two-BN tail)
+                        k2 = tabK2[rl];
+                        rv = (rv - k2.c0) * k2.c1 + k2.c2;
+                    }
+                    z = z + rv;
                 }
                 float gv = v;
                 if (qi.act == ISG_ACT_RELU) {
@@ -586,9 +649,12 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
                     s2[r] = z > 0.f ? 0.f : z * v;
                 }
                 gst(qi.p, off, gv);
-                if (SEG1 && a.res_on && ks.s0.p2)
-                    gst(ks.s0.p2, (int64_t)(rl + m0 - ks.s0.c0) * a.HW + (int64_t)ne * ks.s0.p2ns + pixe,
-                        ks.s0.p2acc ? pp2[i][r] + gv : gv);
+                if constexpr (RES) {
+                    if (ks.s0.p2)
+                        gst(ks.s0.p2, (int64_t)(rl + m0 - ks.s0.c0) * a.HW + (int64_t)ne * ks.s0.p2ns + pixe,
+                            ks.s0.p2acc ? pp2[i][r] + gv : gv);
+                    if (rbn_out) s3[r] = gv * (prr[i][r] - k2.c0);  // centred on the residual's mean
+                }
                 s0[r] = gv;
                 s1[r] = gv * (y - qi.f.mean);
             }
@@ -599,11 +665,13 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
                 const float t0 = row16_sum(s0[r]);
                 const float t1 = row16_sum(s1[r]);
                 const float t2 = row16_sum(s2[r]);
+                const float t3 = rbn_out ? row16_sum(s3[r]) : 0.f;
                 const int rl = rt * 16 + kk * 4 + r;
                 if (pl == 0 && rl < Mb) {
                     red[wave][0][rl] += t0;
                     red[wave][1][rl] += t1;
                     red[wave][2][rl] += t2;
+                    red[wave][3][rl] += t3;
                 }
             }
         }
@@ -613,9 +681,16 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
         STAMP(6);
         for (int rl = tid; rl < Mb; rl += kThreads) {
 #pragma unroll
-            for (int j = 0; j < 3; ++j)
+            for (int j = 0; j < 4; ++j)
                 red[0][j][rl] = ((red[0][j][rl] + red[1][j][rl]) + red[2][j][rl]) + red[3][j][rl];
             sink_row_flush(a.out, m0 + rl, red[0][0][rl], red[0][1][rl], red[0][2][rl]);
+            if (rbn_out && a.out.s[0].rbn.stats) {  // the residual BatchNorm's backward sums
+                const isg_sink& k = a.out.s[0];
+                double* sp = rep_ptr(k.rbn.stats, 4 * k.rbn.C);
+                const int cl = m0 + rl - k.c0;
+                atomicAdd(&sp[2 * k.rbn.C + cl], (double)red[0][0][rl]);
+                atomicAdd(&sp[3 * k.rbn.C + cl], (double)red[0][3][rl]);
+            }
         }
     }
     STAMP(7);
@@ -631,17 +706,18 @@ int pwx_lds(int K, int Kp, int BM, int BP, int& off_k, int& off_ri, int& off_a, 
     AS = Kp + ((8 - Kp % 64) + 64) % 64;
     XS = BP + ((16 - BP % 32) + 32) % 32;  // 16 mod 32 banks
     off_k = pwx_align16(kThreads * (int)sizeof(ChSrc));
-    off_ri = pwx_align16(off_k + K * (int)sizeof(ChanCoef));
+    // tabK, then the residual BatchNorm's per-channel / per-row coefficients (two-BN tails)
+    off_ri = pwx_align16(off_k + (K + std::max(K, BM)) * (int)sizeof(ChanCoef));
     off_a = pwx_align16(off_ri + BM * (int)sizeof(RowInfo));
     off_x = pwx_align16(off_a + BM * AS * (int)sizeof(float));
     // the epilogue's BN partials [4][3][kMaxBM] reuse the slab
-    const int xbytes = std::max(Kp * XS, 4 * 3 * kMaxBM) * (int)sizeof(float);
+    const int xbytes = std::max(Kp * XS, 4 * 4 * kMaxBM) * (int)sizeof(float);
     return off_x + xbytes;
 }
 
-template <int TPW, int BP, bool HY, bool SEG1>
+template <int TPW, int BP, bool HY, bool SEG1, bool RES>
 int32_t pwx_launch(const PwxArgs& a, dim3 grid, int lds, hipStream_t st) {
-    auto k = pwx_kernel<TPW, BP, HY, SEG1>;
+    auto k = pwx_kernel<TPW, BP, HY, SEG1, RES>;
     static bool attr = false;
     if (!attr) {
         if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, kPxMaxLds) != hipSuccess)
@@ -652,21 +728,22 @@ int32_t pwx_launch(const PwxArgs& a, dim3 grid, int lds, hipStream_t st) {
     return isg_check_launch("pwx_kernel");
 }
 
-template <int BP, bool HY, bool SEG1>
+template <int BP, bool HY, bool SEG1, bool RES>
 int32_t pwx_dispatch(const PwxArgs& a, dim3 grid, int lds, int tpw, hipStream_t st) {
     switch (tpw) {
-        case 1: return pwx_launch<1, BP, HY, SEG1>(a, grid, lds, st);
-        case 2: return pwx_launch<2, BP, HY, SEG1>(a, grid, lds, st);
-        case 3: return pwx_launch<3, BP, HY, SEG1>(a, grid, lds, st);
-        case 4: return pwx_launch<4, BP, HY, SEG1>(a, grid, lds, st);
-        case 5: case 6: return pwx_launch<6, BP, HY, SEG1>(a, grid, lds, st);
-        default: return pwx_launch<8, BP, HY, SEG1>(a, grid, lds, st);
+        case 1: return pwx_launch<1, BP, HY, SEG1, RES>(a, grid, lds, st);
+        case 2: return pwx_launch<2, BP, HY, SEG1, RES>(a, grid, lds, st);
+        case 3: return pwx_launch<3, BP, HY, SEG1, RES>(a, grid, lds, st);
+        case 4: return pwx_launch<4, BP, HY, SEG1, RES>(a, grid, lds, st);
+        case 5: case 6: return pwx_launch<6, BP, HY, SEG1, RES>(a, grid, lds, st);
+        default: return pwx_launch<8, BP, HY, SEG1, RES>(a, grid, lds, st);
     }
 }
 template <int BP, bool HY>
 int32_t pwx_dispatch_seg(const PwxArgs& a, dim3 grid, int lds, int tpw, bool seg1, hipStream_t st) {
-    return seg1 ? pwx_dispatch<BP, HY, true>(a, grid, lds, tpw, st)
-                : pwx_dispatch<BP, HY, false>(a, grid, lds, tpw, st);
+    if (a.res_on) return pwx_dispatch<BP, HY, true, true>(a, grid, lds, tpw, st);  // host: seg1
+    return seg1 ? pwx_dispatch<BP, HY, true, false>(a, grid, lds, tpw, st)
+                : pwx_dispatch<BP, HY, false, false>(a, grid, lds, tpw, st);
 }
 // weight quads per row padded to a power of two (pwx_kernel's slot split), and the rows
 int pwx_wrow_quads(int wmode, int BM, int Kp) {
@@ -903,14 +980,16 @@ int32_t isg_pw_gemm(const isg_conv_geom* g, const isg_vtensor* src, const float*
         return isg_set_error(ISG_ERR_UNSUPPORTED, "pw gemm: M = %d rows", a.M);
     // a folded residual tail (isg.h: BN_FWD segment with y / vtensor.mat in the forward,
     // ACTBWD sink's residual form in the input gradient) runs on the slab kernel only
-    bool res_in = src->mat != nullptr, res_out = false;
+    const bool rbn_src = src->rbn.stats || src->rbn.coef;
+    bool res_in = src->mat != nullptr || rbn_src, res_out = false;
     for (int s = 0; s < src->nseg; ++s) res_in |= src->s[s].xform == ISG_XF_BN_FWD && src->s[s].y;
     for (int s = 0; s < out->nsink; ++s) {
         const isg_sink& k = out->s[s];
-        res_out |= k.r || k.old || k.p2;
+        res_out |= k.r || k.old || k.p2 || k.rbn.stats || k.rbn.coef;
     }
     const bool res = res_in || res_out;
     if (res && ((res_in && dgrad) ||
+                (res_in && rbn_src && !(src->s[0].xform == ISG_XF_BN_FWD && src->s[0].y)) ||
                 (res_out && (!dgrad || out->s[0].mode != ISG_SINK_ACTBWD || !out->s[0].r)) ||
                 src->nseg != 1 || out->nsink != 1))
         return isg_set_error(ISG_ERR_UNSUPPORTED, "pw gemm: residual forms need one segment and one "
@@ -947,6 +1026,9 @@ int32_t isg_pw_gemm(const isg_conv_geom* g, const isg_vtensor* src, const float*
         b.fast = host_vt_fast(*src) && host_sinks_fast(*out);
         b.pre_on = 0;
         b.res_on = res_out ? 1 : 0;
+        auto bn_on = [](const isg_bn& q) { return q.stats != nullptr || q.coef != nullptr; };
+        b.rbn_in = res_in && bn_on(src->rbn) ? 1 : 0;
+        b.rbn_out = res_out && bn_on(out->s[0].rbn) ? 1 : 0;
         for (int s = 0; s < out->nsink; ++s)
             if (out->s[s].mode == ISG_SINK_ACTBWD || out->s[s].mode == ISG_SINK_ACCUM) b.pre_on = 1;
         b.stat_on = 0;

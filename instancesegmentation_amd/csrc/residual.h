@@ -7,13 +7,14 @@
 inline bool isg_seg_res(const isg_vseg& s) { return s.xform == ISG_XF_BN_FWD && s.y; }
 inline bool isg_vt_res(const isg_vtensor* v) {
     if (!v) return false;
-    bool r = v->mat != nullptr;
+    bool r = v->mat != nullptr || v->rbn.stats != nullptr || v->rbn.coef != nullptr;
     for (int i = 0; i < v->nseg && i < ISG_MAX_SEGS; ++i) r |= isg_seg_res(v->s[i]);
     return r;
 }
 inline bool isg_sinks_res(const isg_sinks* k) {
     if (!k) return false;
     bool r = false;
-    for (int i = 0; i < k->nsink && i < ISG_MAX_SEGS; ++i) r |= k->s[i].r || k->s[i].old || k->s[i].p2;
+    for (int i = 0; i < k->nsink && i < ISG_MAX_SEGS; ++i)
+        r |= k->s[i].r || k->s[i].old || k->s[i].p2 || k->s[i].rbn.stats || k->s[i].rbn.coef;
     return r;
 }

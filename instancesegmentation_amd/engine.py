@@ -693,7 +693,12 @@ def _fold_tails(g):
             continue
         (y, upy), (r, upr) = t.terms
         C = t.out.C
-        if upy or upr or y.bn is None or y.act != "none" or r.virtual or t.c0 != 0:
+        # the residual: a materialised value, or a second BatchNorm'd conv output (the
+        # BottleneckDown2 / BottleneckDim_Res tails, segment.py:147-148, 202-207)
+        r_ok = not r.virtual or (r.bn is not None and r.act == "none" and r.c0 == 0
+                                 and r.C == r.buf.C and r.buf is not y.buf
+                                 and os.environ.get("ISG_NO_RBN_FOLD", "0") != "1")
+        if upy or upr or y.bn is None or y.act != "none" or not r_ok or t.c0 != 0:
             continue
         if t.out.slot != S_ACT or y.C != C or r.C != C or y.c0 != 0 or y.buf.C != C:
             continue
@@ -852,6 +857,8 @@ class ConvOp:
         vt = vtensor([seg], g.N, self.geom["H"], self.geom["W"])
         vt["mat"] = t.out.ptr()
         vt["mat_n_stride"] = t.out.n_stride
+        if r.bn is not None:  # a BatchNorm'd residual: act(BN(y) + BN2(r))
+            vt["rbn"] = bn_spec(r.bn, g.train)
         return vt
 
     def _res_sink(self, gs):
@@ -867,6 +874,8 @@ class ConvOp:
         ini = gs.inited.get(id(t.out), set())
         if id(t.out) in gs.external or ini - {(0, C)} or id(y.buf) in gs.G:
             return None
+        if r.bn is not None and id(r.buf) in gs.G:
+            return None
         gb = gs.alloc(y.buf, "g_" + y.buf.name)
         gs.G[id(y.buf)] = gb
         s = {"p": gb.ptr(), "n_stride": gb.n_stride, "c0": 0, "C": C, "mode": L.SINK_ACTBWD,
@@ -880,7 +889,14 @@ class ConvOp:
             d = gs.dbuf(t.out)
             s["old"] = d.ptr()
             s["old_n_stride"] = d.n_stride
-        if r.grad:
+        if r.bn is not None:
+            # a BatchNorm'd residual: its BN-output gradient is the same g (the tail's
+            # backward gives both BN terms one buffer), its backward sums go to its own stats
+            gs.G[id(r.buf)] = gb
+            s["rbn"] = bn_spec(r.bn, g.train)
+            if r.bn.fin:
+                gs.pending_final.append(r.bn)
+        elif r.grad:
             db = gs.dbuf(r.buf)
             first = gs.mark(r.buf, r.c0, r.C)
             s["p2"] = db.ptr(r.c0)

@@ -413,20 +413,35 @@ def test_pw_bn_bwd_y_null(cfg):
 RES = [(48, 16, 32, 32), (128, 48, 16, 16), (48, 16, 20, 12)]
 
 
-def _res_state(C, N, H, W, seed):
-    """raw y, residual x, BN parameters and train statistics [sum | sumsq | 0 | 0] of y."""
+def _bn_train_view(t, gamma, beta):
+    """(train-mode BatchNorm of t, its statistics block [sum | sumsq | 0 | 0], mean)."""
+    C = t.shape[1]
+    st = torch.cat([t.sum((0, 2, 3)), (t * t).sum((0, 2, 3)), torch.zeros(2 * C, dtype=torch.float64)])
+    mean = t.mean((0, 2, 3))
+    rstd = 1 / torch.sqrt(t.var((0, 2, 3), unbiased=False) + 1e-5)
+    return (t - mean[None, :, None, None]) * (gamma * rstd)[None, :, None, None] \
+        + beta[None, :, None, None], st, mean
+
+
+def _res_state(C, N, H, W, seed, rbn=False):
+    """raw y, residual x, BN parameters and train statistics [sum | sumsq | 0 | 0] of y;
+    rbn: the residual is itself a raw conv output with its own train-mode BatchNorm
+    (returned as (gamma2, beta2, stats2, mean2))."""
     y = rnd(N, C, H, W, seed=seed) + 0.3
     xr = rnd(N, C, H, W, seed=seed + 1)
     gamma, beta, _, _, slope = bn_eval_params(C, seed + 2)
-    st = torch.cat([y.sum((0, 2, 3)), (y * y).sum((0, 2, 3)), torch.zeros(2 * C, dtype=torch.float64)])
-    mean = y.mean((0, 2, 3))
-    rstd = 1 / torch.sqrt(y.var((0, 2, 3), unbiased=False) + 1e-5)
-    z = (y - mean[None, :, None, None]) * (gamma * rstd)[None, :, None, None] \
-        + beta[None, :, None, None] + xr
-    return y, xr, gamma, beta, slope, st, mean, z
+    by, st, mean = _bn_train_view(y, gamma, beta)
+    r2 = None
+    rv = xr
+    if rbn:
+        xr = xr * 0.7 - 0.2
+        g2, b2, _, _, _ = bn_eval_params(C, seed + 3)
+        rv, st2, mean2 = _bn_train_view(xr, g2, b2)
+        r2 = (g2, b2, st2, mean2)
+    return y, xr, gamma, beta, slope, st, mean, by + rv, r2
 
 
-@pytest.mark.parametrize("act", ["prelu", "relu"])
+@pytest.mark.parametrize("act", ["prelu", "relu", "prelu-rbn"])
 @pytest.mark.parametrize("cfg", RES)
 def test_pw_residual_fwd(cfg, act):
     """Folded residual tail, forward: a 1x1 conv reading act(BN(y) + x) on load (BN_FWD
@@ -436,7 +451,9 @@ def test_pw_residual_fwd(cfg, act):
     C, Co, H, W = cfg
     N = 2
     ge, _, _ = _geom(N, C, Co, H, W, 1, 1, 0, 1)
-    y, xr, gamma, beta, slope, st, _, z = _res_state(C, N, H, W, 71)
+    rbn = act.endswith("-rbn")
+    act = act.split("-")[0]
+    y, xr, gamma, beta, slope, st, _, z, r2 = _res_state(C, N, H, W, 71, rbn)
     v = torch.where(z > 0, z, z * slope[None, :, None, None]) if act == "prelu" else z.clamp_min(0)
     w = rnd(Co, C, 1, 1, seed=74, scale=(2.0 / C) ** 0.5)
     b = rnd(Co, seed=75, scale=0.1)
@@ -450,8 +467,12 @@ def test_pw_residual_fwd(cfg, act):
     OUT = torch.full((N, Co, H, W), float("nan"), device=DEV)
     OST = rep_zeros(4 * Co)
     B, Wt = cuda32(b), cuda32(w)  # kept alive: the call only sees their addresses
-    a = struct(L.VTensor, {"s": [seg], "nseg": 1, "N": N, "H": H, "W": W, "mat": ptr(MAT),
-                           "mat_n_stride": C * H * W})
+    vspec = {"s": [seg], "nseg": 1, "N": N, "H": H, "W": W, "mat": ptr(MAT),
+             "mat_n_stride": C * H * W}
+    if rbn:  # the residual's own BatchNorm (a two-BN tail)
+        G2, B2, ST2 = cuda32(r2[0]), cuda32(r2[1]), rep_from(r2[2])
+        vspec["rbn"] = bn_spec_train(G2, B2, ST2, N * H * W)
+    a = struct(L.VTensor, vspec)
     sk = sinks([{"p": ptr(OUT), "n_stride": Co * H * W, "c0": 0, "C": Co, "mode": L.SINK_STORE,
                  "bias": ptr(B), "stats": ptr(OST)}])
     call("isg_conv_fwd", geom(**ge), a, ptr(Wt), sk, stream())
@@ -462,7 +483,7 @@ def test_pw_residual_fwd(cfg, act):
     close(ost[Co:2 * Co], (ref * ref).sum((0, 2, 3)), tol=4e-6, what="sumsq")
 
 
-@pytest.mark.parametrize("parts", ["old+p2", "old", "p2", "none", "old+p2acc"])
+@pytest.mark.parametrize("parts", ["old+p2", "old", "p2", "none", "old+p2acc", "old+rbn"])
 @pytest.mark.parametrize("cfg", RES)
 def test_pw_residual_dgrad(cfg, parts):
     """Folded residual tail, backward: the 1x1 input gradient's ACTBWD sink in residual
@@ -472,7 +493,8 @@ def test_pw_residual_dgrad(cfg, parts):
     C, Co, H, W = cfg
     N = 2
     ge, _, _ = _geom(N, C, Co, H, W, 1, 1, 0, 1)
-    y, xr, gamma, beta, slope, st, mean, z = _res_state(C, N, H, W, 81)
+    rbn = "rbn" in parts
+    y, xr, gamma, beta, slope, st, mean, z, r2 = _res_state(C, N, H, W, 81, rbn)
     dz = rnd(N, Co, H, W, seed=85)
     w = rnd(Co, C, 1, 1, seed=86, scale=(2.0 / C) ** 0.5)
     old = rnd(N, C, H, W, seed=87) if "old" in parts else torch.zeros(N, C, H, W, dtype=torch.float64)
@@ -490,6 +512,9 @@ def test_pw_residual_dgrad(cfg, parts):
           "r": ptr(XR), "r_n_stride": C * H * W}
     if "old" in parts:
         sk["old"], sk["old_n_stride"] = ptr(OLD), C * H * W
+    if rbn:  # the residual's own BatchNorm: its backward sums go to its statistics
+        G2, B2, ST2 = cuda32(r2[0]), cuda32(r2[1]), rep_from(r2[2])
+        sk["rbn"] = bn_spec_train(G2, B2, ST2, N * H * W)
     P2OLD = rnd(N, C, H, W, seed=88)
     if "p2acc" in parts:  # the residual term's gradient already holds a part: p2 += g
         P2.copy_(cuda32(P2OLD))
@@ -507,10 +532,13 @@ def test_pw_residual_dgrad(cfg, parts):
     else:
         assert torch.isnan(P2).all()
     stf = rep_fold(ST, 4 * C).double().cpu()
-    for got, terms, what in ((stf[2 * C:3 * C], g, "gsum"),
-                             (stf[3 * C:], g * (y - mean[None, :, None, None]), "gxsum"),
-                             (rep_fold(SG, C).double().cpu(), torch.where(z > 0, 0 * z, z * tot),
-                              "slope grad")):
+    checks = [(stf[2 * C:3 * C], g, "gsum"), (stf[3 * C:], g * (y - mean[None, :, None, None]), "gxsum"),
+              (rep_fold(SG, C).double().cpu(), torch.where(z > 0, 0 * z, z * tot), "slope grad")]
+    if rbn:
+        st2 = rep_fold(ST2, 4 * C).double().cpu()
+        checks += [(st2[2 * C:3 * C], g, "residual gsum"),
+                   (st2[3 * C:], g * (xr - r2[3][None, :, None, None]), "residual gxsum")]
+    for got, terms, what in checks:
         err = (got - terms.sum((0, 2, 3))).abs().max().item()
         assert err <= 2e-6 * terms.abs().sum((0, 2, 3)).max().item() + 1e-9, (what, err)
 

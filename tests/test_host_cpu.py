@@ -261,6 +261,8 @@ def test_residual_tails_fold_into_the_next_1x1(monkeypatch):
     fwd = {t.out.name for t in ops if getattr(t, "fwd_folded", False)}
     bwd = {t.out.name for t in ops if getattr(t, "bwd_folded", False)}
     chain = [f"bottle1_x.{i}" for i in range(3)] + [f"bottle{s}_x.{i}" for s in (2, 3) for i in range(4)]
+    # two-BatchNorm tails (BottleneckDown2, BottleneckDim_Res: act(BN(y) + BN2(r)))
+    chain += ["bottle1_1", "bottle2_1", "bottle3_1", "bottle4_2"]
     assert fwd == set(chain)
     assert bwd == set(chain)
     tails_f = [r for r in p.fwd.recs if r.kind == L.OP_TAIL_FWD]

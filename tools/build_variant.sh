@@ -8,7 +8,7 @@ NAME=$1; DEFS=$2
 SRC=instancesegmentation_amd/csrc
 OUT=instancesegmentation_amd/build_obj_$NAME
 mkdir -p $OUT
-FL="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-function -Wno-pass-failed $DEFS"
+FL="--offload-arch=gfx950 -O2 -fno-unroll-loops -std=c++17 -fPIC -Wno-unused-function -Wno-pass-failed $DEFS"
 objs=""
 for s in $SRC/*.hip; do
   f=$(basename $s .hip)
