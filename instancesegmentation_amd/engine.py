@@ -685,8 +685,10 @@ def _fold_tails(g):
                  PReLU slope gradient, and the residual term's gradient as a second
                  output), decided in ConvOp.bwd (falls back to the tail's own launch when
                  the gradient bookkeeping does not allow it).
-    Train mode only (batch statistics); ISG_NO_TAIL_FOLD=1 off."""
-    if os.environ.get("ISG_NO_TAIL_FOLD", "0") == "1" or not g.train:
+    Train mode, and forward-only eval plans (infer: the BN-folded network's tails add a
+    plain conv output, read as an identity-BN segment with the tail's activation);
+    ISG_NO_TAIL_FOLD=1 off."""
+    if os.environ.get("ISG_NO_TAIL_FOLD", "0") == "1" or (not g.train and g.need_grad):
         return
     for t, c in zip(g.ops, g.ops[1:]):
         if not isinstance(t, TailOp) or not isinstance(c, ConvOp) or len(t.terms) != 2:
@@ -695,10 +697,13 @@ def _fold_tails(g):
         C = t.out.C
         # the residual: a materialised value, or a second BatchNorm'd conv output (the
         # BottleneckDown2 / BottleneckDim_Res tails, segment.py:147-148, 202-207)
-        r_ok = not r.virtual or (r.bn is not None and r.act == "none" and r.c0 == 0
+        r_ok = not r.virtual or (g.train and r.bn is not None and r.act == "none" and r.c0 == 0
                                  and r.C == r.buf.C and r.buf is not y.buf
                                  and os.environ.get("ISG_NO_RBN_FOLD", "0") != "1")
-        if upy or upr or y.bn is None or y.act != "none" or not r_ok or t.c0 != 0:
+        # y: a BatchNorm'd raw conv output, or (BN folded into the conv) a plain one under
+        # the tail's activation (the residual form is a BN_FWD segment either way)
+        y_ok = y.act == "none" and (y.bn is not None or (not y.virtual and t.act != "none"))
+        if upy or upr or not y_ok or not r_ok or t.c0 != 0:
             continue
         if t.out.slot != S_ACT or y.C != C or r.C != C or y.c0 != 0 or y.buf.C != C:
             continue
