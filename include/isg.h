@@ -81,7 +81,8 @@ typedef struct {
  *   BN_FWD: v = act((p - mean) * gamma*rstd + beta)            (Conv.forward, segment.py:44-45)
  *           with y non-NULL (a residual block's tail read by its consumer):
  *           v = act((p - mean) * gamma*rstd + beta + y)        (segment.py:75-77: out += residual;
- *           prelu) — accepted only by the 1x1 stride-1 conv forward, one segment
+ *           prelu) — accepted only by the 1x1 stride-1 conv forward, one segment (any
+ *           sinks: a stacked sibling pair's two)
  *   BN_BWD: v = dL/d(conv output) rebuilt from g (= dL/d BN-output) and the forward
  *           raw y: A*g + B*(y - mean) + C                       (BatchNorm2d backward) */
 typedef struct {
@@ -122,8 +123,8 @@ typedef struct {
  *           gradient of the next block's first 1x1, segment.py:75-77): v' = v + old,
  *           z = BN(y) + r, g = v'*act'(z) into p and, when p2 is non-NULL, also into p2
  *           (the residual term's gradient; STORE, or ACCUM with p2_accum); statistics as
- *           ACTBWD with v'. Accepted
- *           only by the 1x1 stride-1 input gradient with one sink. */
+ *           ACTBWD with v'. Accepted only by the 1x1 stride-1 input gradient with one
+ *           sink (any gradient segments: a stacked sibling pair's two). */
 typedef struct {
     float* p;
     int64_t n_stride;

@@ -76,9 +76,20 @@ static bool pointwise(const isg_conv_geom* g) {
     return g->KH == 1 && g->KW == 1 && g->SH == 1 && g->SW == 1 && g->PH == 0 && g->PW == 0 &&
            g->DH == 1 && g->DW == 1 && g->groups == 1 && g->w_ci == 0;
 }
-// one segment of `cin` channels in, one sink of all `cout` rows out
-static bool res_shape_ok(const isg_vtensor* v, int cin, const isg_sinks* k, int cout) {
-    return v->nseg == 1 && v->s[0].C == cin && k->nsink == 1 && k->s[0].c0 == 0 && k->s[0].C == cout;
+// segments covering `cin` channels in (forward: one), consecutive sinks covering all `cout`
+// rows out (input gradient: one)
+static bool res_shape_ok(const isg_vtensor* v, int cin, const isg_sinks* k, int cout, bool dgrad) {
+    if (v->nseg < 1 || v->nseg > ISG_MAX_SEGS || k->nsink < 1 || k->nsink > ISG_MAX_SEGS) return false;
+    if (dgrad ? k->nsink != 1 : v->nseg != 1) return false;
+    int c = 0;
+    for (int i = 0; i < v->nseg; ++i) c += v->s[i].C;
+    if (c != cin) return false;
+    c = 0;
+    for (int i = 0; i < k->nsink; ++i) {
+        if (k->s[i].c0 != c) return false;
+        c += k->s[i].C;
+    }
+    return c == cout;
 }
 int32_t isg_s2k5_fwd(const isg_conv_geom*, const isg_vtensor*, const float*, const isg_sinks*,
                      hipStream_t);
@@ -117,8 +128,8 @@ int32_t isg_conv_fwd(const isg_conv_geom* g, const isg_vtensor* x_, const float*
     if (!x_ || !out) return isg_set_error(ISG_ERR_INVALID, "conv fwd: NULL tensor");
     if (isg_sinks_res(out)) return isg_set_error(ISG_ERR_UNSUPPORTED, "conv fwd: residual sink form");
     if (isg_vt_res(x_)) {  // a folded residual tail: the slab 1x1 GEMM or nothing
-        if (!pointwise(g) || !res_shape_ok(x_, g->Ci, out, g->Co))
-            return isg_set_error(ISG_ERR_UNSUPPORTED, "conv fwd: residual input needs a 1x1 conv, one segment, one sink");
+        if (!pointwise(g) || !res_shape_ok(x_, g->Ci, out, g->Co, false))
+            return isg_set_error(ISG_ERR_UNSUPPORTED, "conv fwd: residual input needs a 1x1 conv and one segment");
         return isg_pw_gemm(g, x_, w, out, false, st);
     }
     const isg_vtensor xr = resolve_y(x_);
@@ -143,8 +154,8 @@ int32_t isg_conv_dgrad(const isg_conv_geom* g, const isg_vtensor* dy_, const flo
     const isg_vtensor dyr = resolve_y(dy_);
     const isg_vtensor* dy = &dyr;
     if (isg_sinks_res(dx)) {  // a folded residual tail's backward: the slab 1x1 GEMM or nothing
-        if (!pointwise(g) || !res_shape_ok(dy, g->Co, dx, g->Ci))
-            return isg_set_error(ISG_ERR_UNSUPPORTED, "conv dgrad: residual sink needs a 1x1 conv, one segment, one sink");
+        if (!pointwise(g) || !res_shape_ok(dy, g->Co, dx, g->Ci, true))
+            return isg_set_error(ISG_ERR_UNSUPPORTED, "conv dgrad: residual sink needs a 1x1 conv and one sink");
         return isg_pw_gemm(g, dy, w, dx, true, st);
     }
     if (partial_w(g)) return isg_set_error(ISG_ERR_UNSUPPORTED, "conv dgrad with w_ci != Ci");

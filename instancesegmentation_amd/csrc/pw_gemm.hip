@@ -329,11 +329,12 @@ ISG_DEV ChanCoef rbn_finish(const isg_bn& bn, const RbnLoad& l) {
     return fwd_coef_of(mean, rstd, l.st.gamma, l.st.beta, 0.f);
 }
 
-// RES (SEG1 only): the one sink is ACTBWD's residual form — its extra operands and
-// reductions exist only in these instantiations (kept out of the common kernels, where
-// their live registers cost occupancy)
+// RES: the one sink is ACTBWD's residual form — its extra operands and reductions exist
+// only in these instantiations (kept out of the common kernels, where their live registers
+// cost occupancy); with SEG1 false the source is a K-stacked pair's two gradient segments
 template <int TPW, int BP, bool HY, bool SEG1, bool RES>
 __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
+    constexpr bool SINK1 = SEG1 || RES;  // one sink: its operands issued in the first round trip
     extern __shared__ f32x4 pwx_smem[];
     char* const smem = reinterpret_cast<char*>(pwx_smem);
     ChSrc* const tabA = reinterpret_cast<ChSrc*>(smem);  // kThreads entries (clamped past K)
@@ -369,10 +370,8 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
     // ---- phase 1 ------------------------------------------------------------------------
     VtSel vs = vt_sel(a.src);
     SkSel ks = sk_sel(a.out);
-    if constexpr (SEG1) {
-        vs.nseg = 1;
-        ks.nsink = 1;
-    }
+    if constexpr (SEG1) vs.nseg = 1;
+    if constexpr (SINK1) ks.nsink = 1;
     // ---- phase 2 first: the activation slab loads (HBM, the longest latency) lead the
     //      round trip; their channel addresses come from the kernel arguments alone, only
     //      the transform needs the coefficient table, after the barrier
@@ -438,7 +437,7 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
     for (int i = 0; i < TR; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) pro[i][r] = prr[i][r] = pp2[i][r] = 0.f;
-    if (SEG1 && a.pre_on) {
+    if (SINK1 && a.pre_on) {
         const SinkLite& k0 = ks.s0;
         const bool ab = k0.mode == ISG_SINK_ACTBWD;
         const float* base = ab ? k0.y : k0.p;
@@ -509,7 +508,7 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
     // ---- phase 3: producer transform into Xs[k][p] --------------------------------------
     // the materialised input (isg_vtensor.mat: a folded residual tail's block output),
     // written once per pixel by the first row block
-    float* const mat = SEG1 && blockIdx.y == 0 ? a.src.mat : nullptr;
+    float* const mat = blockIdx.y == 0 ? a.src.mat : nullptr;  // host: one segment
 #pragma unroll
     for (int u = 0; u < XU; ++u) {
         const int c = cr + u * CPP;
@@ -571,7 +570,7 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
     // ---- phase 5: epilogue; lane holds D[row = rt*16 + kk*4 + r][pixel = ct*16 + pl] ----
     // sink operands first (saved forward output for ACTBWD, old value for ACCUM), all in
     // flight together; other rows load a dummy word
-    if (!SEG1 && a.pre_on) {
+    if (!SINK1 && a.pre_on) {
 #pragma unroll
         for (int i = 0; i < TPW; ++i) {
             const int t = min(wave + 4 * i, nt - 1);
@@ -741,7 +740,9 @@ int32_t pwx_dispatch(const PwxArgs& a, dim3 grid, int lds, int tpw, hipStream_t 
 }
 template <int BP, bool HY>
 int32_t pwx_dispatch_seg(const PwxArgs& a, dim3 grid, int lds, int tpw, bool seg1, hipStream_t st) {
-    if (a.res_on) return pwx_dispatch<BP, HY, true, true>(a, grid, lds, tpw, st);  // host: seg1
+    if (a.res_on)  // host: one sink
+        return seg1 ? pwx_dispatch<BP, HY, true, true>(a, grid, lds, tpw, st)
+                    : pwx_dispatch<BP, HY, false, true>(a, grid, lds, tpw, st);
     return seg1 ? pwx_dispatch<BP, HY, true, false>(a, grid, lds, tpw, st)
                 : pwx_dispatch<BP, HY, false, false>(a, grid, lds, tpw, st);
 }
@@ -988,12 +989,13 @@ int32_t isg_pw_gemm(const isg_conv_geom* g, const isg_vtensor* src, const float*
         res_out |= k.r || k.old || k.p2 || k.rbn.stats || k.rbn.coef;
     }
     const bool res = res_in || res_out;
-    if (res && ((res_in && dgrad) ||
-                (res_in && rbn_src && !(src->s[0].xform == ISG_XF_BN_FWD && src->s[0].y)) ||
-                (res_out && (!dgrad || out->s[0].mode != ISG_SINK_ACTBWD || !out->s[0].r)) ||
-                src->nseg != 1 || out->nsink != 1))
-        return isg_set_error(ISG_ERR_UNSUPPORTED, "pw gemm: residual forms need one segment and one "
-                             "sink (input residual in the forward, ACTBWD residual in the input gradient)");
+    // forward: one source segment (the residual's own BatchNorm: also one sink), any sinks;
+    // input gradient: one residual sink, any gradient segments (a stacked pair's two)
+    if (res && ((res_in && dgrad) || (res_in && src->nseg != 1) ||
+                (res_in && rbn_src && !(src->s[0].xform == ISG_XF_BN_FWD && src->s[0].y && out->nsink == 1)) ||
+                (res_out && (!dgrad || out->nsink != 1 || out->s[0].mode != ISG_SINK_ACTBWD || !out->s[0].r))))
+        return isg_set_error(ISG_ERR_UNSUPPORTED, "pw gemm: residual forms need one segment in the forward "
+                             "(input residual), one ACTBWD residual sink in the input gradient");
     if (!res) {  // thin layers (K, M <= 16) on the VALU
         const int32_t t = thin_pw(a, st);
         if (t != 0) return t < 0 ? t : 0;

@@ -690,8 +690,9 @@ def _fold_tails(g):
     ISG_NO_TAIL_FOLD=1 off."""
     if os.environ.get("ISG_NO_TAIL_FOLD", "0") == "1" or (not g.train and g.need_grad):
         return
-    for t, c in zip(g.ops, g.ops[1:]):
-        if not isinstance(t, TailOp) or not isinstance(c, ConvOp) or len(t.terms) != 2:
+    ops = g.ops
+    for i, t in enumerate(ops):
+        if not isinstance(t, TailOp) or len(t.terms) != 2:
             continue
         (y, upy), (r, upr) = t.terms
         C = t.out.C
@@ -707,22 +708,53 @@ def _fold_tails(g):
             continue
         if t.out.slot != S_ACT or y.C != C or r.C != C or y.c0 != 0 or y.buf.C != C:
             continue
-        ge = c.geom
-        if not (c.kind == "conv" and c.kp is None and not getattr(c, "side", False)
-                and ge["KH"] == 1 and ge["KW"] == 1 and ge["SH"] == 1 and ge["SW"] == 1
-                and ge["PH"] == 0 and ge["PW"] == 0 and ge["DH"] == 1 and ge["DW"] == 1
-                and ge["groups"] == 1 and "w_ci" not in ge):
+        if (t.out.H * t.out.W) % 4 or C % 4 or C > 128:
             continue
-        if len(c.x.segs) != 1:
+        # the side-branch ops forked right after the tail (BottleneckUp_Res's conv2,
+        # segment.py:230-236, reads the block input beside the main chain): each one either
+        # does not read the tail's output or is a 1x1 conv folding the tail on its own load
+        # (no materialised output); then the main-stream 1x1 that writes it
+        side = []
+        j = i + 1
+        while j < len(ops) and getattr(ops[j], "side", False):
+            if any(v.buf is t.out for v in ops[j].x.segs):
+                side.append(ops[j])
+            j += 1
+        if j >= len(ops) or not all(_fold_reader_ok(o, t) for o in side + [ops[j]]):
             continue
-        xv = c.x.segs[0]
-        if xv.buf is not t.out or xv.c0 != 0 or xv.C != C or xv.virtual:
+        if side and os.environ.get("ISG_NO_SIDE_FOLD", "0") == "1":  # A/B switches
             continue
-        # the slab kernel's shapes (pw_gemm.hip isg_pw_gemm): 16-B rows, K and M <= 128
-        if (t.out.H * t.out.W) % 4 or C % 4 or C > 128 or ge["Co"] > 128 or ge["Co"] % 4:
+        if isinstance(ops[j], ConvPairOp) and os.environ.get("ISG_NO_PAIR_FOLD", "0") == "1":
             continue
+        c = ops[j]
         t.fwd_folded = True
-        c.res_tail = t
+        for o in side:
+            o.res_in, o.res_mat = t, False
+        c.res_in, c.res_mat = t, True
+        # the backward: the first reader's input gradient is the last contribution
+        (side[0] if side else c).res_tail = t
+
+
+def _fold_reader_ok(c, t):
+    """A reader of a residual tail's output that can take the tail's forward on its input
+    load (and, as the last gradient contributor, its backward in the input-gradient sink):
+    a dense 1x1 stride-1 conv, or a stacked sibling pair of them (Graph.conv_pair), on exactly
+    that value (pw_gemm.hip: 16-B rows, K, M <= 128)."""
+    if not isinstance(c, (ConvOp, ConvPairOp)):
+        return False
+    ge = c.geom
+    if isinstance(c, ConvOp) and not (c.kind == "conv" and c.kp is None):
+        return False
+    if not (ge["KH"] == 1 and ge["KW"] == 1 and ge["SH"] == 1 and ge["SW"] == 1
+            and ge["PH"] == 0 and ge["PW"] == 0 and ge["DH"] == 1 and ge["DW"] == 1
+            and ge["groups"] == 1 and "w_ci" not in ge):
+        return False
+    if len(c.x.segs) != 1:
+        return False
+    xv = c.x.segs[0]
+    if xv.buf is not t.out or xv.c0 != 0 or xv.C != t.out.C or xv.virtual:
+        return False
+    return ge["Co"] <= 128 and ge["Co"] % 4 == 0
 
 
 def sinks_spec(sinks):
@@ -845,23 +877,24 @@ class GradState:
 
 
 # ---------------------------------------------------------------------------------
-class ConvOp:
-    def __init__(self, g, kind, mod, geom, x, out, bnr):
-        self.g, self.kind, self.mod, self.geom, self.x, self.out, self.bnr = g, kind, mod, geom, x, out, bnr
-        self.kp = None
-        self.res_tail = None  # a residual tail folded into this conv (_fold_tails)
+class _ResFold:
+    """A residual tail folded into a 1x1 conv (ConvOp) or stacked sibling pair (ConvPairOp):
+    read on the input load (res_in; res_mat: this op writes the tail's buffer), run in the
+    input gradient's sink (res_tail). _fold_tails sets them."""
+    res_in, res_mat, res_tail = None, False, None
 
     def _res_input(self):
         """The forward input of a folded tail act(BN(y) + x): one BN_FWD segment of y with
         the residual x and the tail's activation, and the tail's buffer as `mat`."""
-        g, t = self.g, self.res_tail
+        g, t = self.g, self.res_in
         (y, _), (r, _) = t.terms
         seg = fwd_seg(Val(y.buf, y.c0, y.C, y.bn, t.act, t.slope), g.train)
         seg["y"] = r.buf.ptr(r.c0)
         seg["y_n_stride"] = r.buf.n_stride
         vt = vtensor([seg], g.N, self.geom["H"], self.geom["W"])
-        vt["mat"] = t.out.ptr()
-        vt["mat_n_stride"] = t.out.n_stride
+        if self.res_mat:
+            vt["mat"] = t.out.ptr()
+            vt["mat_n_stride"] = t.out.n_stride
         if r.bn is not None:  # a BatchNorm'd residual: act(BN(y) + BN2(r))
             vt["rbn"] = bn_spec(r.bn, g.train)
         return vt
@@ -912,6 +945,12 @@ class ConvOp:
         t.bwd_folded = True
         return s
 
+
+class ConvOp(_ResFold):
+    def __init__(self, g, kind, mod, geom, x, out, bnr):
+        self.g, self.kind, self.mod, self.geom, self.x, self.out, self.bnr = g, kind, mod, geom, x, out, bnr
+        self.kp = None
+
     def _kp_spec(self):
         """isg_kp_stem fields shared by the forward and weight-gradient records."""
         ge = dict(self.geom)
@@ -943,12 +982,12 @@ class ConvOp:
         if self.bnr is not None and g.train:
             sink["stats"] = Ptr(S_STATS, self.bnr.stats_off * 8)
         ge = self.geom
-        a = self._res_input() if self.res_tail is not None else vtensor(segs, g.N, ge["H"], ge["W"])
+        a = self._res_input() if self.res_in is not None else vtensor(segs, g.N, ge["H"], ge["W"])
         rec = {"g": ge, "a": a, "w": g.tptr(self.mod, "weight"), "out": sinks_spec([sink])}
         kind = L.OP_CONVT_FWD if self.kind == "convT" else L.OP_CONV_FWD
         fl, xb, yb, wb = self._cost()
-        if self.res_tail is not None:
-            xb *= 3  # BN'd y and the residual read, the materialised output written
+        if self.res_in is not None:
+            xb *= 3 if self.res_mat else 2  # BN'd y and the residual read (+ the output written)
         ops.add(Record(kind, L.ConvRec, rec, label=self.out.name, flops=fl, nbytes=xb + yb + wb))
         if self.kp is not None:
             ks = dict(self._kp_spec(), w=g.tptr(self.mod, "weight"), y=self.out.ptr(),
@@ -1033,7 +1072,7 @@ class ConvOp:
             gs.bias_from_bn.append((self.mod, self.bnr))
 
 
-class ConvPairOp:
+class ConvPairOp(_ResFold):
     """Two sibling 1x1 convs on one input as one stacked GEMM (Graph.conv_pair)."""
 
     def __init__(self, g, geom, x, outs):
@@ -1060,8 +1099,11 @@ class ConvPairOp:
             c0 += buf.C
         ge = self.geom
         fl, xb, yb, wb = self._cost(ge["Co"])
+        if self.res_in is not None:
+            xb *= 3 if self.res_mat else 2  # BN'd y and the residual read (+ the output written)
+        a = self._res_input() if self.res_in is not None else vtensor(segs, g.N, ge["H"], ge["W"])
         ops.add(Record(L.OP_CONV_FWD, L.ConvRec,
-                       {"g": ge, "a": vtensor(segs, g.N, ge["H"], ge["W"]),
+                       {"g": ge, "a": a,
                         "w": g.tptr(self.outs[0][0], "weight"), "out": sinks_spec(sinks)},
                        label=self.label, flops=fl, nbytes=xb + yb + wb))
 
@@ -1090,8 +1132,9 @@ class ConvPairOp:
         dyv = vtensor(segs, g.N, ge["H"], ge["W"])
         label = "+".join(p[1].name for p in live)
         if self.x.grad:
-            sinks, c = [], 0
-            for v in self.x.segs:
+            rs = self._res_sink(gs) if self.res_tail is not None else None
+            sinks, c = ([rs] if rs is not None else []), 0
+            for v in ([] if rs is not None else self.x.segs):
                 sinks.append(gs.sink_for(v, c, g.train))
                 c += v.C
             ops.add(Record(L.OP_CONV_DGRAD, L.ConvRec,

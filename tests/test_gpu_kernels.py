@@ -441,17 +441,19 @@ def _res_state(C, N, H, W, seed, rbn=False):
     return y, xr, gamma, beta, slope, st, mean, by + rv, r2
 
 
-@pytest.mark.parametrize("act", ["prelu", "relu", "prelu-rbn"])
+@pytest.mark.parametrize("act", ["prelu", "relu", "prelu-rbn", "prelu-pair"])
 @pytest.mark.parametrize("cfg", RES)
 def test_pw_residual_fwd(cfg, act):
     """Folded residual tail, forward: a 1x1 conv reading act(BN(y) + x) on load (BN_FWD
     segment with a residual y, statistics finalised by the consumer) that also writes the
     materialised act(BN(y) + x) to vtensor.mat — segment.py:75-77 then the next block's
-    first conv — against fp64."""
+    first conv — against fp64. "pair": a stacked sibling pair's two sinks (Graph.conv_pair,
+    BottleneckUp_Res convs.0 + conv2 reading the tail, segment.py:326-331)."""
     C, Co, H, W = cfg
     N = 2
     ge, _, _ = _geom(N, C, Co, H, W, 1, 1, 0, 1)
     rbn = act.endswith("-rbn")
+    pair = act.endswith("-pair")
     act = act.split("-")[0]
     y, xr, gamma, beta, slope, st, _, z, r2 = _res_state(C, N, H, W, 71, rbn)
     v = torch.where(z > 0, z, z * slope[None, :, None, None]) if act == "prelu" else z.clamp_min(0)
@@ -464,8 +466,6 @@ def test_pw_residual_fwd(cfg, act):
     if act == "prelu":
         seg["slope"] = ptr(SL)
     MAT = torch.full((N, C, H, W), float("nan"), device=DEV)
-    OUT = torch.full((N, Co, H, W), float("nan"), device=DEV)
-    OST = rep_zeros(4 * Co)
     B, Wt = cuda32(b), cuda32(w)  # kept alive: the call only sees their addresses
     vspec = {"s": [seg], "nseg": 1, "N": N, "H": H, "W": W, "mat": ptr(MAT),
              "mat_n_stride": C * H * W}
@@ -473,23 +473,34 @@ def test_pw_residual_fwd(cfg, act):
         G2, B2, ST2 = cuda32(r2[0]), cuda32(r2[1]), rep_from(r2[2])
         vspec["rbn"] = bn_spec_train(G2, B2, ST2, N * H * W)
     a = struct(L.VTensor, vspec)
-    sk = sinks([{"p": ptr(OUT), "n_stride": Co * H * W, "c0": 0, "C": Co, "mode": L.SINK_STORE,
-                 "bias": ptr(B), "stats": ptr(OST)}])
+    if pair:  # channels [0, Ca) and [Ca, Co) to two buffers with their own statistics
+        Ca = Co // 2 if Co % 8 == 0 else Co // 2 + 2
+        parts = [(0, Ca), (Ca, Co - Ca)]
+    else:
+        parts = [(0, Co)]
+    OUTS = [torch.full((N, c, H, W), float("nan"), device=DEV) for _, c in parts]
+    OSTS = [rep_zeros(4 * c) for _, c in parts]
+    sk = sinks([{"p": ptr(o), "n_stride": c * H * W, "c0": c0, "C": c, "mode": L.SINK_STORE,
+                 "bias": ptr(B[c0:c0 + c]), "stats": ptr(st_)}
+                for o, st_, (c0, c) in zip(OUTS, OSTS, parts)])
     call("isg_conv_fwd", geom(**ge), a, ptr(Wt), sk, stream())
     close(MAT, v, what="materialised block output")
-    close(OUT, ref, what="1x1 on the folded tail")
-    ost = rep_fold(OST, 4 * Co)
-    close(ost[:Co], ref.sum((0, 2, 3)), tol=4e-6, what="sum")
-    close(ost[Co:2 * Co], (ref * ref).sum((0, 2, 3)), tol=4e-6, what="sumsq")
+    for o, st_, (c0, c) in zip(OUTS, OSTS, parts):
+        r = ref[:, c0:c0 + c]
+        close(o, r, what="1x1 on the folded tail")
+        ost = rep_fold(st_, 4 * c)
+        close(ost[:c], r.sum((0, 2, 3)), tol=4e-6, what="sum")
+        close(ost[c:2 * c], (r * r).sum((0, 2, 3)), tol=4e-6, what="sumsq")
 
 
-@pytest.mark.parametrize("parts", ["old+p2", "old", "p2", "none", "old+p2acc", "old+rbn"])
+@pytest.mark.parametrize("parts", ["old+p2", "old", "p2", "none", "old+p2acc", "old+rbn", "old+p2-pair"])
 @pytest.mark.parametrize("cfg", RES)
 def test_pw_residual_dgrad(cfg, parts):
     """Folded residual tail, backward: the 1x1 input gradient's ACTBWD sink in residual
     form — v' = dx + old (what later consumers accumulated), g = v' * PReLU'(BN(y) + x)
     into p and p2, BatchNorm-backward sums of y and the PReLU slope gradient — the tail
-    backward of segment.py:75-77 — against fp64."""
+    backward of segment.py:75-77 — against fp64. "pair": the gradient arrives as a stacked
+    sibling pair's two segments (ConvPairOp.bwd: [Wa; Wb]^T [ga; gb])."""
     C, Co, H, W = cfg
     N = 2
     ge, _, _ = _geom(N, C, Co, H, W, 1, 1, 0, 1)
@@ -522,8 +533,14 @@ def test_pw_residual_dgrad(cfg, parts):
     if "p2" in parts:
         sk["p2"], sk["p2_n_stride"] = ptr(P2), C * H * W
     DZ, Wt = cuda32(dz), cuda32(w)  # kept alive: the call only sees their addresses
-    dyseg = {"p": ptr(DZ), "n_stride": Co * H * W, "C": Co, "xform": L.XF_PLAIN}
-    call("isg_conv_dgrad", geom(**ge), vt([dyseg], N, H, W), ptr(Wt), sinks([sk]), stream())
+    if "pair" in parts:  # two gradient segments, each its own buffer
+        Ca = Co // 2 if Co % 8 == 0 else Co // 2 + 2
+        DZS = [DZ[:, :Ca].contiguous(), DZ[:, Ca:].contiguous()]
+        dysegs = [{"p": ptr(d), "n_stride": d.shape[1] * H * W, "C": d.shape[1], "xform": L.XF_PLAIN}
+                  for d in DZS]
+    else:
+        dysegs = [{"p": ptr(DZ), "n_stride": Co * H * W, "C": Co, "xform": L.XF_PLAIN}]
+    call("isg_conv_dgrad", geom(**ge), vt(dysegs, N, H, W), ptr(Wt), sinks([sk]), stream())
     close(GB, g, what="g (BN-output gradient of y)")
     if "p2acc" in parts:
         close(P2, g + P2OLD, what="p2 += g")

@@ -263,6 +263,10 @@ def test_residual_tails_fold_into_the_next_1x1(monkeypatch):
     chain = [f"bottle1_x.{i}" for i in range(3)] + [f"bottle{s}_x.{i}" for s in (2, 3) for i in range(4)]
     # two-BatchNorm tails (BottleneckDown2, BottleneckDim_Res: act(BN(y) + BN2(r)))
     chain += ["bottle1_1", "bottle2_1", "bottle3_1", "bottle4_2"]
+    # tails read by a side-branch 1x1 beside the next block's first 1x1 (BottleneckUp_Res's
+    # conv2): both fold the tail on load, the main-stream one writes it, the side one (the
+    # first reader) runs its backward
+    chain += ["bottle3_x.4", "bottle4_3"]
     assert fwd == set(chain)
     assert bwd == set(chain)
     tails_f = [r for r in p.fwd.recs if r.kind == L.OP_TAIL_FWD]
@@ -272,14 +276,44 @@ def test_residual_tails_fold_into_the_next_1x1(monkeypatch):
     # the folded conv writes the tail's buffer: its record holds a pointer into it
     for t in ops:
         if getattr(t, "fwd_folded", False):
-            c = next(op for op in ops if getattr(op, "res_tail", None) is t)
-            r = next(r for r in p.fwd.recs if r.label == c.out.name)
+            readers = [op for op in ops if getattr(op, "res_in", None) is t]
+            writers = [c for c in readers if c.res_mat]
+            assert len(writers) == 1 and not getattr(writers[0], "side", False)
             o = t.out.ptr()
-            assert any(fs == o.slot and off == o.off for _, fs, off in r.fix)
+            for c in readers:
+                r = next(r for r in p.fwd.recs if r.label == c.out.name)
+                assert any(fs == o.slot and off == o.off for _, fs, off in r.fix) == c.res_mat
+            bw = [op for op in ops if getattr(op, "res_tail", None) is t]
+            assert len(bw) == 1 and bw[0] is min(readers, key=ops.index)
     monkeypatch.setenv("ISG_NO_TAIL_FOLD", "1")
     q = Plan(Segment(20), [(2, 3, 128, 128), (2, 17, 3)], True, True, (False, False))
     assert len([r for r in q.fwd.recs if r.kind == L.OP_TAIL_FWD]) == len(tails_f) + len(fwd)
     assert len([r for r in q.bwd.recs if r.kind == L.OP_TAIL_BWD]) == len(tails_b) + len(bwd)
+
+
+def test_residual_tails_fold_into_a_stacked_pair():
+    """In the Trainer's flat parameter layout BottleneckUp_Res's convs.0 + conv2 run as one
+    stacked GEMM (Graph.conv_pair) reading the previous tail: the pair takes that tail's
+    forward on its input load (writing the tail's buffer) and its backward in the K-stacked
+    input gradient's residual sink — bottle3_x.4 and bottle4_3 on top of the 15 folds."""
+    from instancesegmentation_amd.engine import ConvPairOp, param_layout
+    from instancesegmentation_amd.train import flatten_module
+    m = Segment(20)
+    lay = param_layout(m)
+    flatten_module(m, "cpu", order=lay)
+    p = Plan(m, [(2, 3, 128, 128), (2, 17, 3)], True, True, (False, False), layout=lay)
+    ops = p.graph.ops
+    pairs = {t.out.name: c for c in ops if isinstance(c, ConvPairOp) and c.res_in is not None
+             for t in [c.res_in]}
+    assert set(pairs) == {"bottle3_x.4", "bottle4_3"}
+    for name, c in pairs.items():
+        assert c.res_mat and c.res_tail is c.res_in and c.res_in.bwd_folded
+        assert not any(r.kind == L.OP_TAIL_FWD and r.label == name for r in p.fwd.recs)
+        assert not any(r.kind == L.OP_TAIL_BWD and r.label == "d_" + name for r in p.bwd.recs)
+        dx = next(r for r in p.bwd.recs if r.label == "dx_" + c.label)
+        assert dx.kind == L.OP_CONV_DGRAD and L.ConvRec.from_buffer_copy(dx.body).out.nsink == 1
+    fwd = {t.out.name for t in ops if getattr(t, "fwd_folded", False)}
+    assert len(fwd) == 17
 
 
 def test_depthwise_backward_is_one_main_stream_op(monkeypatch):
