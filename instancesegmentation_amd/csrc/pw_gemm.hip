@@ -442,9 +442,6 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
         const bool ab = k0.mode == ISG_SINK_ACTBWD;
         const float* base = ab ? k0.y : k0.p;
         const int bns = ab ? k0.yns : k0.ns;
-        // lane-invariant; r is non-NULL in the residual form (host check)
-        const bool res_old = RES && k0.old != nullptr;
-        const bool res_p2a = RES && k0.p2 != nullptr && k0.p2acc != 0;
 #pragma unroll
         for (int i = 0; i < TPW; ++i) {
             const int t = min(wave + 4 * i, nt_ - 1);
@@ -457,11 +454,6 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
             for (int r = 0; r < 4; ++r) {
                 const int cl = min(rt * 16 + kk * 4 + r, Mb - 1) + m0 - k0.c0;
                 pre[i][r] = gld(base, (int64_t)cl * a.HW + (int64_t)ne * bns + pixe);
-                if constexpr (RES) {
-                    if (res_old) pro[i][r] = gld(k0.old, (int64_t)cl * a.HW + (int64_t)ne * k0.ons + pixe);
-                    prr[i][r] = gld(k0.r, (int64_t)cl * a.HW + (int64_t)ne * k0.rns + pixe);
-                    if (res_p2a) pp2[i][r] = gld(k0.p2, (int64_t)cl * a.HW + (int64_t)ne * k0.p2ns + pixe);
-                }
             }
         }
     }
@@ -566,6 +558,33 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
             }
     }
     STAMP(4);
+    // the residual form's operands (old gradient, residual term, p2's old value): issued
+    // here, after the MFMA loop — held from the first round trip they kept 3 x 4 x TPW more
+    // registers live through it (254 VGPRs: one wave per SIMD)
+    if constexpr (RES) {
+        if (a.pre_on) {
+            const SinkLite& k0 = ks.s0;
+            // lane-invariant; r is non-NULL in the residual form (host check)
+            const bool res_old = k0.old != nullptr;
+            const bool res_p2a = k0.p2 != nullptr && k0.p2acc != 0;
+#pragma unroll
+            for (int i = 0; i < TPW; ++i) {
+                const int t = min(wave + 4 * i, nt_ - 1);
+                const int rt = t / CT_, ct = t % CT_;
+                const int64_t pe = p0 + ct * 16 + pl;
+                const bool pve = pe < a.P;
+                const int ne = pve ? (int)((uint32_t)pe / (uint32_t)a.HW) : 0;
+                const int pixe = pve ? (int)pe - ne * a.HW : 0;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int64_t o = (int64_t)(min(rt * 16 + kk * 4 + r, Mb - 1) + m0 - k0.c0) * a.HW + pixe;
+                    if (res_old) pro[i][r] = gld(k0.old, o + (int64_t)ne * k0.ons);
+                    prr[i][r] = gld(k0.r, o + (int64_t)ne * k0.rns);
+                    if (res_p2a) pp2[i][r] = gld(k0.p2, o + (int64_t)ne * k0.p2ns);
+                }
+            }
+        }
+    }
 
     // ---- phase 5: epilogue; lane holds D[row = rt*16 + kk*4 + r][pixel = ct*16 + pl] ----
     // sink operands first (saved forward output for ACTBWD, old value for ACCUM), all in
