@@ -333,8 +333,11 @@ def train_leg(args, dev, world, rank, keypoints, roofline, dp_plan=None):
         trainer.stamp_at = dom
     if not args.eager:
         trainer.capture()
+    # loss=False: the step's BCE still accumulates the summed loss in the graph (reported
+    # through trainer.loss() below); only the per-step eager division for a returned mean
+    # is not launched (nothing here reads it)
     for _ in range(args.warmup):
-        trainer.step()
+        trainer.step(loss=False)
     torch.cuda.synchronize()
     trainer.stamp_reset()
 
@@ -343,7 +346,7 @@ def train_leg(args, dev, world, rank, keypoints, roofline, dp_plan=None):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        trainer.step()
+        trainer.step(loss=False)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

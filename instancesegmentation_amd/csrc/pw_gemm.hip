@@ -533,34 +533,10 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
     __syncthreads();
     STAMP(3);
 
-    // ---- phase 4: MFMA, tile t = wave + 4i -> row tile t / CT, pixel tile t % CT ---------
-    const int nt = (BM / 16) * CT;
-    int aoff[TPW], boff[TPW];
-#pragma unroll
-    for (int i = 0; i < TPW; ++i) {
-        const int t = min(wave + 4 * i, nt - 1);  // surplus tiles recompute the last one
-        aoff[i] = ((t / CT) * 16 + pl) * AS + 4 * kk;
-        boff[i] = (4 * kk) * XS + (t % CT) * 16 + pl;
-    }
-    f32x4 acc[TPW];
-#pragma unroll
-    for (int i = 0; i < TPW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int g = 0; g < Kp; g += 16) {
-        f32x4 a4[TPW];
-#pragma unroll
-        for (int i = 0; i < TPW; ++i) a4[i] = *reinterpret_cast<const f32x4*>(&As[aoff[i] + g]);
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int i = 0; i < TPW; ++i) {
-                const float bv = Xs[boff[i] + (g + j) * XS];
-                acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[i][j], bv, acc[i], 0, 0, 0);
-            }
-    }
-    STAMP(4);
     // the residual form's operands (old gradient, residual term, p2's old value): issued
-    // here, after the MFMA loop — held from the first round trip they kept 3 x 4 x TPW more
-    // registers live through it (254 VGPRs: one wave per SIMD)
+    // here, once the staging registers are dead, so they are in flight during the MFMA loop
+    // — held from the first round trip they kept 3 x 4 x TPW more registers live through
+    // the staging (254 VGPRs: one wave per SIMD)
     if constexpr (RES) {
         if (a.pre_on) {
             const SinkLite& k0 = ks.s0;
@@ -586,6 +562,31 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
         }
     }
 
+    // ---- phase 4: MFMA, tile t = wave + 4i -> row tile t / CT, pixel tile t % CT ---------
+    const int nt = (BM / 16) * CT;
+    int aoff[TPW], boff[TPW];
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) {
+        const int t = min(wave + 4 * i, nt - 1);  // surplus tiles recompute the last one
+        aoff[i] = ((t / CT) * 16 + pl) * AS + 4 * kk;
+        boff[i] = (4 * kk) * XS + (t % CT) * 16 + pl;
+    }
+    f32x4 acc[TPW];
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int g = 0; g < Kp; g += 16) {
+        f32x4 a4[TPW];
+#pragma unroll
+        for (int i = 0; i < TPW; ++i) a4[i] = *reinterpret_cast<const f32x4*>(&As[aoff[i] + g]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int i = 0; i < TPW; ++i) {
+                const float bv = Xs[boff[i] + (g + j) * XS];
+                acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[i][j], bv, acc[i], 0, 0, 0);
+            }
+    }
+    STAMP(4);
     // ---- phase 5: epilogue; lane holds D[row = rt*16 + kk*4 + r][pixel = ct*16 + pl] ----
     // sink operands first (saved forward output for ACTBWD, old value for ACCUM), all in
     // flight together; other rows load a dummy word

@@ -603,11 +603,18 @@ def _fork_pools(ol):
     if os.environ.get("ISG_NO_SIDE_POOL", "0") == "1":
         return
     recs = ol.recs
+    pool = lambda r: r.kind in (L.OP_MAXPOOL_FWD, L.OP_KP_POOL) and getattr(r, "out_range", None) is not None
     for i, r in enumerate(recs):
-        if r.kind not in (L.OP_MAXPOOL_FWD, L.OP_KP_POOL) or getattr(r, "out_range", None) is None:
+        if not pool(r):
             continue
         slot, lo, hi = r.out_range
         for j in range(i + 1, len(recs)):
+            # a pool right behind it into the same buffer (the stem's RGB max-pool and the
+            # heatmaps' pool write disjoint channel slices of init_down) follows it on the
+            # side stream: not a reader to join before
+            if (j == i + 1 and pool(recs[j]) and recs[j].out_range == r.out_range
+                    and os.environ.get("ISG_NO_POOL_PAIR", "0") != "1"):  # A/B switch
+                continue
             if any(fs == slot and lo <= off < hi for _, fs, off in recs[j].fix):
                 if j > i + 1:  # something to overlap with
                     r.flags |= Record.OPF_SIDE | Record.OPF_FORK_NOW
@@ -661,6 +668,8 @@ def _fork_late_wgrads(recs, late):
     # operands (dy, the forward input) are ready, so it forks before that kernel instead of
     # behind it (a weight gradient reads nothing the input gradient writes)
     for i in range(first_late, len(recs) - 1):
+        if os.environ.get("ISG_NO_STEM_SWAP", "0") == "1":  # A/B switch
+            break
         a, b = recs[i], recs[i + 1]
         if (a.kind == L.OP_CONV_DGRAD and b.kind == L.OP_CONV_WGRAD and a.label.startswith("dx_")
                 and b.label == "dw_" + a.label[3:]):

@@ -361,9 +361,11 @@ class Trainer:
                 e1.record()
                 self.events.append((ev, e1))
 
-    def step(self, x=None, target=None):
+    def step(self, x=None, target=None, loss=True):
         """One optimisation step. x: list of input tensors (copied into the static input
-        buffers), target: mask. Returns the loss as a device tensor (no host sync)."""
+        buffers), target: mask. Returns the loss as a device tensor (no host sync); with
+        loss=False nothing (the mean is one more eager launch per step; the summed loss
+        stays in loss_acc for loss())."""
         if self.device.type != "cuda":
             raise RuntimeError("Trainer.step runs on the MI355X only (no CPU path)")
         if x is not None:
@@ -373,7 +375,7 @@ class Trainer:
             self.target.copy_(target, non_blocking=True)
         self.step_count += 1
         self._run(self.graphs if self.graphs else self._schedule(self.split))
-        return self.loss_acc / self.logits.numel()
+        return self.loss_acc / self.logits.numel() if loss else None
 
     def loss(self):
         return (self.loss_acc / self.logits.numel()).item()
