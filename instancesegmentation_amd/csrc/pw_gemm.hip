@@ -1114,6 +1114,11 @@ int32_t isg_pw_gemm(const isg_conv_geom* g, const isg_vtensor* src, const float*
             const dim3 grid((unsigned)((a.P + best_bp - 1) / best_bp), (unsigned)((a.M + best_bm - 1) / best_bm));
             int32_t rc;
             const bool seg1 = src->nseg == 1 && out->nsink == 1;
+            static const bool log = getenv("ISG_PWX_LOG") != nullptr;  // diagnostics: the chosen tiling
+            if (log)
+                fprintf(stderr, "pwx %s M %d K %d P %lld BM %d BP %d TPW %d HY %d SEG1 %d RES %d blocks %lld\n",
+                        dgrad ? "dgrad" : "fwd", a.M, a.K, (long long)a.P, best_bm, best_bp, tpw, (int)hy,
+                        (int)seg1, b.res_on, (long long)best_blocks);
             if (best_bp == 64) rc = hy ? pwx_dispatch_seg<64, true>(b, grid, best_lds, tpw, seg1, st)
                                        : pwx_dispatch_seg<64, false>(b, grid, best_lds, tpw, seg1, st);
             else if (best_bp == 32) rc = hy ? pwx_dispatch_seg<32, true>(b, grid, best_lds, tpw, seg1, st)

@@ -646,6 +646,41 @@ def _fork_branches(ol, side_recs):
                 break
 
 
+_FORK_DELAY = os.environ.get("ISG_FORK_DELAY", "1")  # 0 off, 1 the first fork group, 2 all
+
+
+def _delay_forks(ol):
+    """Capture a forward fork group behind the main-stream record that follows it (unless
+    that record joins it). The graph runtime dispatches nodes in capture order and a node
+    that waits on another queue waits for everything already dispatched there: with the
+    side work captured first, the main stream's next node (at the step's start: the stem's
+    first conv behind the replica memset and both stem pools) waited for the whole group
+    (kernel trace: 40 us of the stem chain's start). Delaying a group only adds one main-
+    stream dependency to it; nothing a main record between fork and join reads is written
+    by the group (the join sits at its first reader, _fork_pools / _fork_branches)."""
+    if _FORK_DELAY == "0":
+        return
+    recs, out, i, done = ol.recs, [], 0, False
+    while i < len(recs):
+        r = recs[i]
+        if not r.flags & Record.OPF_SIDE or (done and _FORK_DELAY == "1"):
+            out.append(r)
+            i += 1
+            continue
+        j = i
+        while j < len(recs) and recs[j].flags & Record.OPF_SIDE:
+            j += 1
+        done = True
+        if j < len(recs) and not recs[j].flags & Record.OPF_JOIN:
+            out.append(recs[j])
+            out += recs[i:j]
+            i = j + 1
+        else:
+            out += recs[i:j]
+            i = j
+    recs[:] = out
+
+
 def _fork_late_wgrads(recs, late):
     """The executor defers side-stream weight gradients in batches until a join; at the end
     of the backward that parks the last batch (and the stem's own weight gradients, whose
@@ -1418,6 +1453,7 @@ class Plan:
                 fw.add(Record(L.OP_BN_UPDATE, L.ListRec, {"n": len(chunk)}, L.BnUpdate, chunk))
         _fork_pools(fw)
         _fork_branches(fw, side_recs)
+        _delay_forks(fw)
         self.fwd = fw.compile()
         self.act_size = g.act_size
         self.stats_size = max(g.stats_size, 8)
