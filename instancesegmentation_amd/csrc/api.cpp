@@ -119,7 +119,7 @@ static isg_vtensor resolve_y(const isg_vtensor* v) {
 extern "C" {
 
 const char* isg_last_error(void) { return g_last_error.c_str(); }
-int32_t isg_abi_version(void) { return 10; }
+int32_t isg_abi_version(void) { return 11; }
 int32_t isg_stat_replicas(void) { return ISG_STAT_REP; }
 
 int32_t isg_conv_fwd(const isg_conv_geom* g, const isg_vtensor* x_, const float* w,
@@ -464,7 +464,8 @@ int32_t isg_exec_ms2(const void* ops, int32_t nops, void* const* table, isg_stre
         bool spread = side2 != nullptr;
         for (auto& op : bt.ops)
             spread = spread && (op.first == OP_CONV_WGRAD || op.first == OP_KP_STEM_WGRAD ||
-                                op.first == OP_HEAD_FOLD || op.first == OP_GRAD_FINAL);
+                                op.first == OP_HEAD_FOLD || op.first == OP_GRAD_FINAL ||
+                                op.first == OP_BN_UPDATE);
         // a batch behind a side-only one (the gradient finalisation lists behind the replica
         // fold at ISG_SIDE_CLOSE=1) may read what that one writes: it stays on `side`, in order
         if (spread && side_serial) spread = false;

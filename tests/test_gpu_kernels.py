@@ -888,6 +888,33 @@ def test_adam_matches_golden(golden_dir):
         assert err <= 2.5e-7, f"adam step {step}: {err}"
 
 
+def test_adam_dev_counter_matches_host_steps():
+    """isg_adam_dev (ABI v11): the device step counter advances inside the update launch —
+    step[0] + 1 is every workgroup's step, the last one to finish stores it and clears the
+    ticket step[1]. Three replays over a many-workgroup buffer equal isg_adam with host
+    steps 1, 2, 3 bit for bit, the counter reads 3 and the ticket 0."""
+    n = 3 * 1024 * 1024 + 17
+    gen = torch.Generator().manual_seed(9)
+    p0 = torch.randn(n, generator=gen)
+    gs = [torch.randn(n, generator=gen) * 1e-2 for _ in range(3)]
+    live = (torch.rand(n, generator=gen) > 0.1).to(torch.uint8).to(DEV)
+    pa, pb = p0.clone().to(DEV), p0.clone().to(DEV)
+    ma, va, mb, vb = (torch.zeros(n, device=DEV) for _ in range(4))
+    step = torch.zeros(2, dtype=torch.int32, device=DEV)
+    for k, g in enumerate(gs, 1):
+        G = g.to(DEV)
+        call("isg_adam", ptr(pa), ptr(G), ptr(ma), ptr(va), ptr(live), n, k, 1e-3, 0.9, 0.999,
+             1e-8, 1e-4, stream())
+        call("isg_adam_dev", ptr(pb), ptr(G), ptr(mb), ptr(vb), ptr(live), n, ptr(step), 1e-3,
+             0.9, 0.999, 1e-8, 1e-4, stream())
+    torch.cuda.synchronize()
+    assert step.tolist() == [3, 0]
+    # the same formula; the bias corrections' pow runs on the host in one and on the device
+    # in the other (a last-ulp difference of the double may survive the rounding to f32)
+    for a_, b_ in ((pa, pb), (ma, mb), (va, vb)):
+        assert ((a_ - b_).abs() / b_.abs().clamp_min(1e-3)).max().item() <= 3e-7
+
+
 def test_paste_and_nms_bit_exact():
     from oracle import maskops_oracle as MO
     rng = np.random.Generator(np.random.PCG64(5))
