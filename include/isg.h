@@ -327,11 +327,9 @@ int32_t isg_adam(float* param, const float* grad, float* exp_avg, float* exp_avg
                  const uint8_t* live, int64_t n, int32_t step, double lr, double beta1,
                  double beta2, double eps, double weight_decay, isg_stream_t stream);
 
-/* Same update with the step counter in device memory, so the launch can be captured in a
- * HIP graph and replayed (the host-side form bakes `step` into the kernel arguments):
- * step points to int32[2] — step[0] the count, used as step[0] + 1 and advanced by this
- * call, step[1] a completion ticket that must be 0 between calls (one launch: the last
- * workgroup to finish stores the new count and resets the ticket). ABI v11. */
+/* Same update with the step counter in device memory: *step is incremented on the
+ * stream first, then used — the launch sequence can be captured in a HIP graph and
+ * replayed (the host-side form bakes `step` into the kernel arguments). */
 int32_t isg_adam_dev(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
                      const uint8_t* live, int64_t n, int32_t* step, double lr, double beta1,
                      double beta2, double eps, double weight_decay, isg_stream_t stream);

@@ -793,14 +793,10 @@ __global__ void adam_kernel(float* p, const float* g, float* m, float* v, const 
 // but 1.3e-5 (relative) off torch's second moment whenever the optimizer state comes from
 // torch (a reference checkpoint, train_instance.py:320-328).
 __global__ void adam_dev_kernel(float* p, const float* g, float* m, float* v, const uint8_t* live,
-                                int64_t n, int32_t* step, double lr, double b1, double b2,
+                                int64_t n, const int32_t* step, double lr, double b1, double b2,
                                 double eps, double wd) {
 #pragma clang fp contract(off)
-    // step[0] + 1 is this update's step; the last workgroup to finish (step[1]: a ticket,
-    // zero between calls) stores it — every workgroup has read step[0] before it takes a
-    // ticket, so no workgroup sees the new count (one launch instead of a counter kernel)
-    const int32_t s1 = __atomic_load_n(step, __ATOMIC_RELAXED) + 1;
-    const double st = (double)s1;
+    const double st = (double)*step;
     const double bc1 = 1.0 - pow(b1, st);
     const double bc2 = 1.0 - pow(b2, st);
     const float neg_step = (float)(-(lr / bc1));
@@ -824,15 +820,9 @@ __global__ void adam_dev_kernel(float* p, const float* g, float* m, float* v, co
         v[i] = vi;
         p[i] = pi + neg_step * mi / denom;
     }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence();
-        if (atomicAdd(&step[1], 1) == (int)gridDim.x - 1) {
-            atomicExch(&step[0], s1);
-            atomicExch(&step[1], 0);
-        }
-    }
 }
+
+__global__ void step_inc_kernel(int32_t* c) { *c += 1; }
 
 // One timestamp of the chip-global 100 MHz counter, accumulated (isg_stamp): sign * t added
 // to buf[slot] and t folded into the max (buf[2]) / min (buf[3]) — vector atomics whose
@@ -1056,7 +1046,7 @@ int32_t isg_adam(float* param, const float* grad, float* exp_avg, float* exp_avg
 int32_t isg_adam_dev(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
                      const uint8_t* live, int64_t n, int32_t* step, double lr, double beta1,
                      double beta2, double eps, double weight_decay, isg_stream_t st) {
-    if (!step) return isg_set_error(ISG_ERR_INVALID, "adam_dev: NULL step counter");
+    hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, st, step);
     hipLaunchKernelGGL(adam_dev_kernel, dim3(grid_for(n)), dim3(kThreads), 0, st, param, grad,
                        exp_avg, exp_avg_sq, live, n, step, lr, beta1, beta2, eps, weight_decay);
     return isg_check_launch("adam_dev_kernel");

@@ -179,9 +179,7 @@ class Trainer:
         self.exp_avg = torch.zeros_like(self.flat)
         self.exp_avg_sq = torch.zeros_like(self.flat)
         self.step_count = 0
-        # Adam's step on device: [count, completion ticket] (isg_adam_dev), step_dev = count
-        self._step_buf = torch.zeros(2, dtype=torch.int32, device=dev)
-        self.step_dev = self._step_buf[:1]
+        self.step_dev = torch.zeros(1, dtype=torch.int32, device=dev)  # Adam's step, on device
         # 4-D: image / heatmaps (float32); 3-D: keypoints [N, parts, 3] (float64, engine.Keypoints)
         self.inputs = [torch.empty(s, dtype=torch.float32 if len(s) == 4 else torch.float64,
                                    device=dev) for s in self.in_shapes]

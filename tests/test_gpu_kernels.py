@@ -889,10 +889,9 @@ def test_adam_matches_golden(golden_dir):
 
 
 def test_adam_dev_counter_matches_host_steps():
-    """isg_adam_dev (ABI v11): the device step counter advances inside the update launch —
-    step[0] + 1 is every workgroup's step, the last one to finish stores it and clears the
-    ticket step[1]. Three replays over a many-workgroup buffer equal isg_adam with host
-    steps 1, 2, 3 bit for bit, the counter reads 3 and the ticket 0."""
+    """isg_adam_dev: the device step counter advances on the stream before the update (the
+    graph-replayable form). Three calls over a many-workgroup buffer match isg_adam with
+    host steps 1, 2, 3 and the counter reads 3."""
     n = 3 * 1024 * 1024 + 17
     gen = torch.Generator().manual_seed(9)
     p0 = torch.randn(n, generator=gen)
@@ -900,7 +899,7 @@ def test_adam_dev_counter_matches_host_steps():
     live = (torch.rand(n, generator=gen) > 0.1).to(torch.uint8).to(DEV)
     pa, pb = p0.clone().to(DEV), p0.clone().to(DEV)
     ma, va, mb, vb = (torch.zeros(n, device=DEV) for _ in range(4))
-    step = torch.zeros(2, dtype=torch.int32, device=DEV)
+    step = torch.zeros(1, dtype=torch.int32, device=DEV)
     for k, g in enumerate(gs, 1):
         G = g.to(DEV)
         call("isg_adam", ptr(pa), ptr(G), ptr(ma), ptr(va), ptr(live), n, k, 1e-3, 0.9, 0.999,
@@ -908,7 +907,7 @@ def test_adam_dev_counter_matches_host_steps():
         call("isg_adam_dev", ptr(pb), ptr(G), ptr(mb), ptr(vb), ptr(live), n, ptr(step), 1e-3,
              0.9, 0.999, 1e-8, 1e-4, stream())
     torch.cuda.synchronize()
-    assert step.tolist() == [3, 0]
+    assert step.tolist() == [3]
     # the same formula; the bias corrections' pow runs on the host in one and on the device
     # in the other (a last-ulp difference of the double may survive the rounding to f32)
     for a_, b_ in ((pa, pb), (ma, mb), (va, vb)):
