@@ -717,6 +717,8 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
 
 int pwx_align16(int v) { return (v + 15) & ~15; }
 
+// (measured: 256 — one workgroup per CU, fewer and larger tiles — 3.656/3.542 -> 3.801/3.978
+// ms per step)
 constexpr int kPwxMinBlocks = 512;
 
 // LDS bytes of a (BP, BM) configuration
