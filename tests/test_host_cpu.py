@@ -291,6 +291,41 @@ def test_residual_tails_fold_into_the_next_1x1(monkeypatch):
     assert len([r for r in q.bwd.recs if r.kind == L.OP_TAIL_BWD]) == len(tails_b) + len(bwd)
 
 
+def test_forward_fork_group_captured_behind_the_next_main_record(monkeypatch):
+    """engine._delay_forks (ISG_FORK_DELAY=1, the default): the forward's first fork group
+    (the replica memset and the stem's two pools) is captured after the stem's first conv,
+    so that conv does not wait on the side queue's tail; every side record still precedes
+    its join, and a group is never moved past a record that joins it. =0 keeps the capture
+    order, =2 delays every group."""
+    from instancesegmentation_amd import engine as E
+    from instancesegmentation_amd.engine import Record
+
+    def plan(mode):
+        monkeypatch.setattr(E, "_FORK_DELAY", mode)
+        return Plan(Segment(20), [(2, 3, 128, 128), (2, 17, 3)], True, True, (False, False))
+
+    def check(recs):
+        joins = [i for i, r in enumerate(recs) if r.flags & Record.OPF_JOIN]
+        for i, r in enumerate(recs):
+            if r.flags & Record.OPF_SIDE:  # a join follows every forked record
+                assert any(j > i for j in joins), r.label
+
+    p0, p1, p2 = plan("0"), plan("1"), plan("2")
+    lab = lambda p: [r.label for r in p.fwd.recs]
+    assert sorted(lab(p0)) == sorted(lab(p1)) == sorted(lab(p2))
+    side0 = [r.label for r in p0.fwd.recs if r.flags & Record.OPF_SIDE]
+    first = lab(p1).index("init_conv.layer1")
+    assert lab(p0).index("init_conv.layer1") > lab(p0).index(side0[0])
+    assert all(lab(p1).index(x) > first for x in ("zero_wgrad_replicas", "init_down",
+                                                    "kp_pool_init_down"))
+    for p in (p0, p1, p2):
+        check(p.fwd.recs)
+    # =1 moves only the first group: the later forward groups keep their places
+    later = [x for x in side0 if x not in ("zero_wgrad_replicas", "init_down", "kp_pool_init_down")]
+    assert [lab(p1).index(x) - lab(p1).index(later[0]) for x in later] == \
+        [lab(p0).index(x) - lab(p0).index(later[0]) for x in later]
+
+
 def test_residual_tails_fold_into_a_stacked_pair():
     """In the Trainer's flat parameter layout BottleneckUp_Res's convs.0 + conv2 run as one
     stacked GEMM (Graph.conv_pair) reading the previous tail: the pair takes that tail's
