@@ -766,6 +766,8 @@ def _fold_tails(g):
             j += 1
         if j >= len(ops) or not all(_fold_reader_ok(o, t) for o in side + [ops[j]]):
             continue
+        if r.virtual and isinstance(ops[j], ConvPairOp):
+            continue  # the residual's own BatchNorm needs one sink (pw_gemm.hip host check)
         if side and os.environ.get("ISG_NO_SIDE_FOLD", "0") == "1":  # A/B switches
             continue
         if isinstance(ops[j], ConvPairOp) and os.environ.get("ISG_NO_PAIR_FOLD", "0") == "1":
