@@ -274,10 +274,7 @@ _SIDE = {}
 
 
 def side_stream_ptr(device=None):
-    """The executor's side stream of `device` (weight gradients fork onto it), or None
-    when disabled (ISG_NO_SIDE_STREAM=1)."""
-    if os.environ.get("ISG_NO_SIDE_STREAM", "0") == "1":
-        return None
+    """The executor's side stream of `device` (weight gradients fork onto it)."""
     d = torch.cuda.current_device() if device is None else torch.device(device).index
     if d is None:
         d = torch.cuda.current_device()
@@ -291,8 +288,8 @@ _SIDE2 = {}
 
 def side_stream2_ptr(device=None):
     """The executor's second side stream (batches of weight gradients are dealt over both),
-    or None when disabled (ISG_NO_SIDE2=1 or ISG_NO_SIDE_STREAM=1)."""
-    if os.environ.get("ISG_NO_SIDE2", "0") == "1" or side_stream_ptr(device) is None:
+    or None when disabled (ISG_NO_SIDE2=1, under its own parity test)."""
+    if os.environ.get("ISG_NO_SIDE2", "0") == "1":
         return None
     d = torch.cuda.current_device() if device is None else torch.device(device).index
     if d is None:

@@ -102,19 +102,7 @@ int32_t isg_tap_wgrad(const isg_conv_geom*, const isg_vtensor*, const isg_vtenso
 // part): only tap_conv / tap_wgrad index the weight with a separate channel count
 static bool partial_w(const isg_conv_geom* g) { return g->w_ci > 0 && g->w_ci != g->Ci; }
 
-// a BN_BWD segment without y (isg.h isg_vseg: y = p, at p's image stride), resolved once
-// here so no kernel has to know the convention
-static isg_vtensor resolve_y(const isg_vtensor* v) {
-    isg_vtensor r{};
-    if (!v) return r;  // nseg 0: refused by the kernels' channel checks
-    r = *v;
-    for (int i = 0; i < r.nseg && i < ISG_MAX_SEGS; ++i)
-        if (r.s[i].xform == ISG_XF_BN_BWD && !r.s[i].y) {
-            r.s[i].y = r.s[i].p;
-            r.s[i].y_n_stride = r.s[i].n_stride;
-        }
-    return r;
-}
+static isg_vtensor resolve_y(const isg_vtensor* v) { return isg_resolve_y(v); }  // residual.h
 
 extern "C" {
 
@@ -438,17 +426,12 @@ int32_t isg_exec_ms2(const void* ops, int32_t nops, void* const* table, isg_stre
     alignas(16) char buf[8192];
     hipEvent_t ev_join = nullptr, ev_join2 = nullptr, *ev_forks = nullptr;
     bool forked = false, forked2 = false;  // side-stream work outstanding since the last join
-    // both knobs are read per call (cheap next to a launch), so a test can switch them
-    const int batch = [] {
-        // weight gradients deferred per fork: 48 with two side streams and one backward
-        // part (4.415 -> 4.365 ms/step against 24; 36: 4.405, 64: 4.42, 96: 4.48 — r03y)
-        const char* e = getenv("ISG_SIDE_BATCH");
-        const int b = e ? atoi(e) : 48;
-        return b < 1 ? 1 : b;
-    }();
+    // weight gradients deferred per fork: 48 with two side streams and one backward
+    // part (4.415 -> 4.365 ms/step against 24; 36: 4.405, 64: 4.42, 96: 4.48 — r03y)
+    constexpr int batch = 48;
     // grouped 1x1 weight gradients in weight-gradient batches (4.04 -> 3.96
-    // ms/step, 2 interleaved 200-step pairs; ISG_NO_PWG_GROUP=1 off)
-    const bool pwg_group_on = getenv("ISG_NO_PWG_GROUP") == nullptr;
+    // ms/step, 2 interleaved 200-step pairs)
+    constexpr bool pwg_group_on = true;
     struct Batch {
         std::vector<std::pair<int32_t, std::string>> ops;
         hipEvent_t ev;

@@ -274,27 +274,25 @@ int32_t isg_dense_conv_fwd(const isg_conv_geom* g, const isg_vtensor* x, const f
                            const isg_sinks* out, hipStream_t st) {
     if (vt_channels(x) != g->Ci) return isg_set_error(ISG_ERR_INVALID, "conv fwd: Ci mismatch");
     if (int32_t e = check_sinks(out, g->Co, "conv fwd")) return e;
-    static const bool special_off = getenv("ISG_GENERIC_CONV") != nullptr;
-    if (!special_off && is_pointwise(g)) return isg_pw_gemm(g, x, w, out, false, st);
-    if (!special_off) {  // thin stride-1 convs on the VALU (thin_conv.hip)
+    if (is_pointwise(g)) return isg_pw_gemm(g, x, w, out, false, st);
+    {  // thin stride-1 convs on the VALU (thin_conv.hip)
         const int32_t t = isg_thin_conv(g, x, w, out, false, st);
         if (t != 0) return t < 0 ? t : 0;
     }
-    if (!special_off) {  // k 2S, stride S: the sub-pixel convT's input gradient (down_conv.hip)
+    {  // k 2S, stride S: the sub-pixel convT's input gradient (down_conv.hip)
         const int32_t t = isg_down_conv_fwd(g, x, w, out, st);
         if (t != 0) return t < 0 ? t : 0;
     }
-    if (!special_off) {  // 5x5 stride 2, <= 16 channels: the stem's second conv (down_conv.hip)
+    {  // 5x5 stride 2, <= 16 channels: the stem's second conv (down_conv.hip)
         const int32_t t = isg_s2k5_fwd(g, x, w, out, st);
         if (t != 0) return t < 0 ? t : 0;
     }
-    if (!special_off) {  // dense spatial conv, <= 48 output channels (tap_conv.hip)
+    {  // dense spatial conv, <= 48 output channels (tap_conv.hip)
         const int32_t t = isg_tap_conv(g, x, w, out, false, st);
         if (t != 0) return t < 0 ? t : 0;
     }
     // narrow outputs with spatial taps: LDS halo-tiled kernel (halo_conv.hip)
-    static const bool halo_off = special_off || getenv("ISG_NO_HALO_CONV") != nullptr;
-    if (!halo_off) {
+    {
         const int32_t h = isg_halo_conv_fwd(g, x, w, out, st);
         if (h != 0) return h < 0 ? h : 0;
     }
@@ -317,17 +315,16 @@ int32_t isg_dense_conv_dgrad(const isg_conv_geom* g, const isg_vtensor* dy, cons
                              const isg_sinks* dx, hipStream_t st) {
     if (vt_channels(dy) != g->Co) return isg_set_error(ISG_ERR_INVALID, "conv dgrad: Co mismatch");
     if (int32_t e = check_sinks(dx, g->Ci, "conv dgrad")) return e;
-    static const bool special_off = getenv("ISG_GENERIC_CONV") != nullptr;
-    if (!special_off && is_pointwise(g)) return isg_pw_gemm(g, dy, w, dx, true, st);
-    if (!special_off) {
+    if (is_pointwise(g)) return isg_pw_gemm(g, dy, w, dx, true, st);
+    {
         const int32_t t = isg_thin_conv(g, dy, w, dx, true, st);
         if (t != 0) return t < 0 ? t : 0;
     }
-    if (!special_off) {  // 5x5 stride 2 as a sub-pixel transposed conv (down_conv.hip)
+    {  // 5x5 stride 2 as a sub-pixel transposed conv (down_conv.hip)
         const int32_t t = isg_sub2_dgrad(g, dy, w, dx, st);
         if (t != 0) return t < 0 ? t : 0;
     }
-    if (!special_off) {
+    {
         const int32_t t = isg_tap_conv(g, dy, w, dx, true, st);
         if (t != 0) return t < 0 ? t : 0;
     }

@@ -1190,9 +1190,8 @@ ISG_STAMP_ACCESSOR(isg_dbg_stamps_down)
 // Returns 1 if launched, 0 if the shape is not for these kernels, <0 on error.
 int32_t isg_down_conv_fwd(const isg_conv_geom* g, const isg_vtensor* src, const float* w,
                           const isg_sinks* out, hipStream_t st) {
-    static const bool off = getenv("ISG_NO_DOWN_CONV") != nullptr;
     int S = 0;
-    if (off || !down_geom(g, S) || g->Ci > kMaxC || g->Co > kMaxM || !down_src_ok(src)) return 0;
+    if (!down_geom(g, S) || g->Ci > kMaxC || g->Co > kMaxM || !down_src_ok(src)) return 0;
     // measured: S = 2 (bottle5_1up's k4 s2, 128^2 cells) ran 15.6 -> 18.2 us here against the
     // halo kernel (too few cells per lane-owned output for the VALU form); S = 4 only
     if (S != 4) return 0;
@@ -1216,9 +1215,8 @@ int32_t isg_down_conv_fwd(const isg_conv_geom* g, const isg_vtensor* src, const 
 int32_t isg_down_conv_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x,
                             double* dw, double* dbias, int64_t rep_stride, int32_t nrep,
                             hipStream_t st) {
-    static const bool off = getenv("ISG_NO_DOWN_CONV") != nullptr;
     int S = 0;
-    if (off || dbias || !down_geom(g, S) || g->Ci > kMaxC || g->Co > kMaxM) return 0;
+    if (dbias || !down_geom(g, S) || g->Ci > kMaxC || g->Co > kMaxM) return 0;
     if (g->Ci * 4 * S * S > kThreads) return 0;
     DownArgs a{};
     a.x = *dy;   // M channels on the cell grid
@@ -1247,8 +1245,7 @@ int32_t isg_down_conv_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const
 // Returns 1 if launched, 0 if the shape is not for this kernel, <0 on error.
 int32_t isg_sub2_dgrad(const isg_conv_geom* g, const isg_vtensor* dy, const float* w,
                        const isg_sinks* dx, hipStream_t st) {
-    static const bool off = getenv("ISG_NO_SUB2_DGRAD") != nullptr;
-    if (off || g->groups != 1 || g->SH != 2 || g->SW != 2 || g->KH != 5 || g->KW != 5 ||
+    if (g->groups != 1 || g->SH != 2 || g->SW != 2 || g->KH != 5 || g->KW != 5 ||
         g->PH != 2 || g->PW != 2 || g->DH != 1 || g->DW != 1 || g->H != 2 * g->OH ||
         g->W != 2 * g->OW || g->Co > kMaxM || g->Ci > kMaxM || (g->w_ci && g->w_ci != g->Ci))
         return 0;
@@ -1266,8 +1263,7 @@ int32_t isg_sub2_dgrad(const isg_conv_geom* g, const isg_vtensor* dy, const floa
 // Returns 1 if launched, 0 if the shape is not for this kernel, <0 on error.
 int32_t isg_s2k5_fwd(const isg_conv_geom* g, const isg_vtensor* x, const float* w,
                      const isg_sinks* out, hipStream_t st) {
-    static const bool off = getenv("ISG_NO_S2K5") != nullptr;  // A/B: tap_conv instead
-    if (off || g->groups != 1 || g->SH != 2 || g->SW != 2 || g->KH != 5 || g->KW != 5 ||
+    if (g->groups != 1 || g->SH != 2 || g->SW != 2 || g->KH != 5 || g->KW != 5 ||
         g->PH != 2 || g->PW != 2 || g->DH != 1 || g->DW != 1 || g->H != 2 * g->OH ||
         g->W != 2 * g->OW || g->W % 4 || g->Co > kMaxM || g->Ci > kMaxM ||
         (g->w_ci && g->w_ci < g->Ci) || !down_src_ok(x))
@@ -1317,8 +1313,7 @@ int32_t isg_s2k5_fwd(const isg_conv_geom* g, const isg_vtensor* x, const float* 
 // Returns 1 if launched, 0 if the shape is not for this kernel, <0 on error.
 int32_t isg_s2k5_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x,
                        double* dw, double* dbias, int64_t rep_stride, int32_t nrep, hipStream_t st) {
-    static const bool off = getenv("ISG_NO_S2K5_WGRAD") != nullptr;
-    if (off || g->groups != 1 || g->SH != 2 || g->SW != 2 || g->KH != 5 || g->KW != 5 ||
+    if (g->groups != 1 || g->SH != 2 || g->SW != 2 || g->KH != 5 || g->KW != 5 ||
         g->PH != 2 || g->PW != 2 || g->DH != 1 || g->DW != 1 || g->H != 2 * g->OH ||
         g->W != 2 * g->OW || g->OW % 4 || g->Co > kMaxM || g->Ci > kMaxM ||
         (g->w_ci && g->w_ci < g->Ci) || !down_src_ok(x) || !down_src_ok(dy))
@@ -1353,8 +1348,7 @@ int32_t isg_s2k5_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_
     bool yb = false;
     for (int i = 0; i < dy->nseg; ++i) yb |= dy->s[i].xform == ISG_XF_BN_BWD && dy->s[i].y != dy->s[i].p;
     const size_t lds = (size_t)2 * kWgLds * sizeof(float);
-    static const bool no_narrow = getenv("ISG_NO_S2W_NARROW") != nullptr;  // A/B
-    const int nar = no_narrow || a.C > 4 ? 0 : a.C <= 3 ? 1 : 2;
+    const int nar = a.C > 4 ? 0 : a.C <= 3 ? 1 : 2;
     auto k = yb ? (nar == 1 ? s2k5_wgrad_kernel<true, 5> : nar == 2 ? s2k5_wgrad_kernel<true, 7> : s2k5_wgrad_kernel<true, 0>)
                 : (nar == 1 ? s2k5_wgrad_kernel<false, 5> : nar == 2 ? s2k5_wgrad_kernel<false, 7> : s2k5_wgrad_kernel<false, 0>);
     const int ki = 3 * yb + nar;

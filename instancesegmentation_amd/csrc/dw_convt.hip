@@ -336,8 +336,7 @@ __global__ __launch_bounds__(kThreads) void dw_tile_kernel(DwArgs a) {
 // 1: launched, 0: shape not for the tiled kernel
 template <bool DGRAD>
 int dw_tile_try(const isg_conv_geom* g, const DwArgs& a, hipStream_t st) {
-    static const bool off = getenv("ISG_NO_DW_TILE") != nullptr;
-    if (off || g->SH != 1 || g->SW != 1 || g->OH != g->H || g->OW != g->W || g->W % 4)
+    if (g->SH != 1 || g->SW != 1 || g->OH != g->H || g->OW != g->W || g->W % 4)
         return 0;
     const isg_sink& o = a.out;
     if (o.mode == ISG_SINK_NONE || ((uintptr_t)o.p & 15) || o.n_stride % 4 ||
@@ -864,9 +863,8 @@ int32_t isg_depthwise_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const
     a.N = g->N; a.C = g->Ci; a.H = g->H; a.W = g->W; a.OH = g->OH; a.OW = g->OW;
     a.KH = g->KH; a.KW = g->KW; a.PH = g->PH; a.PW = g->PW; a.DH = g->DH; a.DW = g->DW;
     {
-        static const bool off = getenv("ISG_NO_DW_TILE") != nullptr;
         const isg_vseg& d = a.dy;
-        const bool ok = !off && g->SH == 1 && g->SW == 1 && g->OH == g->H && g->OW == g->W && g->W % 4 == 0 &&
+        const bool ok = g->SH == 1 && g->SW == 1 && g->OH == g->H && g->OW == g->W && g->W % 4 == 0 &&
                         !((uintptr_t)d.p & 15) && d.n_stride % 4 == 0 &&
                         (d.xform != ISG_XF_BN_BWD || (!((uintptr_t)d.y & 15) && d.y_n_stride % 4 == 0)) &&
                         (g->KH - 1) * g->DH <= 16 && (g->KW - 1) * g->DW <= 16;
@@ -898,10 +896,14 @@ int32_t isg_depthwise_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const
 
 // dx and dw of one depthwise layer (isg.h isg_depthwise_bwd): the fused tile kernel when
 // both tile kernels would run, else the two separate entry points in order
-int32_t isg_depthwise_bwd(const isg_conv_geom* g, const isg_vtensor* dy, const float* w,
-                          const isg_sinks* dx, const isg_vtensor* x, double* dw, double* dbias,
+int32_t isg_depthwise_bwd(const isg_conv_geom* g, const isg_vtensor* dy_, const float* w,
+                          const isg_sinks* dx, const isg_vtensor* x_, double* dw, double* dbias,
                           int64_t rep_stride, int32_t nrep, hipStream_t st) {
-    if (!g || !dy || !x) return isg_set_error(ISG_ERR_INVALID, "depthwise bwd: NULL argument");
+    if (!g || !dy_ || !x_) return isg_set_error(ISG_ERR_INVALID, "depthwise bwd: NULL argument");
+    // a BN_BWD segment with y NULL means y = p (isg.h): resolved here like the conv entry
+    // points do, so neither the fused kernel nor the two fallbacks read through NULL
+    const isg_vtensor dyr = isg_resolve_y(dy_), xr = isg_resolve_y(x_);
+    const isg_vtensor *dy = &dyr, *x = &xr;
     if (g->groups <= 1 || g->groups != g->Ci || g->Ci != g->Co)
         return isg_set_error(ISG_ERR_UNSUPPORTED, "depthwise bwd: not a depthwise layer");
     if (isg_vt_res(dy) || isg_vt_res(x) || isg_sinks_res(dx))
@@ -911,8 +913,7 @@ int32_t isg_depthwise_bwd(const isg_conv_geom* g, const isg_vtensor* dy, const f
     const bool has_dx = dx && dx->nsink > 0;
     bool fuse = has_dx && dw && dy->nseg == 1 && x->nseg == 1 && dx->nsink == 1 &&
                 x->s[0].xform != ISG_XF_BN_BWD && g->SH == 1 && g->SW == 1 && g->OH == g->H &&
-                g->OW == g->W && g->W % 4 == 0 && (g->KH - 1) * g->DH <= 16 && (g->KW - 1) * g->DW <= 16 &&
-                getenv("ISG_NO_DW_TILE") == nullptr;
+                g->OW == g->W && g->W % 4 == 0 && (g->KH - 1) * g->DH <= 16 && (g->KW - 1) * g->DW <= 16;
     const int KH = g->KH, KW = g->KW;
     fuse = fuse && ((KH == 3 && KW == 3) || (KH == 5 && KW == 1) || (KH == 1 && KW == 5));
     if (fuse) {

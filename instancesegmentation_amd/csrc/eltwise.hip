@@ -444,8 +444,7 @@ bool al(const void* p, int b) { return ((uintptr_t)p % b) == 0; }
 bool tail4_ok(const isg_tail& t, const isg_tail_grad* tg) {
     // planes of >= 128^2 pixels only: at 64^2 the halved grid (512 workgroups at 128
     // channels) measured 0.3-0.4 us slower per op, at 128^2 and up 1.3-2.5 us faster (r03v)
-    static const bool off = getenv("ISG_NO_TAIL4") != nullptr;
-    if (off || t.W % 4 || (int64_t)t.H * t.W < 16384) return false;
+    if (t.W % 4 || (int64_t)t.H * t.W < 16384) return false;
     for (int i = 0; i < t.nterm; ++i) {
         const isg_vseg& s = t.term[i];
         if (!al(s.p, t.up[i] ? 8 : 16) || s.n_stride % (t.up[i] ? 2 : 4)) return false;

@@ -398,11 +398,7 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
     const int trow = min(tid, Mb - 1);
     const SinkLoad skl = sink_issue(ks, m0 + trow, w, stat_on);
     // the residual's BatchNorm: forward per input channel, input gradient per output row
-#ifdef ISG_NO_RBN_KERNEL  // A/B build (tools/build_variant.sh): the residual-BN code compiled out
-    const bool rbn_in = false, rbn_out = false;
-#else
     const bool rbn_in = SEG1 && HY && a.rbn_in != 0, rbn_out = RES && a.rbn_out != 0;
-#endif
 
     // weight slot i -> (row, quad): quads per row padded to 2^wsh, so the split is a shift
     // and a mask; forward rows are m with k contiguous, dgrad rows are k with m contiguous.
@@ -958,8 +954,7 @@ bool sinks_aligned16(const isg_sinks& sk) {
 
 // 1: launched, 0: not applicable, < 0: error
 int32_t thin_pw(const PwArgs& a, hipStream_t st) {
-    static const bool off = getenv("ISG_NO_THIN_PW") != nullptr;
-    if (off || a.HW % 4 || !pwx_src_ok(a.src, a.HW) || !sinks_aligned16(a.out))
+    if (a.HW % 4 || !pwx_src_ok(a.src, a.HW) || !sinks_aligned16(a.out))
         return 0;
     ThinPwArgs b{};
     b.src = a.src; b.out = a.out; b.w = a.w; b.rs = a.rs; b.cs = a.cs; b.HW = a.HW;
@@ -1022,7 +1017,6 @@ int32_t isg_pw_gemm(const isg_conv_geom* g, const isg_vtensor* src, const float*
         const int32_t t = thin_pw(a, st);
         if (t != 0) return t < 0 ? t : 0;
     }
-    static const bool slab_off = getenv("ISG_PW_CHUNKED") != nullptr;
     int wmode = 0;
     if (aligned16(w)) {
         if (!dgrad && a.K % 4 == 0) wmode = 1;
@@ -1034,15 +1028,12 @@ int32_t isg_pw_gemm(const isg_conv_geom* g, const isg_vtensor* src, const float*
     // per-workgroup phase chain loses to the chunked kernel (the 128 -> 48 dgrads
     // 12.2 -> 17.0 us, the 256 -> 128 resconv forward 27.6 -> 49.5 us)
     // (r02g per-op tables: the 64^2 128 -> 48 forwards 13.8 -> 12.5 us on the slab)
-    static const bool fwd_small = getenv("ISG_NO_PW_FWD_SLAB_SMALL") == nullptr;
     // (round 3, after the single-segment prologue: the 48 -> 128 expansions and their
     // transposes, M = 128 rows over K = 48, on 32 x 64 tiles — kbench fwd 15.3 -> 14.8 us,
     // dgrad 18.4 -> 17.2 us against the chunked kernel)
-    static const bool wide_rows = getenv("ISG_NO_PWX_WIDE_ROWS") == nullptr;
     const bool slab_pays = res || (!dgrad && a.P >= 65536) || (dgrad && a.M <= 64 && a.K <= 128) ||
-                           (fwd_small && !dgrad && a.M <= 64 && a.K <= 128) ||
-                           (wide_rows && a.M <= 128 && a.K <= 64);
-    if ((!slab_off || res) && slab_pays && wmode && pwx_src_ok(*src, a.HW) && a.P < ((int64_t)1 << 31)) {
+                           (!dgrad && a.M <= 64 && a.K <= 128) || (a.M <= 128 && a.K <= 64);
+    if (slab_pays && wmode && pwx_src_ok(*src, a.HW) && a.P < ((int64_t)1 << 31)) {
         PwxArgs b{};
         b.src = a.src; b.out = a.out; b.w = w; b.rs = a.rs; b.cs = a.cs;
         b.HW = a.HW; b.M = a.M; b.K = a.K; b.Kp = (a.K + 15) / 16 * 16; b.P = a.P;

@@ -11,6 +11,19 @@ inline bool isg_vt_res(const isg_vtensor* v) {
     for (int i = 0; i < v->nseg && i < ISG_MAX_SEGS; ++i) r |= isg_seg_res(v->s[i]);
     return r;
 }
+// a BN_BWD segment without y (isg.h isg_vseg: y = p, at p's image stride), resolved at
+// every public entry point that takes a vtensor, so no kernel has to know the convention
+inline isg_vtensor isg_resolve_y(const isg_vtensor* v) {
+    isg_vtensor r{};
+    if (!v) return r;  // nseg 0: refused by the kernels' channel checks
+    r = *v;
+    for (int i = 0; i < r.nseg && i < ISG_MAX_SEGS; ++i)
+        if (r.s[i].xform == ISG_XF_BN_BWD && !r.s[i].y) {
+            r.s[i].y = r.s[i].p;
+            r.s[i].y_n_stride = r.s[i].n_stride;
+        }
+    return r;
+}
 inline bool isg_sinks_res(const isg_sinks* k) {
     if (!k) return false;
     bool r = false;

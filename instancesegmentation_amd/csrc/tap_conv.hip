@@ -432,10 +432,7 @@ int32_t tap_launch_g(const TapArgs& a, size_t lds, int G, bool yb, bool pair, hi
 //   dgrad = 1: out[Ci] = conv^T(dy)   src = dy (C = Co), rows M = Ci, weight [Co][Ci][KH][KW]
 int32_t isg_tap_conv(const isg_conv_geom* g, const isg_vtensor* src, const float* w,
                      const isg_sinks* out, bool dgrad, hipStream_t st) {
-    static const bool off = getenv("ISG_NO_TAP_CONV") != nullptr;
-    static const bool off_fwd = getenv("ISG_NO_TAP_FWD") != nullptr;   // debugging
-    static const bool off_dg = getenv("ISG_NO_TAP_DGRAD") != nullptr;  // debugging
-    if (off || (dgrad ? off_dg : off_fwd) || g->groups != 1) return 0;
+    if (g->groups != 1) return 0;
     TapArgs a{};
     a.q = TapGeo{g->KH, g->KW, g->SH, g->SW, g->PH, g->PW, g->DH, g->DW, dgrad ? 1 : 0};
     const int KK = g->KH * g->KW;

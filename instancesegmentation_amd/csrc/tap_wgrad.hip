@@ -666,8 +666,7 @@ bool twa_layout(TwaArgs& a, int& ntiles) {
 // Returns 1 if launched, 0 if the shape is not for this kernel, <0 on error.
 int32_t twa_try(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, double* dw,
                 double* dbias, int64_t rep_stride, int32_t nrep, hipStream_t st) {
-    static const bool off = getenv("ISG_NO_TWA") != nullptr;
-    if (off || g->SH != 2 || g->SW != 2 || g->DH != 1 || g->DW != 1) return 0;
+    if (g->SH != 2 || g->SW != 2 || g->DH != 1 || g->DW != 1) return 0;
     if (g->PW % 2 || g->W % 2) return 0;
     const int KK = g->KH * g->KW;
     // measured (kbench): the stem layer1 (20 x 25 columns) 433 -> 308 us; the 16-channel
@@ -748,8 +747,7 @@ int32_t twa_try(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor
 // Returns 1 if launched, 0 if the shape is not for this kernel, <0 on error.
 int32_t isg_tap_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, double* dw,
                       double* dbias, int64_t rep_stride, int32_t nrep, hipStream_t st) {
-    static const bool off = getenv("ISG_NO_TAP_WGRAD") != nullptr;
-    if (off || g->groups != 1 || g->Co > 16 || g->Ci > kMaxC) return 0;
+    if (g->groups != 1 || g->Co > 16 || g->Ci > kMaxC) return 0;
     for (int i = 0; i < x->nseg; ++i)
         if (x->s[i].xform == ISG_XF_BN_BWD) return 0;
     if ((int64_t)g->H * g->W * 4 < (1ll << 31) && (int64_t)g->OH * g->OW * 4 < (1ll << 31)) {

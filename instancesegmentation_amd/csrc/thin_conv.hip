@@ -301,8 +301,7 @@ __global__ __launch_bounds__(kThreads) void thin_wgrad3_x4_kernel(ThinWgArgs a) 
 // Returns 1 if launched, 0 if the shape is not for this kernel, <0 on error.
 int32_t isg_thin_conv(const isg_conv_geom* g, const isg_vtensor* src, const float* w,
                       const isg_sinks* out, bool dgrad, hipStream_t st) {
-    static const bool off = getenv("ISG_NO_THIN_CONV") != nullptr;
-    if (off || g->groups != 1 || g->SH != 1 || g->SW != 1 || g->KH != g->KW || g->PH != g->PW ||
+    if (g->groups != 1 || g->SH != 1 || g->SW != 1 || g->KH != g->KW || g->PH != g->PW ||
         g->DH != g->DW)
         return 0;
     const int C = dgrad ? g->Co : g->Ci, M = dgrad ? g->Ci : g->Co, K = g->KH;
@@ -341,8 +340,7 @@ int32_t isg_thin_conv(const isg_conv_geom* g, const isg_vtensor* src, const floa
 // Returns 1 if launched, 0 if the shape is not for this kernel, <0 on error.
 int32_t isg_thin_wgrad(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, double* dw,
                        double* dbias, int64_t rep_stride, int32_t nrep, hipStream_t st) {
-    static const bool off = getenv("ISG_NO_THIN_WGRAD") != nullptr;
-    if (off || g->groups != 1 || g->SH != 1 || g->SW != 1 || g->KH != 3 || g->KW != 3 ||
+    if (g->groups != 1 || g->SH != 1 || g->SW != 1 || g->KH != 3 || g->KW != 3 ||
         g->PH != 1 || g->PW != 1 || g->DH != 1 || g->DW != 1 || g->OH != g->H || g->OW != g->W ||
         g->W % 4 || dy->nseg != 1 || x->nseg != 1 || (g->w_ci > 0 && g->w_ci != g->Ci))
         return 0;

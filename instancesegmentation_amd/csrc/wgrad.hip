@@ -878,8 +878,6 @@ struct PwgPlan {
 // the shape and operand checks of pwg_try and the launch geometry; false: not for pwg
 bool pwg_plan(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, double* dw,
               double* dbias, int64_t rep_stride, int32_t nrep, PwgPlan& pl) {
-    static const bool off = getenv("ISG_PWG_OFF") != nullptr;
-    if (off) return false;
     if (!(g->KH == 1 && g->KW == 1 && g->SH == 1 && g->SW == 1 && g->PH == 0 && g->PW == 0))
         return false;
     if (g->OH != g->H || g->OW != g->W || g->Co < 2) return false;
@@ -981,8 +979,6 @@ int32_t pwg_run(const PwgPlan* const* pl, int n, hipStream_t st) {
 int32_t pwg_try(const isg_conv_geom* g, const isg_vtensor* dy, const isg_vtensor* x, double* dw,
                 double* dbias, int64_t rep_stride, int32_t nrep, hipStream_t st) {
     {
-        static const bool off = getenv("ISG_PWG_OFF") != nullptr;
-        if (off) return 0;
         if (!(g->KH == 1 && g->KW == 1 && g->SH == 1 && g->SW == 1 && g->PH == 0 && g->PW == 0))
             return 0;
         if (g->OH != g->H || g->OW != g->W || g->Co < 2) return 0;

@@ -317,6 +317,10 @@ class Graph:
             off += self.params[k].numel()  # packed: the flat grad buffer in layout order
         self.pgrad_size = off
         self.used_params = set()
+        # (tensor index of a's weight, of b's weight, a's weight bytes) of every sibling pair
+        # emitted as ONE stacked GEMM: the plan reads b's rows through a's pointer, so it is
+        # valid only while the two weights stay adjacent (Plan.stacking_holds)
+        self.stacked = []
 
     # -- naming ------------------------------------------------------------------------
     def pname(self, mod, attr):
@@ -447,9 +451,7 @@ class Graph:
         over the stacked rows. Returns (value_a, value_b), or None when the pair does not
         qualify (then the caller emits two convs): not 1x1 / stride 1 / dense, no BN, or the
         weights not adjacent in the layout AND in memory (a module's own parameters are
-        separate tensors; ISG_NO_STACK=1 off)."""
-        if os.environ.get("ISG_NO_STACK", "0") == "1":
-            return None
+        separate tensors)."""
         a, b = ca.conv, cb.conv
         for c in (a, b):
             if not (c.kernel_size == (1, 1) and c.stride == (1, 1) and c.padding == (0, 0)
@@ -467,6 +469,8 @@ class Graph:
         if (wa.device != wb.device or not wa.is_contiguous() or not wb.is_contiguous()
                 or wb.data_ptr() != wa.data_ptr() + wa.numel() * wa.element_size()):
             return None
+        self.stacked.append((self.tensor_names.index(ka), self.tensor_names.index(kb),
+                             wa.numel() * wa.element_size()))
         H, W = x.H, x.W
         geom = dict(N=self.N, Ci=x.C, H=H, W=W, Co=a.out_channels + b.out_channels, OH=H, OW=W,
                     KH=1, KW=1, SH=1, SW=1, PH=0, PW=0, DH=1, DW=1, groups=1)
@@ -504,9 +508,7 @@ class Graph:
         """The mask head (segment.py:435-438, 504-505): ConvTranspose2d(16 -> 4, k8, s4, p2)
         then Conv2d(4 -> 1, 3x3, p1) as ONE fused op (isg_mask_head_*: the 4-channel
         intermediate never reaches HBM), or None when the modules / input do not have
-        that exact shape (the caller then emits the two convolutions) or ISG_NO_HEAD=1."""
-        if os.environ.get("ISG_NO_HEAD", "0") == "1":
-            return None
+        that exact shape (the caller then emits the two convolutions)."""
         if not (ct.in_channels == 16 and ct.out_channels == 4 and ct.kernel_size == (8, 8)
                 and ct.stride == (4, 4) and ct.padding == (2, 2) and ct.groups == 1
                 and ct.dilation == (1, 1) and not any(ct.output_padding)
@@ -600,8 +602,6 @@ def _fork_pools(ol):
     nothing writes what they read or produce until their first consumer: fork each onto
     the executor's side stream and join right before the first later op that touches its
     output buffer (out_range = the whole buffer, _buf_range)."""
-    if os.environ.get("ISG_NO_SIDE_POOL", "0") == "1":
-        return
     recs = ol.recs
     pool = lambda r: r.kind in (L.OP_MAXPOOL_FWD, L.OP_KP_POOL) and getattr(r, "out_range", None) is not None
     for i, r in enumerate(recs):
@@ -612,8 +612,7 @@ def _fork_pools(ol):
             # a pool right behind it into the same buffer (the stem's RGB max-pool and the
             # heatmaps' pool write disjoint channel slices of init_down) follows it on the
             # side stream: not a reader to join before
-            if (j == i + 1 and pool(recs[j]) and recs[j].out_range == r.out_range
-                    and os.environ.get("ISG_NO_POOL_PAIR", "0") != "1"):  # A/B switch
+            if j == i + 1 and pool(recs[j]) and recs[j].out_range == r.out_range:
                 continue
             if any(fs == slot and lo <= off < hi for _, fs, off in recs[j].fix):
                 if j > i + 1:  # something to overlap with
@@ -629,7 +628,7 @@ def _fork_branches(ol, side_recs):
     input). The first later main-stream record that reads any byte the branch writes —
     its output or its BN statistics/coefficients — joins the side stream. Forward only:
     backward sinks accumulate into shared gradient buffers."""
-    if os.environ.get("ISG_NO_SIDE_BRANCH", "0") == "1" or not side_recs:
+    if not side_recs:
         return
     recs = ol.recs
     pos = {id(r): i for i, r in enumerate(recs)}
@@ -687,7 +686,7 @@ def _fork_late_wgrads(recs, late):
     dy is ready before the stem's input-gradient chain runs) behind the whole stem chain.
     Fork the pending batch where the stem's backward begins, and each stem weight gradient
     at its place (OPF_FORK_NOW), so they overlap the stem's input-gradient kernels."""
-    if os.environ.get("ISG_NO_LATE_FORK", "0") == "1" or not late:
+    if not late:
         return
     tag = late.rstrip(".")
     first_late = next((i for i, r in enumerate(recs) if tag in r.label), None)
@@ -703,15 +702,10 @@ def _fork_late_wgrads(recs, late):
     # operands (dy, the forward input) are ready, so it forks before that kernel instead of
     # behind it (a weight gradient reads nothing the input gradient writes)
     for i in range(first_late, len(recs) - 1):
-        if os.environ.get("ISG_NO_STEM_SWAP", "0") == "1":  # A/B switch
-            break
         a, b = recs[i], recs[i + 1]
         if (a.kind == L.OP_CONV_DGRAD and b.kind == L.OP_CONV_WGRAD and a.label.startswith("dx_")
                 and b.label == "dw_" + a.label[3:]):
             recs[i], recs[i + 1] = b, a
-
-
-_GF_MAIN = os.environ.get("ISG_GRAD_FINAL_MAIN", "0") == "1"  # A/B: finalisation on the main stream
 
 
 def _fold_tails(g):
@@ -743,8 +737,7 @@ def _fold_tails(g):
         # the residual: a materialised value, or a second BatchNorm'd conv output (the
         # BottleneckDown2 / BottleneckDim_Res tails, segment.py:147-148, 202-207)
         r_ok = not r.virtual or (g.train and r.bn is not None and r.act == "none" and r.c0 == 0
-                                 and r.C == r.buf.C and r.buf is not y.buf
-                                 and os.environ.get("ISG_NO_RBN_FOLD", "0") != "1")
+                                 and r.C == r.buf.C and r.buf is not y.buf)
         # y: a BatchNorm'd raw conv output, or (BN folded into the conv) a plain one under
         # the tail's activation (the residual form is a BN_FWD segment either way)
         y_ok = y.act == "none" and (y.bn is not None or (not y.virtual and t.act != "none"))
@@ -768,10 +761,6 @@ def _fold_tails(g):
             continue
         if r.virtual and isinstance(ops[j], ConvPairOp):
             continue  # the residual's own BatchNorm needs one sink (pw_gemm.hip host check)
-        if side and os.environ.get("ISG_NO_SIDE_FOLD", "0") == "1":  # A/B switches
-            continue
-        if isinstance(ops[j], ConvPairOp) and os.environ.get("ISG_NO_PAIR_FOLD", "0") == "1":
-            continue
         c = ops[j]
         t.fwd_folded = True
         for o in side:
@@ -1250,7 +1239,7 @@ class HeadOp:
         # replicas by a side-stream op (isg.h isg_mask_head.dw1_part): the kernel's tail was
         # its 4096 fp64 atomics per workgroup
         nslab = L.head_part_floats(g.N, self.x.H, self.x.W)
-        if nslab > 0 and os.environ.get("ISG_NO_HEAD_FOLD", "0") != "1":
+        if nslab > 0:
             part = gs.alloc(Buf(S_GRAD, 1, 1, 1, nslab, "head_dw1_part"), "head_dw1_part")
             s["dw1_part"] = part.ptr()
         fl, nb = self._cost()
@@ -1420,8 +1409,7 @@ class Plan:
         fw = OpList()
         if g.stats_size:
             fw.add(Record(L.OP_MEMSET, L.MemsetRec, {"p": Ptr(S_STATS), "bytes": g.stats_size * 8}))
-        self.wrep_zero_fwd = need_grad and os.environ.get("ISG_WREP_ZERO_BWD", "0") != "1"
-        if self.wrep_zero_fwd:
+        if need_grad:
             # the weight-gradient replicas (L.WREP fp64 copies of the flat gradient, 34 MB for
             # Segment(20)) are zeroed on the side stream under the forward instead of at the
             # head of the backward's critical path; the forward's final join covers it
@@ -1464,6 +1452,18 @@ class Plan:
         self.bwd = None
         if need_grad:
             self._build_backward(g, ins)
+
+    def stacking_holds(self, tensors):
+        """True while every stacked sibling pair's weights (Graph.stacked) are still adjacent
+        in memory in `tensors` (the module's parameters + buffers in named order). Parameters
+        rebound after the plan was built (load_state_dict(assign=True), `p.data = ...`, a
+        re-flatten) can break that; the caller then rebuilds the plan."""
+        for ia, ib, nb in self.graph.stacked:
+            wa, wb = tensors[ia], tensors[ib]
+            if (wa.device != wb.device or not wa.is_contiguous() or not wb.is_contiguous()
+                    or wb.data_ptr() != wa.data_ptr() + nb):
+                return False
+        return True
 
     @staticmethod
     def _late_prefix(g):
@@ -1541,14 +1541,11 @@ class Plan:
             if isinstance(v, Value) and v.grad:
                 b = v.segs[0].buf
                 gs.external[id(b)] = Buf(S_DIN[i], b.N, b.C, b.H, b.W, f"din{i}")
-        bw = OpList()
         # weight gradients accumulate (fp64 atomics of fp32 workgroup partials: exact, so
         # order-independent, isg.h ISG_WREP) into L.WREP replicas — zeroed by the forward
         # (its side-stream memset) — folded into S_PGRAD by OP_SUM_REP before the BN/PReLU
         # finalisation overwrites its own entries
-        if not self.wrep_zero_fwd:  # A/B: the replicas zeroed at the head of the backward
-            bw.add(Record(L.OP_MEMSET, L.MemsetRec, {"p": Ptr(S_WREP),
-                                                     "bytes": L.WREP * g.pgrad_size * 8}))
+        bw = OpList()
         body = OpList()
         gs.pending_final = []
         for op in reversed(g.ops):
@@ -1610,7 +1607,7 @@ class Plan:
                 recs.append(Record(L.OP_GRAD_FINAL, L.ListRec, {"n": len(chunk)}, L.GradFinal,
                                    chunk))
             for r in recs:
-                if side or (r.kind == L.OP_GRAD_FINAL and not _GF_MAIN):
+                if side or r.kind == L.OP_GRAD_FINAL:
                     # the finalisation lists are independent of each other: forked behind
                     # the fold, dealt over both side streams (api.cpp), joined at the end
                     # of the list (5 launches of ~5 us each ran back to back on the main
@@ -1623,9 +1620,6 @@ class Plan:
         # backward runs last). The Trainer all-reduces bucket 1 on RCCL's stream while the
         # stem backward (body[split:]) runs. split == len(body): one bucket at the end.
         part1, part2 = OpList(), OpList()
-        if bw.recs:
-            part1.add(bw.recs[0])  # the replica memset (ISG_WREP_ZERO_BWD=1)
-        n0 = len(bw.recs)
         for r in body.recs[:split]:
             part1.add(r)
         if split < len(body.recs):
@@ -1638,7 +1632,7 @@ class Plan:
         else:
             cut = 0
             close(part1, 0, g.pgrad_size, [it for _, it in items])
-        for r in part1.recs[n0:] + part2.recs:
+        for r in part1.recs + part2.recs:
             bw.add(r)
         self.bucket_cut = cut
         self.bwd_parts = [part1.compile()] + ([part2.compile()] if part2.recs else [])

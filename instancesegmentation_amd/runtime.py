@@ -195,6 +195,8 @@ def run_module(mod, xs):
     in_grad = tuple(bool(grad_on and x.requires_grad) for x in xs)
     key = (tuple(tuple(x.shape) for x in xs), train, need_grad or any(in_grad), in_grad)
     runner = mod._plans.get(key)
+    if runner is not None and not runner.plan.stacking_holds(module_tensors(mod)):
+        runner = None  # a stacked pair's weights were rebound apart: plan again (two convs)
     if runner is None:
         # sibling 1x1 convs run stacked where their weights are adjacent in memory
         # (train.flatten_module with engine.param_layout); separate tensors: two convs

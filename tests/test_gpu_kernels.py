@@ -679,18 +679,23 @@ def test_depthwise(cfg):
     close(DB, dy.sum((0, 2, 3)), what="dw dbias")
 
 
+@pytest.mark.parametrize("ynull", [False, True], ids=["y", "ynull"])
 @pytest.mark.parametrize("cfg", DW_CFG)
-def test_depthwise_bwd_fused(cfg):
+def test_depthwise_bwd_fused(cfg, ynull):
     """isg_depthwise_bwd (one launch, the dy tile staged once) against the two calls it
     replaces, bit for bit — dx through an ACTBWD sink with its BatchNorm-backward and PReLU
     slope sums, the weight/bias-gradient replicas — with dy the BatchNorm backward of the
-    layer's output and x a BatchNorm + PReLU view; and the weight gradient against fp64."""
+    layer's output and x a BatchNorm + PReLU view; and the weight gradient against fp64.
+    ynull: the fused call gets the BN_BWD segment with y = NULL (isg.h: y = p), the
+    separate calls the same y spelled out — resolved at the entry point."""
     C, H, W, kh, kw, ph, pw, d = cfg
     N = 2
     ge = dict(N=N, Ci=C, H=H, W=W, Co=C, OH=H, OW=W, KH=kh, KW=kw, SH=1, SW=1, PH=ph, PW=pw,
               DH=d, DW=d, groups=C)
     yraw = rnd(N, C, H, W, seed=41) + 0.3
     gbn = rnd(N, C, H, W, seed=42)
+    if ynull:  # y = p: the BatchNorm backward rebuilt from the gradient buffer itself
+        yraw = gbn
     og, ob, st, _ = _bn_train_state(yraw, gbn, 43)
     dy = _bn_bwd_ref(yraw, gbn, og)
     x = rnd(N, C, H, W, seed=44)
@@ -706,6 +711,8 @@ def test_depthwise_bwd_fused(cfg):
         ST = rep_from(st)
         dyseg = {"p": ptr(Gb), "y": ptr(Yr), "n_stride": C * H * W, "y_n_stride": C * H * W,
                  "C": C, "xform": L.XF_BN_BWD, "bn": bn_spec_train(GA, BE, ST, N * H * W)}
+        if ynull and fused:
+            dyseg.update(y=0, y_n_stride=0)
         xseg = {"p": ptr(X), "n_stride": C * H * W, "C": C, "xform": L.XF_BN_FWD,
                 "act": L.ACT["prelu"], "slope": ptr(G[4]), "bn": bn_spec_eval(*G[:4])}
         DX = torch.full((N, C, H, W), float("nan"), device=DEV)

@@ -11,7 +11,8 @@ import torch
 
 from instancesegmentation_amd import _lib as L
 from instancesegmentation_amd.engine import Plan
-from instancesegmentation_amd.model.segment import Segment
+from instancesegmentation_amd.model.segment import BottleneckDim_Res, BottleneckDown2, Segment
+from instancesegmentation_amd.runtime import EngineModule
 from oracle import maskops_oracle as MO
 from tests.golden_util import SEGMENT_FIXTURES, SegmentFixture
 
@@ -349,6 +350,60 @@ def test_residual_tails_fold_into_a_stacked_pair():
         assert dx.kind == L.OP_CONV_DGRAD and L.ConvRec.from_buffer_copy(dx.body).out.nsink == 1
     fwd = {t.out.name for t in ops if getattr(t, "fwd_folded", False)}
     assert len(fwd) == 17
+
+
+class _Down2ThenDimRes(EngineModule):
+    """A two-BatchNorm tail (BottleneckDown2: act(BN(y) + BN2(r))) read by a stacked sibling
+    pair (BottleneckDim_Res's convs.0 + resconv) — no such edge exists in Segment(20)."""
+
+    def __init__(self):
+        super().__init__()
+        self.down = BottleneckDown2(16, 8, 32)
+        self.dimres = BottleneckDim_Res(32, 8, 48, True)
+
+    def emit(self, g, x):
+        y, _ = self.down.emit(g, x)
+        return self.dimres.emit(g, y)
+
+
+def _stacked_plan(m):
+    from instancesegmentation_amd.engine import param_layout
+    from instancesegmentation_amd.train import flatten_module
+    lay = param_layout(m)
+    flatten_module(m, "cpu", order=lay)
+    return Plan(m, [(2, 16, 32, 32)], True, True, (False,), layout=lay)
+
+
+def test_two_bn_tail_before_a_stacked_pair_stays_a_launch():
+    """engine._fold_tails (cb9f310): a two-BatchNorm tail whose reader is a
+    stacked pair is NOT folded (the residual's own BatchNorm rides on one sink in pw_gemm),
+    so it keeps its own tail launch in both directions; the pair itself still stacks."""
+    from instancesegmentation_amd.engine import ConvPairOp
+    m = _Down2ThenDimRes()
+    p = _stacked_plan(m)
+    ops = p.graph.ops
+    pair = [c for c in ops if isinstance(c, ConvPairOp)]
+    assert len(pair) == 1 and pair[0].res_in is None
+    assert not any(getattr(t, "fwd_folded", False) or getattr(t, "bwd_folded", False) for t in ops)
+    # (out0: the output materialised into its slot)
+    assert [r.label for r in p.fwd.recs if r.kind == L.OP_TAIL_FWD] == ["down", "dimres", "out0"]
+    assert sorted(r.label for r in p.bwd.recs if r.kind == L.OP_TAIL_BWD) == ["d_dimres", "d_down", "d_out0"]
+
+
+def test_stacked_pair_plan_rebuilt_when_weights_are_rebound_apart():
+    """Plan.stacking_holds: a plan that runs a sibling pair as ONE stacked GEMM
+    reads b's rows through a's pointer; once the weights stop being adjacent (here b's
+    weight rebound to a copy of its own) the cached plan is no longer valid."""
+    from instancesegmentation_amd.runtime import module_tensors
+    m = _Down2ThenDimRes()
+    p = _stacked_plan(m)
+    assert len(p.graph.stacked) == 1
+    assert p.stacking_holds(module_tensors(m))
+    rc = m.dimres.resconv[0].conv
+    rc.weight.data = rc.weight.detach().clone()
+    assert not p.stacking_holds(module_tensors(m))
+    q = Plan(m, [(2, 16, 32, 32)], True, True, (False,))  # layout order: no stacking at all
+    assert q.graph.stacked == [] and q.stacking_holds(module_tensors(m))
 
 
 def test_depthwise_backward_is_one_main_stream_op(monkeypatch):
