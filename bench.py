@@ -141,6 +141,41 @@ def pmc_traffic(label, args):
     return None
 
 
+# the stem's two 5x5 s2 convs (init_head_s4, segment.py:19-31): layer 2 (16 -> 16) in all
+# three directions, layer 1's RGB part forward and weight gradient
+BACKBONE_OPS = [("fwd", "init_conv.layer2"), ("bwd", "dx_init_conv.layer2"),
+                ("bwd", "dw_init_conv.layer2"), ("fwd", "init_conv.layer1"),
+                ("bwd", "dw_init_conv.layer1")]
+
+
+def stamp_op(trainer, phase, label, args):
+    """The roofline of one recorded op timed in place: the step re-captured with OP_STAMP
+    records around it (Trainer.stamp_at), args.steps replays after 2 warm-up replays. A
+    side-stream op (a weight gradient) is moved onto the main stream for its bracket."""
+    ol = trainer.plan.fwd if phase == "fwd" else trainer.plan.bwd
+    idx = next((i for i, r in enumerate(ol.recs) if r.label == label), None)
+    if idx is None:
+        return None
+    rec = ol.recs[idx]
+    trainer.stamp_at = (phase, idx)
+    trainer.capture()
+    for _ in range(2):
+        trainer.step(loss=False)
+    torch.cuda.synchronize()
+    trainer.stamp_reset()
+    for _ in range(args.steps):
+        trainer.step(loss=False)
+    torch.cuda.synchronize()
+    raw, brk, _ = trainer.stamp_times(args.steps)
+    ms = max(raw - brk, 1e-6)
+    r = roofline_of(rec, ms)
+    r["kernel"] = f"{phase}:{label}"
+    r["avg_ms"] = round(ms, 4)
+    r["gflop"] = round(rec.flops / 1e9, 4)
+    r["traffic"] = pmc_traffic(label, args)
+    return r
+
+
 def infer_scene(H, W, persons, dups, seed=11):
     """A crowded synthetic image (BASELINE config 4, OCHuman-style): `persons` overlapping
     person boxes with 17 keypoints each, plus `dups` repeated detections of the same people
@@ -252,6 +287,19 @@ def infer_bench(dev, reps=20):
             "dtype": "f32", "data": "synthetic"}
 
 
+def cpu_model():
+    """The host CPU's model name (/proc/cpuinfo), for the cpu_baseline record."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
 def cpu_baseline(args):
     """Oracle (torch eager fp32 CPU) train step on the same config: bounded sample."""
     import numpy as np
@@ -280,7 +328,7 @@ def cpu_baseline(args):
         t_total += time.perf_counter() - t0
         steps += 1
     return {"value": round(steps * args.batch / t_total, 3), "unit": "images/s",
-            "cores": threads, "kind": "port",
+            "cores": threads, "cpu_model": cpu_model(), "kind": "port",
             "sample": f"{steps} fp32 train steps (fwd+bwd) of Segment({args.cin}) at "
                       f"bs{args.batch} {args.size}x{args.size} on {threads} host threads"}
 
@@ -371,6 +419,11 @@ def train_leg(args, dev, world, rank, keypoints, roofline, dp_plan=None):
         roof["traffic"] = pmc_traffic(dom_rec.label, args)
     res = {"value": world * args.batch * args.steps / elapsed,
            "ms_per_step": 1e3 * elapsed / args.steps, "loss": trainer.loss(), "roofline": roof}
+    if roofline and not args.eager:
+        # north_star's target op: the backbone (stem) convs, each stamped in place the same
+        # way in a re-captured step after the timed region (segment.py:19-31)
+        res["roofline_backbone"] = [r for r in (stamp_op(trainer, ph, lab, args)
+                                                for ph, lab in BACKBONE_OPS) if r is not None]
     del trainer
     torch.cuda.synchronize()
     return res
@@ -387,9 +440,22 @@ def main():
     dense_leg = None
     if kp and not args.no_dense_leg:
         dense_leg = train_leg(args, dev, world, rank, False, False)
-    dp_leg = None
+    dp_leg = dp_nccl_leg = None
     if world == 1 and not args.no_dp_leg:
         dp_leg = train_leg(args, dev, world, rank, kp, False, dp_plan=True)
+        # the same structure with REAL one-rank RCCL all-reduces (a world-size-1 "nccl"
+        # group): what the exchange code path itself costs on one GPU
+        import socket
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0,
+                                world_size=1, device_id=dev)
+        try:
+            dp_nccl_leg = train_leg(args, dev, world, rank, kp, False, dp_plan=True)
+        finally:
+            dist.destroy_process_group()
 
     value = main_leg["value"]
     out = {
@@ -409,6 +475,16 @@ def main():
                    "execution": "eager" if args.eager else "hip-graph"},
         "roofline": main_leg["roofline"], "loss": round(main_leg["loss"], 6),
     }
+    if main_leg.get("roofline_backbone"):
+        bb = main_leg["roofline_backbone"]
+        # north_star's metric: fraction of the fp32 MFMA roofline on the backbone conv (the
+        # stem's 5x5 s2 convs), each op stamped in place; aggregate = their flops / time
+        tot_f = sum(r["gflop"] for r in bb)
+        tot_ms = sum(r["avg_ms"] for r in bb)
+        out["roofline_backbone"] = {
+            "ops": bb, "aggregate_frac": round(tot_f * 1e9 / (tot_ms * 1e-3) / 1e12 /
+                                               PEAK_F32_MFMA_TFLOPS, 4),
+            "unit": "fraction of the fp32 MFMA peak (157.3 TFLOP/s)"}
     if dense_leg is not None:
         out["dense_heatmaps"] = {"value": round(dense_leg["value"], 3),
                                  "ms_per_step": round(dense_leg["ms_per_step"], 3),
@@ -421,6 +497,13 @@ def main():
             "what": "the step as it runs at world > 1 (two backward parts, two gradient buckets, "
                     "three HIP graphs with the RCCL exchange points between them), at world 1 "
                     "where the exchanges are no-ops: the per-GPU ceiling of weak scaling"}
+    if dp_nccl_leg is not None:
+        out["dp_plan_at_world1_nccl"] = {
+            "value": round(dp_nccl_leg["value"], 3),
+            "ms_per_step": round(dp_nccl_leg["ms_per_step"], 3),
+            "what": "the same data-parallel step with a world-size-1 RCCL process group: the "
+                    "two bucket all-reduces are real one-rank RCCL collectives (bucket 1 "
+                    "asynchronous under the stem backward, bucket 2, the wait)"}
     if rank == 0 and world == 1 and not args.no_infer:
         out["infer"] = infer_bench(dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

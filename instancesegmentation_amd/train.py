@@ -48,15 +48,20 @@ class GradSync:
     current stream wait for them; on gloo (CPU tests) they complete on the host. BN batch
     statistics stay local to each replica, as in the reference run per replica."""
 
-    def __init__(self, process_group=None):
+    def __init__(self, process_group=None, force=False):
+        """force: issue the collectives even at world size 1 when a process group exists
+        (a one-rank RCCL communicator: the real exchange code path — communicator, RCCL's
+        stream ordering, the asynchronous bucket-1 handle — on one GPU, where the SUM is the
+        identity)."""
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(process_group) if dist.is_initialized() else 0
+        self.active = self.world > 1 or (bool(force) and dist.is_initialized())
         self._pending = []
 
     def begin(self, bucket):
         """Launch the SUM all-reduce of `bucket` (a view of comm) asynchronously."""
-        if self.world > 1 and bucket.numel():
+        if self.active and bucket.numel():
             self._pending.append(dist.all_reduce(bucket, op=dist.ReduceOp.SUM, group=self.pg,
                                                  async_op=True))
 
@@ -128,14 +133,16 @@ class Trainer:
                  eps=1e-8, weight_decay=0.0, process_group=None, dp_plan=None):
         """dp_plan: build the data-parallel step structure (two backward parts, two gradient
         buckets, three HIP graphs with the exchange markers between them) even at world
-        size 1, where the exchanges are no-ops — what that structure costs on one GPU
-        (bench.py's dp_plan leg). Default: only at world size > 1."""
+        size 1 — what that structure costs on one GPU (bench.py's dp_plan legs). Without a
+        process group its exchanges are no-ops; with one (a world-size-1 "nccl" group) they
+        are real one-rank RCCL all-reduces. Default: only at world size > 1."""
         self.device = torch.device(device or "cuda")
         dev = self.device
         self.model = model.to(dev).train()
-        self.sync = GradSync(process_group)
+        world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        self.dp_plan = world > 1 if dp_plan is None else bool(dp_plan)
+        self.sync = GradSync(process_group, force=self.dp_plan)
         self.world, self.rank = self.sync.world, self.sync.rank
-        self.dp_plan = self.world > 1 if dp_plan is None else bool(dp_plan)
         n = sum(p.numel() for p in self.model.parameters())
         nb = _float_buffer_count(self.model)
         self.comm = torch.zeros(n + max(nb, 1), dtype=torch.float32, device=dev)

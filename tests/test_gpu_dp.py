@@ -141,3 +141,65 @@ def test_train_loop_fit_two_ranks(tmp_path):
     assert h0 == h1 and len(h0) >= 1
     assert s0 == s1 == 3
     assert d0 == 0.0 and d1 == 0.0
+
+
+def _nccl_world1_worker(rank, port, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    from instancesegmentation_amd.data import device_batch
+    from instancesegmentation_amd.model.segment import Segment
+    from instancesegmentation_amd.train import Trainer
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    n, h, w = 2, 256, 256
+    torch.manual_seed(91)
+    init = Segment(20).state_dict()
+    xs, mask = device_batch(n, h, w, dev, seed=400, keypoints=True)
+    shapes = [tuple(t.shape) for t in xs]
+
+    def run(tr, steps=2):
+        res = []
+        for _ in range(steps):
+            tr.step(xs, mask)
+            torch.cuda.synchronize()
+            res.append((tr.grad_flat.clone(), tr.flat.clone(), tr.flatb.clone(), tr.loss()))
+        return res
+
+    # the world-1 default plan (one graph, no exchange) first, without any process group
+    m0 = Segment(20)
+    m0.load_state_dict(init)
+    ref = run(Trainer(m0, n, shapes, device=dev).capture())
+    dist.init_process_group("nccl", rank=rank, world_size=1, device_id=dev)
+    try:
+        assert dist.get_backend() == "nccl"
+        m1 = Segment(20)
+        m1.load_state_dict(init)
+        tr = Trainer(m1, n, shapes, device=dev, dp_plan=True).capture()
+        assert tr.world == 1 and tr.sync.active and len(tr.graphs) >= 3
+        assert "coll1" in tr.graphs and "coll2" in tr.graphs
+        got = run(tr)
+        diffs = []
+        for (g0, p0, b0, l0), (g1, p1, b1, l1) in zip(ref, got):
+            diffs.append((int((g0 != g1).sum()), int((p0 != p1).sum()), int((b0 != b1).sum()),
+                          abs(l0 - l1)))
+        out[rank] = diffs
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_plan_over_rccl_at_world1_matches_default_plan():
+    """RCCL (the "nccl" backend) on the one leased GPU: a world-size-1
+    nccl process group in a fresh process drives the data-parallel step structure with REAL
+    one-rank RCCL all-reduces — the three captured graphs, bucket 1 launched asynchronously
+    on RCCL's stream while backward part 2 (the stem) runs, bucket 2, the wait, the running
+    statistics in the exchange buffer — and two steps of it equal the world-1 default plan
+    (one graph, no exchange) bit for bit: gradient, parameters after Adam, running
+    statistics (a one-rank SUM is the identity; the backward is deterministic)."""
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_nccl_world1_worker, args=(_free_port(), out), nprocs=1, join=True)
+    for step, (dg, dp, db, dl) in enumerate(out[0], 1):
+        print(f"step {step}: elements differing (grad, params, running stats) {dg}, {dp}, {db}; "
+              f"loss diff {dl:.2e}")
+        assert (dg, dp, db) == (0, 0, 0)
+        assert dl <= 1e-12

@@ -1,7 +1,11 @@
-"""Host enqueue time of the captured train step against its GPU time: if graph replay
-takes about as long on the host as the step takes on the GPU, the launch is host-paced.
+"""Host enqueue time of the train step against its GPU time: if issuing a step takes
+about as long on the host as the step takes on the GPU, the launch is host-paced.
 
-    python tools/replay_host.py [--steps 20]
+    python tools/replay_host.py [--steps 20] [--eager]
+
+Default: HIP-graph replay of the captured step. --eager: the step issued by the C++
+executor (isg_exec_ms2: one host call per op list, one hipLaunchKernel per record) with no
+graph — the other host floor.
 """
 import argparse
 import os
@@ -19,6 +23,7 @@ from instancesegmentation_amd.train import Trainer  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--eager", action="store_true", help="no graph: the C++ executor per step")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.manual_seed(1234)
@@ -26,7 +31,8 @@ def main():
     xs, mask = device_batch(2, 1024, 1024, dev, seed=100, cin=20, keypoints=True)
     tr = Trainer(model, 2, [tuple(x.shape) for x in xs], device=dev)
     tr.step(xs, mask)
-    tr.capture()
+    if not a.eager:
+        tr.capture()
     for _ in range(5):
         tr.step()
     torch.cuda.synchronize()
@@ -42,7 +48,9 @@ def main():
     t2 = time.perf_counter()
     print(f"host per step {1e3 * sum(host) / len(host):.3f} ms (max {1e3 * max(host):.3f}); "
           f"wall per step {1e3 * (t2 - t0) / a.steps:.3f} ms; GPU drain after the last "
-          f"replay {1e3 * (t2 - t1):.3f} ms; graphs {len(tr.graphs)}")
+          f"replay {1e3 * (t2 - t1):.3f} ms; mode {'eager executor' if a.eager else 'graph replay'}; "
+          f"graphs {len(tr.graphs) if tr.graphs else 0}; records per step "
+          f"{len(tr.plan.fwd.recs) + len(tr.plan.bwd.recs)}")
     # GPU idle test: one step after the GPU has gone idle, with the host far ahead
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
