@@ -29,3 +29,10 @@ def pytest_terminal_summary(terminalreporter):
     for tag, err, bar, d32, floor in LOGITS_MARGINS:
         tr.write_line(f"  {tag:40s} err {err:.3e} bar {bar:.3e} err/bar {err / bar:.2f}  "
                       f"vs CPU-fp32 {d32:.3e}  CPU-fp32 floor {floor:.3e}")
+    from tests.grad_check import WELL_CONDITIONED
+    over = [m for m in LOGITS_MARGINS if m[3] > 1e-4]
+    wc = [m for m in LOGITS_MARGINS if m[4] <= WELL_CONDITIONED]
+    tr.write_line(f"logits checks: {len(LOGITS_MARGINS)}; more than 1e-4 from the CPU-fp32 "
+                  f"reference: {len(over)} ({', '.join(m[0] for m in over) or 'none'}); in the "
+                  f"well-conditioned regime (CPU-fp32 floor <= {WELL_CONDITIONED:g}): {len(wc)}, of "
+                  f"them above 1e-4: {sum(m[3] > 1e-4 for m in wc)}")

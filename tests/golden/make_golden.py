@@ -2,7 +2,8 @@
 
 Run in the build container only (it reads /root/reference, which does not exist
 on the GPU box):   PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
-(`--well-conditioned` writes only segment20_n2_128_wc.npz, added in round 4)
+(`--well-conditioned` writes only segment20_n2_128_wc.npz, added in round 4;
+`--strict-regime` writes only segment3_n2_64x96_wc.npz and kp20_n2_128_wc.npz, round 6)
 
 What it does:
   * imports /root/reference/model/segment.py with a `cv2` stub (the import is unused,
@@ -53,14 +54,15 @@ def set_params(model, pvals):
             v.copy_(torch.as_tensor(pvals[k]).to(v.dtype))
 
 
-def capture_train(Segment, cin, n, h, w, pseed, bseed, dtype, head_scale=1.0):
+def capture_train(Segment, cin, n, h, w, pseed, bseed, dtype, head_scale=1.0, batch=None):
+    """batch: (x, mask) to use instead of the seeded synth_batch (the keypoint fixture)."""
     torch.manual_seed(0)
     m = Segment(cin)
     shapes = [(k, tuple(v.shape)) for k, v in m.state_dict().items()]
     pv = synth_params(shapes, pseed, head_scale)
     m = m.to(dtype)
     set_params(m, pv)
-    x, mask = synth_batch(n, cin, h, w, bseed)
+    x, mask = synth_batch(n, cin, h, w, bseed) if batch is None else batch
     xt = torch.from_numpy(x).to(dtype)
     yt = torch.from_numpy(mask).to(dtype)
     cap = {}
@@ -94,9 +96,9 @@ def capture_train(Segment, cin, n, h, w, pseed, bseed, dtype, head_scale=1.0):
 
 
 def make_segment_fixture(Segment, cin, n, h, w, pseed, bseed, path, head_scale=1.0,
-                         logits_dtype=np.float32):
-    r64 = capture_train(Segment, cin, n, h, w, pseed, bseed, torch.float64, head_scale)
-    r32 = capture_train(Segment, cin, n, h, w, pseed, bseed, torch.float32, head_scale)
+                         logits_dtype=np.float32, batch=None, extra=None):
+    r64 = capture_train(Segment, cin, n, h, w, pseed, bseed, torch.float64, head_scale, batch)
+    r32 = capture_train(Segment, cin, n, h, w, pseed, bseed, torch.float32, head_scale, batch)
     buf_keys = list(r64["bufs"].keys())
     out = dict(
         meta=np.array(json.dumps(dict(cin=cin, n=n, h=h, w=w, param_seed=pseed,
@@ -115,6 +117,7 @@ def make_segment_fixture(Segment, cin, n, h, w, pseed, bseed, path, head_scale=1
                                for k in buf_keys]).astype(np.float64),
         eval_logits64=r64["eval_logits"].numpy().astype(logits_dtype),
     )
+    out.update(extra or {})
     np.savez_compressed(path, **out)
     return r32
 
@@ -157,6 +160,64 @@ def make_bce_fixture(path):
     loss.backward()
     np.savez_compressed(path, logits=lg, target=tg, loss=np.float32(loss.item()),
                         dlogits=lt.grad.numpy(), prob=p.detach().numpy())
+
+
+def reference_keypoint2heatmaps():
+    """The reference's keypoint2heatmaps (train_instance.py:33-68) and its part order,
+    extracted with `ast` (the module's other imports — ymlib, imgaug, cv2 — are absent)."""
+    src = open(os.path.join(REF, "train_instance.py")).read()
+    tree = ast.parse(src)
+    keep = [nd for nd in tree.body
+            if (isinstance(nd, ast.FunctionDef) and nd.name == "keypoint2heatmaps")
+            or (isinstance(nd, ast.Assign) and any(getattr(t, "id", "") == "ORDER_PART_NAMES"
+                                                    for t in nd.targets))]
+    ns = {"np": np, "math": __import__("math"), "key_combine": lambda a, b: a}
+    exec(compile(ast.Module(body=keep, type_ignores=[]), "train_instance.py", "exec"), ns)
+    return ns["keypoint2heatmaps"], ns["ORDER_PART_NAMES"]
+
+
+def fixture_keypoints(seed, n, h, w, margin=30):
+    """Seeded keypoints [n, 17, (x, y, visible)] placed so windows straddle the stem's
+    16x16 output tiles and the image border (partly and almost wholly outside), with
+    invisible parts — the same construction as tests/test_gpu_kp_stem._keypoints."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    kp = np.zeros((n, 17, 3), np.float64)
+    kp[..., 0] = rng.uniform(-margin, w + margin, (n, 17))
+    kp[..., 1] = rng.uniform(-margin, h + margin, (n, 17))
+    kp[..., 2] = (rng.uniform(size=(n, 17)) < 0.8).astype(np.float64)
+    kp[0, 0] = (w - 1.5, 7.25, 1.0)
+    kp[0, 1] = (16.0 * 3, 16.0 * 2, 1.0)
+    kp[-1, 2] = (-25.0, h / 2, 1.0)
+    return kp
+
+
+def make_kp_fixture(Segment, path, n=2, h=128, w=128, pseed=1234, bseed=99, kseed=17):
+    """The keypoint path in the well-conditioned regime: the image and mask of
+    synth_batch(cin=3), 17 heatmaps per image made by the REFERENCE's keypoint2heatmaps from
+    seeded keypoints (stored in the fixture as `keypoints`), then the reference Segment(20)
+    train step on cat(image, heatmaps) with the last conv's weight x0.35."""
+    k2h, parts = reference_keypoint2heatmaps()
+    img, mask = synth_batch(n, 3, h, w, bseed)
+    kp = fixture_keypoints(kseed, n, h, w)
+    maps = np.zeros((n, 17, h, w), np.float32)
+    for b in range(n):
+        pts = {parts[j]: {"status": "vis" if kp[b, j, 2] > 0 else "occ",
+                          "point": (float(kp[b, j, 0]), float(kp[b, j, 1]))} for j in range(17)}
+        maps[b] = np.stack(k2h(pts, (h, w))).astype(np.float32)
+    x = np.concatenate([img, maps], 1)
+    make_segment_fixture(Segment, 20, n, h, w, pseed, bseed, path, head_scale=0.35,
+                         logits_dtype=np.float64, batch=(x, mask),
+                         extra={"keypoints": kp, "heatmap_nonzero": np.int64((maps > 0).sum())})
+
+
+def make_strict_regime(Segment):
+    """Round 6: Segment(3) and the keypoint path in the regime where
+    the CPU-fp32 reference is within 5e-5 of fp64, so the GPU-vs-CPU-fp32 1e-4 bar is
+    asserted directly."""
+    make_segment_fixture(Segment, 3, 2, 64, 96, 4321, 77,
+                         os.path.join(HERE, "segment3_n2_64x96_wc.npz"), head_scale=0.35,
+                         logits_dtype=np.float64)
+    make_kp_fixture(Segment, os.path.join(HERE, "kp20_n2_128_wc.npz"))
 
 
 def make_heatmap_fixture(path):
@@ -212,6 +273,10 @@ def main():
         make_well_conditioned(Segment)
         print("well-conditioned fixture written to", HERE)
         return
+    if "--strict-regime" in sys.argv:  # added in round 6; leaves the others untouched
+        make_strict_regime(Segment)
+        print("strict-regime fixtures written to", HERE)
+        return
     r32 = make_segment_fixture(Segment, 20, 2, 128, 128, 1234, 99,
                                os.path.join(HERE, "segment20_n2_128.npz"))
     make_adam_fixture(r32, os.path.join(HERE, "adam_segment20.npz"))
@@ -220,6 +285,7 @@ def main():
     make_bce_fixture(os.path.join(HERE, "bce.npz"))
     make_heatmap_fixture(os.path.join(HERE, "heatmaps.npz"))
     make_well_conditioned(Segment)
+    make_strict_regime(Segment)
     print("golden fixtures written to", HERE)
 
 

@@ -736,6 +736,8 @@ def test_depthwise_bwd_fused(cfg, ynull):
     for u, v, what in zip(a, b, ("dx", "BN-backward sums", "slope gradient", "dW replicas")):
         assert not torch.isnan(u).any(), what
         assert torch.equal(u, v), f"fused {what} differs from the separate calls"
+    if ynull:  # y = g: the BatchNorm backward of g w.r.t. itself is 0 up to rounding noise,
+        return  # so only the bitwise agreement with the spelled-out y is meaningful
     OUT = torch.full((stride_,), float("nan"), device=DEV)
     call("isg_sum_replicas", ptr(OUT), ptr(a[3]), stride_, L.WREP, stride_, stream())
     wref = torch.nn.grad.conv2d_weight(xt, (C, 1, kh, kw), dy, padding=(ph, pw), dilation=d,

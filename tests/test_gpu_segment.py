@@ -30,7 +30,9 @@ def run_step(m, fx):
     x = torch.from_numpy(fx.x).to(DEV)
     y = torch.from_numpy(fx.mask).to(DEV)
     m.train()
-    if fx.cin == 20:
+    if fx.keypoints is not None:  # the keypoint path: heatmaps synthesised in the stem
+        logits = m(x[:, :3].contiguous(), torch.from_numpy(fx.keypoints).to(DEV))
+    elif fx.cin == 20:
         logits = m(x[:, :3].contiguous(), x[:, 3:].contiguous())
     else:
         logits = m(x)
@@ -77,7 +79,10 @@ def test_segment_eval_matches_reference(name):
     m.eval()
     x = torch.from_numpy(fx.x).to(DEV)
     with torch.no_grad():
-        logits = m(x)
+        if fx.keypoints is not None:
+            logits = m(x[:, :3].contiguous(), torch.from_numpy(fx.keypoints).to(DEV))
+        else:
+            logits = m(x)
     ref = torch.from_numpy(fx.z["eval_logits64"])
     err = (logits.cpu() - ref).abs().max().item()
     scale = max(1.0, ref.abs().max().item())
