@@ -51,6 +51,19 @@ def main():
           f"replay {1e3 * (t2 - t1):.3f} ms; mode {'eager executor' if a.eager else 'graph replay'}; "
           f"graphs {len(tr.graphs) if tr.graphs else 0}; records per step "
           f"{len(tr.plan.fwd.recs) + len(tr.plan.bwd.recs)}")
+    # the host cost itself: steps issued into an IDLE GPU queue (right after a sync) cannot
+    # be held back by queue back-pressure, unlike the pipelined loop above, whose host time
+    # per step converges to the GPU's step time once the host runs ~4 steps ahead
+    cold = []
+    for _ in range(10):
+        torch.cuda.synchronize()
+        h0 = time.perf_counter()
+        tr.step()
+        cold.append(time.perf_counter() - h0)
+    torch.cuda.synchronize()
+    cold.sort()
+    print(f"host cost of one step issued into an idle queue: median {1e3 * cold[5]:.3f} ms "
+          f"(min {1e3 * cold[0]:.3f}, max {1e3 * cold[-1]:.3f})")
     # GPU idle test: one step after the GPU has gone idle, with the host far ahead
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
