@@ -428,7 +428,11 @@ int32_t isg_exec_ms2(const void* ops, int32_t nops, void* const* table, isg_stre
     bool forked = false, forked2 = false;  // side-stream work outstanding since the last join
     // weight gradients deferred per fork: 48 with two side streams and one backward
     // part (4.415 -> 4.365 ms/step against 24; 36: 4.405, 64: 4.42, 96: 4.48 — r03y)
-    constexpr int batch = 48;
+    static const int batch = [] {  // (ISG_SIDE_BATCH: round-6 measurement knob)
+        const char* e = getenv("ISG_SIDE_BATCH");
+        const int b = e ? atoi(e) : 48;
+        return b < 1 ? 1 : b;
+    }();
     // grouped 1x1 weight gradients in weight-gradient batches (4.04 -> 3.96
     // ms/step, 2 interleaved 200-step pairs)
     constexpr bool pwg_group_on = true;
