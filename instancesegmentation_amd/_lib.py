@@ -224,6 +224,7 @@ SIGNATURES = {
     "isg_exec": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p]),
     "isg_exec_ms": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p]),
     "isg_exec_ms2": (c_int32, [c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "isg_side_stream_create": (c_int32, [c_int32, c_void_p]),
     "isg_last_error": (c_char_p, []),
     "isg_abi_version": (c_int32, []),
     "isg_stat_replicas": (c_int32, []),
@@ -273,13 +274,28 @@ def stream_ptr(device=None):
 _SIDE = {}
 
 
+def _side_keep():
+    """CUs of every 8 the side streams may occupy (isg_side_stream_create); 8 = all."""
+    return int(os.environ.get("ISG_SIDE_CU", "8"))
+
+
+def _new_side_stream(d):
+    keep = _side_keep()
+    if keep >= 8:
+        return torch.cuda.Stream(device=d)
+    with torch.cuda.device(d):
+        h = ctypes.c_void_p()
+        check(lib().isg_side_stream_create(keep, ctypes.byref(h)), "side stream")
+        return torch.cuda.ExternalStream(h.value, device=torch.device("cuda", d))
+
+
 def side_stream_ptr(device=None):
     """The executor's side stream of `device` (weight gradients fork onto it)."""
     d = torch.cuda.current_device() if device is None else torch.device(device).index
     if d is None:
         d = torch.cuda.current_device()
     if d not in _SIDE:
-        _SIDE[d] = torch.cuda.Stream(device=d)
+        _SIDE[d] = _new_side_stream(d)
     return _SIDE[d].cuda_stream
 
 
@@ -295,5 +311,5 @@ def side_stream2_ptr(device=None):
     if d is None:
         d = torch.cuda.current_device()
     if d not in _SIDE2:
-        _SIDE2[d] = torch.cuda.Stream(device=d)
+        _SIDE2[d] = _new_side_stream(d)
     return _SIDE2[d].cuda_stream

@@ -598,6 +598,22 @@ int32_t isg_exec(const void* ops, int32_t nops, void* const* table, isg_stream_t
     return isg_exec_ms2(ops, nops, table, st, nullptr, nullptr);
 }
 
+int32_t isg_side_stream_create(int32_t keep, isg_stream_t* out) {
+    if (!out || keep < 1 || keep > 8) return isg_set_error(ISG_ERR_INVALID, "side stream: keep %d of 8", keep);
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+        return isg_check_launch("side stream: CU count");
+    std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0u);
+    for (int i = 0; i < cus; ++i)
+        if (i % 8 < keep) mask[(size_t)i / 32] |= 1u << (i % 32);
+    hipStream_t s = nullptr;
+    if (hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()) != hipSuccess)
+        return isg_check_launch("side stream: hipExtStreamCreateWithCUMask");
+    *out = s;
+    return ISG_OK;
+}
+
 // sizes of the executor records, so the Python planner can verify its ctypes mirrors
 int32_t isg_record_size(int32_t which) {
     switch (which) {
