@@ -282,24 +282,30 @@ struct OpHdr {
     int32_t kind, desc_bytes, nfix, flags;  // flags: ISG_OPF_SIDE | ISG_OPF_JOIN
 };
 enum { ISG_OPF_SIDE = 1, ISG_OPF_JOIN = 2, ISG_OPF_FORK_NOW = 4 };  // FORK_NOW: no batching
+// flags >> 8 of a JOIN: how many of the most recent side records (in list order) the op does
+// NOT depend on — it waits only for the side work up to the one before them (engine.py
+// _join_exclusions); 0 = wait for all side work
+constexpr int kJoinExclShift = 8;
 
 // fork / join events of the executor's side streams, per device (created on first use,
 // never destroyed; timing disabled): ev[0] fork, ev[1] join of side stream 0, ev[2] join
 // of side stream 1
 constexpr int kForkPool = 16;  // fork events of side-stream batches, used round robin
-static int32_t side_events(hipEvent_t* join, hipEvent_t* join2, hipEvent_t** forks) {
-    static hipEvent_t ev[64][2 + kForkPool];
+constexpr int kDonePool = 64;  // batch-completion events (partial joins), round robin
+static int32_t side_events(hipEvent_t* join, hipEvent_t* join2, hipEvent_t** forks, hipEvent_t** done) {
+    static hipEvent_t ev[64][2 + kForkPool + 2 * kDonePool];
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64)
         return isg_set_error(ISG_ERR_HIP, "exec: no device for the side stream");
     if (!ev[dev][0]) {
-        for (int i = 0; i < 2 + kForkPool; ++i)
+        for (int i = 0; i < 2 + kForkPool + 2 * kDonePool; ++i)
             if (hipEventCreateWithFlags(&ev[dev][i], hipEventDisableTiming) != hipSuccess)
                 return isg_check_launch("exec: side-stream events");
     }
     *join = ev[dev][0];
     *join2 = ev[dev][1];
     *forks = &ev[dev][2];
+    *done = &ev[dev][2 + kForkPool];
     return ISG_OK;
 }
 struct Fix {
@@ -424,7 +430,7 @@ int32_t isg_exec_ms2(const void* ops, int32_t nops, void* const* table, isg_stre
                      isg_stream_t side, isg_stream_t side2) {
     const char* p = (const char*)ops;
     alignas(16) char buf[8192];
-    hipEvent_t ev_join = nullptr, ev_join2 = nullptr, *ev_forks = nullptr;
+    hipEvent_t ev_join = nullptr, ev_join2 = nullptr, *ev_forks = nullptr, *ev_done = nullptr;
     bool forked = false, forked2 = false;  // side-stream work outstanding since the last join
     // weight gradients deferred per fork: 48 with two side streams and one backward
     // part (4.415 -> 4.365 ms/step against 24; 36: 4.405, 64: 4.42, 96: 4.48 — r03y)
@@ -442,6 +448,16 @@ int32_t isg_exec_ms2(const void* ops, int32_t nops, void* const* table, isg_stre
     };
     std::vector<std::pair<int32_t, std::string>> pending;
     int pool_next = 0;
+    // partial joins: for every issued batch, the side-record count after it and the events
+    // recorded behind it on the side stream(s) it used
+    struct Done {
+        int upto;
+        hipEvent_t e1, e2;
+    };
+    std::vector<Done> done_list;
+    int done_next = 0;
+    int nside = 0;  // side records seen so far (list order)
+    int issued = 0;  // side records issued so far
     int deal = 0;  // weight gradients alternate between the side streams across batches too
     bool side_serial = false;  // a side-only batch ran on `side` since side 2 last waited for it
     auto launch = [&](Batch& bt) -> int32_t {
@@ -526,7 +542,32 @@ int32_t isg_exec_ms2(const void* ops, int32_t nops, void* const* table, isg_stre
         bt.ops.swap(pending);
         bt.ev = ev_forks[pool_next++ % kForkPool];
         if (hipEventRecord(bt.ev, main_st) != hipSuccess) return isg_check_launch("exec: fork point");
-        return launch(bt);
+        if (int32_t e = launch(bt)) return e;
+        issued += (int)bt.ops.size();
+        // its completion on the side stream(s) holding outstanding work, for a later partial
+        // join (side 2 behind this batch covers it too when the batch did not use side 2)
+        Done d{issued, ev_done[2 * (done_next % kDonePool)], nullptr};
+        if (hipEventRecord(d.e1, side) != hipSuccess) return isg_check_launch("exec: batch done");
+        if (forked2) {
+            d.e2 = ev_done[2 * (done_next % kDonePool) + 1];
+            if (hipEventRecord(d.e2, side2) != hipSuccess) return isg_check_launch("exec: batch done 2");
+        }
+        ++done_next;
+        done_list.push_back(d);
+        return ISG_OK;
+    };
+    // wait for the side work up to side record `upto` (exclusive count) only
+    auto join_upto = [&](int upto) -> int32_t {
+        if (upto > issued)
+            if (int32_t e = close_batch()) return e;
+        for (const Done& d : done_list) {
+            if (d.upto < upto) continue;
+            if (hipStreamWaitEvent(main_st, d.e1, 0) != hipSuccess ||
+                (d.e2 && hipStreamWaitEvent(main_st, d.e2, 0) != hipSuccess))
+                return isg_check_launch("exec: partial join");
+            return ISG_OK;
+        }
+        return ISG_OK;  // (nothing issued up to there: no side work to wait for)
     };
     auto join = [&]() -> int32_t {
         if (int32_t e = close_batch()) return e;
@@ -548,14 +589,20 @@ int32_t isg_exec_ms2(const void* ops, int32_t nops, void* const* table, isg_stre
         std::memcpy(&h, p, sizeof(h));
         isg_stream_t st = main_st;
         if ((h.flags & ISG_OPF_JOIN) && side) {
-            if (int32_t e = join()) return e;
+            const int excl = h.flags >> kJoinExclShift;
+            if (excl > 0 && excl <= nside) {
+                if (int32_t e = join_upto(nside - excl)) return e;
+            } else if (int32_t e = join()) {
+                return e;
+            }
         }
         if ((h.flags & ISG_OPF_SIDE) && side) {
             // the op depends on everything issued so far on the main stream
             if (!ev_join) {
-                if (int32_t e = side_events(&ev_join, &ev_join2, &ev_forks)) return e;
+                if (int32_t e = side_events(&ev_join, &ev_join2, &ev_forks, &ev_done)) return e;
             }
             st = side;
+            ++nside;
         }
         p += sizeof(h);
         if (h.desc_bytes < 0 || h.desc_bytes > (int)sizeof(buf))

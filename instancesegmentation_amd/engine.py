@@ -84,6 +84,8 @@ def _fill(obj, spec, base, fix):
 
 class Record:
     OPF_SIDE, OPF_JOIN, OPF_FORK_NOW = 1, 2, 4  # executor header flags (api.cpp)
+    # a join's count of the most recent side records it does NOT wait for (_join_exclusions)
+    EXCL_SHIFT, EXCL_MAX = 8, (1 << 20) - 1
 
     def __init__(self, kind, cls, spec, items_cls=None, items=None, label="", flops=0, nbytes=0):
         self.kind = kind
@@ -156,11 +158,20 @@ class OpList:
         before = stamp(0, -1)
         # a join the op carries happens before its first stamp; a side-stream op (a weight
         # gradient) is timed on the main stream
-        before.flags = op.flags & Record.OPF_JOIN
-        op.flags &= ~(Record.OPF_JOIN | Record.OPF_SIDE | Record.OPF_FORK_NOW)
+        # (with its exclusion count: the stamp adds no side record)
+        before.flags = op.flags & (Record.OPF_JOIN | (Record.EXCL_MAX << Record.EXCL_SHIFT))
+        was_side = op.flags & Record.OPF_SIDE
+        op.flags = 0
         o = OpList()
         o.recs = [stamp(1, -1), stamp(1, 1)] + self.recs[:idx] + [before, op, stamp(0, 1)] + \
             self.recs[idx + 1:]
+        if was_side:  # one side record fewer: recount (a join on the moved op waits for all)
+            new = {id(r): copy.copy(r) for r in o.recs}
+            for r in new.values():
+                if getattr(r, "join_deps", None):
+                    r.join_deps = {id(new[d]) for d in r.join_deps if d in new}
+            o.recs = [new[id(r)] for r in o.recs]
+            _join_exclusions(o.recs)
         return o.compile()
 
 
@@ -618,6 +629,7 @@ def _fork_pools(ol):
                 if j > i + 1:  # something to overlap with
                     r.flags |= Record.OPF_SIDE | Record.OPF_FORK_NOW
                     recs[j].flags |= Record.OPF_JOIN
+                    _join_dep(recs[j], r)
                 break
 
 
@@ -642,7 +654,36 @@ def _fork_branches(ol, side_recs):
             if any(fs == slot and lo <= off < hi for _, fs, off in recs[j].fix
                    for slot, lo, hi in ranges):
                 recs[j].flags |= Record.OPF_JOIN
+                _join_dep(recs[j], r)
                 break
+
+
+def _join_dep(rec, side_rec):
+    """Remember which forked record a join waits for (_join_exclusions)."""
+    if not hasattr(rec, "join_deps"):
+        rec.join_deps = set()
+    rec.join_deps.add(id(side_rec))
+
+
+def _join_exclusions(recs):
+    """Narrow every join to the side work it depends on: a join made by _fork_pools /
+    _fork_branches waits only for the side records up to the LAST one it reads (in list
+    order), not for side records forked after that one — the executor's join would
+    otherwise cover the side stream's whole tail, e.g. bottle1_1's 2x2 conv waiting for its
+    own forked residual branch (pool + convm) when it only reads the stem's pools. The
+    count of excluded (later) side records goes into the header flags' upper bits
+    (api.cpp OPF_JOIN); joins without recorded dependencies wait for everything."""
+    order = []
+    for r in recs:
+        if r.flags & Record.OPF_JOIN:
+            r.flags &= (1 << Record.EXCL_SHIFT) - 1
+            deps = getattr(r, "join_deps", None)
+            pos = {i: k for k, i in enumerate(order)}
+            if deps and all(d in pos for d in deps):
+                excl = len(order) - 1 - max(pos[d] for d in deps)
+                r.flags |= min(excl, Record.EXCL_MAX) << Record.EXCL_SHIFT
+        if r.flags & Record.OPF_SIDE:
+            order.append(id(r))
 
 
 _FORK_DELAY = os.environ.get("ISG_FORK_DELAY", "1")  # 0 off, 1 the first fork group, 2 all
@@ -1446,6 +1487,7 @@ class Plan:
         _fork_pools(fw)
         _fork_branches(fw, side_recs)
         _delay_forks(fw)
+        _join_exclusions(fw.recs)
         self.fwd = fw.compile()
         self.act_size = g.act_size
         self.stats_size = max(g.stats_size, 8)
