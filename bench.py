@@ -354,7 +354,8 @@ def _train_leg(args, dev, world, rank, keypoints, roofline, dp_plan=None):
     xs, mask = device_batch(args.batch, args.size, args.size, dev, seed=100 + rank, cin=args.cin,
                             keypoints=keypoints and args.cin == 20)
     in_shapes = [tuple(x.shape) for x in xs]
-    trainer = Trainer(model, args.batch, in_shapes, device=dev, dp_plan=dp_plan)
+    trainer = Trainer(model, args.batch, in_shapes, device=dev, dp_plan=dp_plan,
+                      fused_tail=False if os.environ.get("ISG_NO_FUSED_TAIL") else None)
     trainer.step(xs, mask)
     torch.cuda.synchronize()
 

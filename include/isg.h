@@ -313,6 +313,36 @@ typedef struct {
 } isg_grad_final;
 int32_t isg_grad_finalize(const isg_grad_final* items, int32_t nitems, isg_stream_t stream);
 
+/* The end of a world-size-1 training step as ONE launch (train_instance.py:379-380:
+ * the gradient complete, then optimizer.step()): fold the weight-gradient replicas
+ * (isg_sum_replicas) into `grad` and apply Adam (isg_adam_dev's arithmetic, step already
+ * advanced by isg_step_inc) to every folded element; finalise the statistics-derived
+ * gradients of the `ngf` items (isg_grad_finalize) into `grad` and apply Adam to those; update
+ * the running statistics of the `nbnu` BatchNorm layers (isg_bn_update_running). `gf` and
+ * `bnu` are DEVICE arrays. owner[i]: bit 0 = Adam updates element i (a used parameter),
+ * bit 1 = a grad_final item writes grad[i] (the fold skips it). Bitwise the result of those
+ * separate calls. hyper = (lr, beta1, beta2, eps, weight_decay), device doubles. */
+typedef struct {
+    float* grad;
+    const double* rep;         /* nrep replicas, replica stride n */
+    int64_t n;
+    int32_t nrep;
+    int32_t ngf;
+    float* param;
+    float* exp_avg;
+    float* exp_avg_sq;
+    const uint8_t* owner;
+    const int32_t* step;
+    const double* hyper;
+    const isg_grad_final* gf;
+    const isg_bn_update* bnu;
+    int32_t nbnu;
+    int32_t pad_;
+} isg_step_tail_args;
+int32_t isg_step_tail(const isg_step_tail_args* args, isg_stream_t stream);
+/* step += 1 on the device (the 1-based Adam step of isg_step_tail / isg_adam_dev). */
+int32_t isg_step_inc(int32_t* step, isg_stream_t stream);
+
 /* sigmoid + nn.BCELoss(mean) forward and backward in one pass (segment.py:534,
  * train_instance.py:299,378-379), torch clamp semantics: log clamped at -100,
  * dL/dp = (p-y)/max(p(1-p),1e-12)/n, dL/dlogit = dL/dp * p(1-p).
@@ -518,7 +548,7 @@ int32_t isg_side_stream_create(int32_t keep, isg_stream_t* out);
 /* sizeof() of the ABI structs and executor records (0 vtensor, 1 sinks, 2 conv record,
  * 3 wgrad record, 4 pool record, 5 tail, 6 tail_grad, 7 bn_update, 8 grad_final,
  * 9 bce record, 10 conv_geom, 11 bn, 12 vseg, 13 sink, 14 sum_rep record, 15 kp_stem,
- * 16 mask_head, 17 stamp record, 18 depthwise-backward record) so
+ * 16 mask_head, 17 stamp record, 18 depthwise-backward record, 19 step tail) so
  * bindings can verify layouts. */
 int32_t isg_record_size(int32_t which);
 

@@ -158,6 +158,18 @@ class DwBwdRec(Structure):
                 ("pad_", c_int32)]
 
 
+class StepTail(Structure):  # isg.h isg_step_tail_args (also the OP_STEP_TAIL record)
+    _fields_ = [("grad", c_void_p), ("rep", c_void_p), ("n", c_int64), ("nrep", c_int32),
+                ("ngf", c_int32), ("param", c_void_p), ("exp_avg", c_void_p),
+                ("exp_avg_sq", c_void_p), ("owner", c_void_p), ("step", c_void_p),
+                ("hyper", c_void_p), ("gf", c_void_p), ("bnu", c_void_p), ("nbnu", c_int32),
+                ("pad_", c_int32)]
+
+
+class StepIncRec(Structure):
+    _fields_ = [("step", c_void_p)]
+
+
 OP_CONV_FWD, OP_CONV_DGRAD, OP_CONV_WGRAD, OP_CONVT_FWD = 1, 2, 3, 4
 OP_MAXPOOL_FWD, OP_MAXPOOL_BWD, OP_TAIL_FWD, OP_TAIL_BWD = 5, 6, 7, 8
 OP_BN_UPDATE, OP_GRAD_FINAL, OP_BCE, OP_MEMSET = 9, 10, 11, 12
@@ -167,11 +179,12 @@ OP_HEAD_FWD, OP_HEAD_BWD = 18, 19
 OP_STAMP = 20
 OP_DW_BWD = 21
 OP_HEAD_FOLD = 22
+OP_STEP_TAIL, OP_STEP_INC = 24, 25
 
 _RECORD_CHECK = [(0, VTensor), (1, Sinks), (2, ConvRec), (3, WgradRec), (4, PoolRec), (5, Tail),
                  (6, TailGrad), (7, BnUpdate), (8, GradFinal), (9, BceRec), (10, Geom), (11, Bn),
                  (12, VSeg), (13, Sink), (14, SumRepRec), (15, KpStem), (16, MaskHead),
-                 (17, StampRec), (18, DwBwdRec)]
+                 (17, StampRec), (18, DwBwdRec), (19, StepTail)]
 
 # exported symbol -> (restype, argtypes)
 SIGNATURES = {
@@ -201,6 +214,8 @@ SIGNATURES = {
     "isg_adam_dev": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
                                c_void_p, c_double, c_double, c_double, c_double, c_double,
                                c_void_p]),
+    "isg_step_tail": (c_int32, [POINTER(StepTail), c_void_p]),
+    "isg_step_inc": (c_int32, [c_void_p, c_void_p]),
     "isg_fill_f64": (c_int32, [c_void_p, c_int64, c_double, c_void_p]),
     "isg_stamp": (c_int32, [c_void_p, c_int32, c_int32, c_void_p]),
     "isg_mask_paste": (c_int32, [c_void_p, c_int32, c_int32, c_void_p, c_int32, c_int32, c_void_p,

@@ -207,6 +207,8 @@ enum {
     OP_HEAD_BWD = 19,
     OP_STAMP = 20,
     OP_DW_BWD = 21,
+    OP_STEP_TAIL = 24,
+    OP_STEP_INC = 25,
     OP_HEAD_FOLD = 22,
 };
 
@@ -260,6 +262,9 @@ struct BceRec {
 struct MemsetRec {
     void* p;
     int64_t bytes;
+};
+struct StepIncRec {  // OP_STEP_INC: isg_step_inc
+    int32_t* step;
 };
 struct DwBwdRec {  // OP_DW_BWD: isg_depthwise_bwd
     isg_conv_geom g;
@@ -412,6 +417,14 @@ static int32_t run_op(int32_t kind, char* buf, isg_stream_t st) {
         case OP_STAMP: {
             auto* r = (StampRec*)buf;
             rc = isg_stamp(r->buf, r->slot, r->sign, st);
+            break;
+        }
+        case OP_STEP_TAIL:
+            rc = isg_step_tail((const isg_step_tail_args*)buf, st);
+            break;
+        case OP_STEP_INC: {
+            auto* r = (StepIncRec*)buf;
+            rc = isg_step_inc(r->step, st);
             break;
         }
         case OP_MEMSET: {
@@ -683,6 +696,7 @@ int32_t isg_record_size(int32_t which) {
         case 16: return (int32_t)sizeof(isg_mask_head);
         case 17: return (int32_t)sizeof(StampRec);
         case 18: return (int32_t)sizeof(DwBwdRec);
+        case 19: return (int32_t)sizeof(isg_step_tail_args);
         default: return -1;
     }
 }

@@ -559,10 +559,7 @@ struct GradFinalList {
     isg_grad_final it[ISG_LIST_CHUNK];
 };
 
-__global__ void bn_update_kernel(BnUpdateList items, int nitems) {
-    const int it = blockIdx.x;
-    if (it >= nitems) return;
-    const isg_bn_update& u = items.it[it];
+ISG_DEV void bn_update_item(const isg_bn_update& u) {
     for (int c = threadIdx.x; c < u.C; c += blockDim.x) {
         const double M = (double)u.count;
         const double mean = rep_sum(u.stats, 4 * u.C, c) / M;
@@ -574,6 +571,12 @@ __global__ void bn_update_kernel(BnUpdateList items, int nitems) {
         u.running_var[c] = (1.f - m) * u.running_var[c] + m * (float)unb;
     }
     if (threadIdx.x == 0 && u.num_batches_tracked) u.num_batches_tracked[0] += 1;
+}
+
+__global__ void bn_update_kernel(BnUpdateList items, int nitems) {
+    const int it = blockIdx.x;
+    if (it >= nitems) return;
+    bn_update_item(items.it[it]);
 }
 
 struct BnFinalList {
@@ -615,13 +618,13 @@ __global__ void bn_finalize1_kernel(isg_bn bn, int bwd) {
     }
 }
 
-__global__ void grad_final_kernel(GradFinalList items, int nitems) {
-    const int it = blockIdx.x;
-    if (it >= nitems) return;
-    const isg_grad_final& f = items.it[it];
+// one item's values; put(dst, value) stores each (grad_final_kernel: a plain store; the
+// fused step tail: the store plus that element's Adam update)
+template <class Put>
+ISG_DEV void grad_final_item(const isg_grad_final& f, Put put) {
     for (int c = threadIdx.x; c < f.C; c += blockDim.x) {
         if (f.slope_acc) {
-            f.dslope[c] = (float)rep_sum(f.slope_acc, f.slope_stride, c);
+            put(f.dslope + c, (float)rep_sum(f.slope_acc, f.slope_stride, c));
             continue;
         }
         const double M = (double)f.count;
@@ -638,8 +641,8 @@ __global__ void grad_final_kernel(GradFinalList items, int nitems) {
         const double gs = rep_sum(f.stats, 4 * f.C, 2 * f.C + c);
         const double gxs = rep_sum(f.stats, 4 * f.C, 3 * f.C + c);  // sum g*(y - mean), centred
         const double dgamma = rstd * gxs;
-        if (f.dgamma) f.dgamma[c] = (float)dgamma;
-        if (f.dbeta) f.dbeta[c] = (float)gs;
+        if (f.dgamma) put(f.dgamma + c, (float)dgamma);
+        if (f.dbeta) put(f.dbeta + c, (float)gs);
         if (f.dconv_bias) {
             // sum over pixels of dy = A*g + B*(y-mean) + C  (BatchNorm backward)
             const double gam = (double)f.gamma[c];
@@ -651,9 +654,15 @@ __global__ void grad_final_kernel(GradFinalList items, int nitems) {
             } else {
                 db = gam * rstd * gs;
             }
-            f.dconv_bias[c] = (float)db;
+            put(f.dconv_bias + c, (float)db);
         }
     }
+}
+
+__global__ void grad_final_kernel(GradFinalList items, int nitems) {
+    const int it = blockIdx.x;
+    if (it >= nitems) return;
+    grad_final_item(items.it[it], [](float* d, float v) { *d = v; });
 }
 
 // ---- sigmoid + BCE ----------------------------------------------------------------
@@ -791,34 +800,88 @@ __global__ void adam_kernel(float* p, const float* g, float* m, float* v, const 
 // the bias corrections from them, so a float beta would leave this kernel self-consistent
 // but 1.3e-5 (relative) off torch's second moment whenever the optimizer state comes from
 // torch (a reference checkpoint, train_instance.py:320-328).
+struct AdamCoef {
+    float neg_step, bc2_sqrt, w1, b2f, one_m_b2, epsf, wdf;
+};
+ISG_DEV AdamCoef adam_coef(int32_t step, double lr, double b1, double b2, double eps, double wd) {
+#pragma clang fp contract(off)
+    const double st = (double)step;
+    const double bc1 = 1.0 - pow(b1, st);
+    const double bc2 = 1.0 - pow(b2, st);
+    AdamCoef k;
+    k.neg_step = (float)(-(lr / bc1));
+    k.bc2_sqrt = (float)sqrt(bc2);
+    k.w1 = (float)(1.0 - b1);
+    k.b2f = (float)b2;
+    k.one_m_b2 = (float)(1.0 - b2);
+    k.epsf = (float)eps;
+    k.wdf = (float)wd;
+    return k;
+}
+ISG_DEV void adam_elem(float* p, float* m, float* v, int64_t i, float gi, const AdamCoef& k) {
+#pragma clang fp contract(off)
+    const float pi = p[i];
+    if (k.wdf != 0.f) gi = gi + k.wdf * pi;
+    float mi = m[i];
+    mi = mi + k.w1 * (gi - mi);
+    float vi = v[i] * k.b2f;
+    vi = vi + k.one_m_b2 * gi * gi;
+    const float denom = sqrtf(vi) / k.bc2_sqrt + k.epsf;
+    m[i] = mi;
+    v[i] = vi;
+    p[i] = pi + k.neg_step * mi / denom;
+}
+
 __global__ void adam_dev_kernel(float* p, const float* g, float* m, float* v, const uint8_t* live,
                                 int64_t n, const int32_t* step, double lr, double b1, double b2,
                                 double eps, double wd) {
-#pragma clang fp contract(off)
-    const double st = (double)*step;
-    const double bc1 = 1.0 - pow(b1, st);
-    const double bc2 = 1.0 - pow(b2, st);
-    const float neg_step = (float)(-(lr / bc1));
-    const float bc2_sqrt = (float)sqrt(bc2);
-    const float w1 = (float)(1.0 - b1);
-    const float b2f = (float)b2;
-    const float one_m_b2 = (float)(1.0 - b2);
-    const float epsf = (float)eps, wdf = (float)wd;
+    const AdamCoef k = adam_coef(*step, lr, b1, b2, eps, wd);
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x) {
         if (live && !live[i]) continue;
-        float gi = g[i];
-        const float pi = p[i];
-        if (wdf != 0.f) gi = gi + wdf * pi;
-        float mi = m[i];
-        mi = mi + w1 * (gi - mi);
-        float vi = v[i] * b2f;
-        vi = vi + one_m_b2 * gi * gi;
-        const float denom = sqrtf(vi) / bc2_sqrt + epsf;
-        m[i] = mi;
-        v[i] = vi;
-        p[i] = pi + neg_step * mi / denom;
+        adam_elem(p, m, v, i, g[i], k);
     }
+}
+
+// The end of a world-1 training step in ONE launch (isg.h isg_step_tail): workgroups
+// [0, nfold) fold the weight-gradient replicas into the flat gradient and apply Adam to each
+// folded element; the next ngf fold the statistics-derived gradients (grad_final_item) and
+// apply Adam to those; the last nbnu update the BatchNorm running statistics. Element
+// arithmetic is sum_rep_n_kernel's, grad_final_kernel's and adam_dev_kernel's (the same
+// device functions), so the result is bitwise that of the separate launches, which ran as
+// 1 + 5 + 1 (+1 step counter) launches hopping between streams, plus 3 BN-update launches
+// on the forward's critical path.
+template <int NREP>
+__global__ __launch_bounds__(kThreads) void step_tail_kernel(isg_step_tail_args a, int nfold) {
+    const int b = blockIdx.x;
+    const double* hp = a.hyper;
+    const AdamCoef k = adam_coef(*a.step, hp[0], hp[1], hp[2], hp[3], hp[4]);
+    if (b < nfold) {
+        const int64_t i = (int64_t)b * kThreads + threadIdx.x;
+        if (i >= a.n) return;
+        const uint8_t o = a.owner[i];
+        if (o & 2) return;  // written by a grad_final item below
+        double v[NREP];
+#pragma unroll
+        for (int r = 0; r < NREP; ++r) v[r] = gld_d(a.rep, r * a.n + i);
+        double s = v[0];
+#pragma unroll
+        for (int r = 1; r < NREP; ++r) s += v[r];
+        const float g = (float)s;
+        a.grad[i] = g;
+        if (o & 1) adam_elem(a.param, a.exp_avg, a.exp_avg_sq, i, g, k);
+        return;
+    }
+    if (b < nfold + a.ngf) {
+        const isg_grad_final f = a.gf[b - nfold];
+        grad_final_item(f, [&](float* d, float g) {
+            *d = g;
+            const int64_t i = d - a.grad;
+            if (a.owner[i] & 1) adam_elem(a.param, a.exp_avg, a.exp_avg_sq, i, g, k);
+        });
+        return;
+    }
+    if (b < nfold + a.ngf + a.nbnu) bn_update_item(a.bnu[b - nfold - a.ngf]);
 }
 
 __global__ void step_inc_kernel(int32_t* c) { *c += 1; }
@@ -1049,6 +1112,29 @@ int32_t isg_adam_dev(float* param, const float* grad, float* exp_avg, float* exp
     hipLaunchKernelGGL(adam_dev_kernel, dim3(grid_for(n)), dim3(kThreads), 0, st, param, grad,
                        exp_avg, exp_avg_sq, live, n, step, lr, beta1, beta2, eps, weight_decay);
     return isg_check_launch("adam_dev_kernel");
+}
+
+int32_t isg_step_tail(const isg_step_tail_args* a, isg_stream_t st) {
+    if (!a || !a->grad || !a->rep || !a->param || !a->exp_avg || !a->exp_avg_sq || !a->owner ||
+        !a->step || !a->hyper || a->n < 0 || (a->ngf > 0 && !a->gf) || (a->nbnu > 0 && !a->bnu) ||
+        a->ngf < 0 || a->nbnu < 0)
+        return isg_set_error(ISG_ERR_INVALID, "step tail: NULL or negative argument");
+    if (a->nrep != 16 && a->nrep != 8 && a->nrep != 4)
+        return isg_set_error(ISG_ERR_UNSUPPORTED, "step tail: %d replicas (4, 8 or 16)", a->nrep);
+    const int64_t nfold = (a->n + kThreads - 1) / kThreads;
+    const int64_t grid = nfold + a->ngf + a->nbnu;
+    if (grid < 1) return ISG_OK;
+    if (grid >= ((int64_t)1 << 31)) return isg_set_error(ISG_ERR_UNSUPPORTED, "step tail: %lld elements", (long long)a->n);
+    if (a->nrep == 16) hipLaunchKernelGGL(step_tail_kernel<16>, dim3((unsigned)grid), dim3(kThreads), 0, st, *a, (int)nfold);
+    else if (a->nrep == 8) hipLaunchKernelGGL(step_tail_kernel<8>, dim3((unsigned)grid), dim3(kThreads), 0, st, *a, (int)nfold);
+    else hipLaunchKernelGGL(step_tail_kernel<4>, dim3((unsigned)grid), dim3(kThreads), 0, st, *a, (int)nfold);
+    return isg_check_launch("step_tail_kernel");
+}
+
+int32_t isg_step_inc(int32_t* step, isg_stream_t st) {
+    if (!step) return isg_set_error(ISG_ERR_INVALID, "step inc: NULL counter");
+    hipLaunchKernelGGL(step_inc_kernel, dim3(1), dim3(1), 0, st, step);
+    return isg_check_launch("step_inc_kernel");
 }
 
 int32_t isg_sum_replicas(float* dst, const double* src, int64_t n, int32_t nrep, int64_t stride,

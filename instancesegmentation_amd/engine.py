@@ -38,7 +38,11 @@ S_DOUT = (10, 11)
 S_DIN = (12, 13)
 S_WREP = 14  # L.WREP fp64 replicas of the flat parameter gradient (wgrad atomics, isg.h)
 S_STAMP = 15  # timestamp buffer of OP_STAMP records (isg_stamp: uint32 counter, then slots)
-S_TENSOR0 = 16
+# the fused step tail (Plan fused_tail, isg.h isg_step_tail): the Trainer's flat parameters,
+# Adam moments, per-element owner mask, device step counter, hyperparameters (5 doubles) and
+# the device tables of its grad_final / BatchNorm-update items
+S_PARAM, S_EXPAVG, S_EXPAVGSQ, S_OWNER, S_STEP, S_HYPER, S_TAILGF, S_TAILBNU = range(16, 24)
+S_TENSOR0 = 24
 
 ALIGN = 64  # elements (256 B) between arena buffers
 
@@ -1415,13 +1419,23 @@ class TailOp:
 class Plan:
     """Compiled forward (+ optional backward) op lists of one module at one shape."""
 
-    def __init__(self, owner, in_shapes, train, need_grad, in_grad, buckets=2, layout=None):
+    def __init__(self, owner, in_shapes, train, need_grad, in_grad, buckets=2, layout=None,
+                 fused_tail=False):
         """buckets: gradient buckets of the backward (2: the stem's parameters finalised in a
         second part after the others, for a data-parallel exchange that overlaps the stem
         backward; 1: one part, every finalisation at the end — at world size 1 nothing
         needs bucket 1 early, and the part boundary's side-stream join made the stem's
-        input-gradient chain wait ~0.6 ms for the queued weight gradients)."""
+        input-gradient chain wait ~0.6 ms for the queued weight gradients).
+        fused_tail (a training plan with one bucket: the Trainer at world size 1): the
+        backward ends in ONE OP_STEP_TAIL record — replica fold, gradient finalisation,
+        Adam and the BatchNorm running-stat updates (isg.h isg_step_tail) — instead of the
+        fold, the finalisation lists and the forward's BN-update lists; the Adam step
+        counter advances in an OP_STEP_INC record forked at the backward's head. Its
+        pointers come from slots S_PARAM..S_TAILBNU; the item tables to resolve and upload
+        are tail_gf / tail_bnu (Records), the owned gradient ranges tail_owned."""
         self.n_buckets = buckets
+        self.fused_tail = bool(fused_tail and train and need_grad and buckets == 1)
+        self.tail_gf, self.tail_bnu, self.tail_owned = None, None, []
         N = in_shapes[0][0]
         g = Graph(owner, N, train, need_grad, layout)
         ins = [g.input(i, s[1], s[2], s[3], in_grad[i]) if len(s) == 4 else
@@ -1475,6 +1489,7 @@ class Plan:
                 if bnr is not None:
                     rng.append((S_STATS, bnr.stats_off * 8, bnr.coef_end * 8))
                 side_recs += [(r, rng) for r in fw.recs[i0:]]
+        self.tail_bnu = None
         if train and g.bns:
             items = []
             for b in g.bns:
@@ -1482,6 +1497,11 @@ class Plan:
                               "running_mean": b.names["rm"], "running_var": b.names["rv"],
                               "num_batches_tracked": b.names["nbt"], "C": b.C,
                               "count": float(b.count), "momentum": float(b.mod.momentum)})
+            if self.fused_tail:  # updated by the step tail (the statistics stay intact)
+                self.tail_bnu = Record(L.OP_BN_UPDATE, L.ListRec, {"n": len(items)}, L.BnUpdate,
+                                       items)
+                self.tail_bnu_n = len(items)
+                items = []
             # (measured: forked as one side batch at the head of the backward instead, the
             # step was 0.1 ms slower, profiles/r07v_ab_bn_update.txt)
             for i in range(0, len(items), L.LIST_CHUNK):
@@ -1509,6 +1529,49 @@ class Plan:
                     or wb.data_ptr() != wa.data_ptr() + nb):
                 return False
         return True
+
+    def tail_tables(self, table):
+        """The fused tail's item tables with every pointer resolved against `table` (the
+        pointer-table array the Trainer runs the plan with): (grad_final items bytes,
+        BatchNorm-update items bytes), to upload into the buffers of slots S_TAILGF /
+        S_TAILBNU. The Trainer's arenas never move, so this is done once."""
+        def resolve(rec):
+            if rec is None:
+                return b""
+            body = bytearray(rec.body)
+            for loc, slot, off in rec.fix:
+                base = table[slot]
+                struct.pack_into("<Q", body, loc, (base + off) if base else 0)
+            return bytes(body[ctypes.sizeof(L.ListRec):])
+        return resolve(self.tail_gf), resolve(self.tail_bnu)
+
+    def _step_tail(self, g, ol, gf_items):
+        """The fused end of the step (fused_tail): the Adam step counter advanced on the side
+        stream from the backward's head (the tail's join waits for it), then one
+        OP_STEP_TAIL record joining every forked weight gradient."""
+        inc = Record(L.OP_STEP_INC, L.StepIncRec, {"step": Ptr(S_STEP)}, label="step_inc")
+        inc.flags |= Record.OPF_SIDE | Record.OPF_FORK_NOW
+        ol.recs.insert(0, inc)
+        self.tail_gf = Record(L.OP_GRAD_FINAL, L.ListRec, {"n": len(gf_items)}, L.GradFinal,
+                              gf_items)
+        # gradient elements a grad_final item writes (the fold skips them): (offset, count)
+        self.tail_owned = []
+        for it in gf_items:
+            for k in ("dgamma", "dbeta", "dconv_bias", "dslope"):
+                v = it.get(k)
+                if isinstance(v, Ptr):
+                    assert v.slot == S_PGRAD and v.off % 4 == 0
+                    self.tail_owned.append((v.off // 4, it["C"]))
+        nbnu = self.tail_bnu_n if self.tail_bnu else 0
+        r = Record(L.OP_STEP_TAIL, L.StepTail,
+                   {"grad": Ptr(S_PGRAD), "rep": Ptr(S_WREP), "n": g.pgrad_size, "nrep": L.WREP,
+                    "ngf": len(gf_items), "param": Ptr(S_PARAM), "exp_avg": Ptr(S_EXPAVG),
+                    "exp_avg_sq": Ptr(S_EXPAVGSQ), "owner": Ptr(S_OWNER), "step": Ptr(S_STEP),
+                    "hyper": Ptr(S_HYPER), "gf": Ptr(S_TAILGF),
+                    "bnu": Ptr(S_TAILBNU) if nbnu else None, "nbnu": nbnu},
+                   label="step_tail")
+        r.flags |= Record.OPF_JOIN  # every forked weight gradient (and the counter) is done
+        ol.add(r)
 
     @staticmethod
     def _late_prefix(g):
@@ -1674,6 +1737,9 @@ class Plan:
             for r in body.recs[split:]:
                 part2.add(r)
             close(part2, 0, cut, [it for m, it in items if is_late(m)])
+        elif self.fused_tail:
+            cut = 0
+            self._step_tail(g, part1, [it for _, it in items])
         else:
             cut = 0
             close(part1, 0, g.pgrad_size, [it for _, it in items])

@@ -25,7 +25,8 @@ import torch
 import torch.distributed as dist
 
 from . import _lib as L
-from .engine import (S_ACT, S_DOUT, S_GRAD, S_IN, S_OUT, S_PGRAD, S_STAMP, S_STATS, S_TENSOR0,
+from .engine import (S_ACT, S_DOUT, S_EXPAVG, S_EXPAVGSQ, S_GRAD, S_HYPER, S_IN, S_OUT, S_OWNER,
+                     S_PARAM, S_PGRAD, S_STAMP, S_STATS, S_STEP, S_TAILBNU, S_TAILGF, S_TENSOR0,
                      S_WREP, Plan, param_layout)
 
 STAMP_HZ = 100e6  # s_memrealtime: the chip-global 100 MHz counter (MI355X_MICROARCH.md)
@@ -130,12 +131,16 @@ class Trainer:
     on a CPU device (tests drive its exchange over gloo); `step()` needs the GPU."""
 
     def __init__(self, model, batch, in_shapes, device=None, lr=1e-3, betas=(0.9, 0.999),
-                 eps=1e-8, weight_decay=0.0, process_group=None, dp_plan=None):
+                 eps=1e-8, weight_decay=0.0, process_group=None, dp_plan=None, fused_tail=None):
         """dp_plan: build the data-parallel step structure (two backward parts, two gradient
         buckets, three HIP graphs with the exchange markers between them) even at world
         size 1 — what that structure costs on one GPU (bench.py's dp_plan legs). Without a
         process group its exchanges are no-ops; with one (a world-size-1 "nccl" group) they
-        are real one-rank RCCL all-reduces. Default: only at world size > 1."""
+        are real one-rank RCCL all-reduces. Default: only at world size > 1.
+        fused_tail: end the single-bucket step (no data-parallel exchange) in ONE launch —
+        replica fold, gradient finalisation, Adam, BatchNorm running statistics
+        (isg.h isg_step_tail, Plan fused_tail); default: whenever there is no exchange.
+        False keeps the separate launches (the parity reference of the fused form)."""
         self.device = torch.device(device or "cuda")
         dev = self.device
         self.model = model.to(dev).train()
@@ -150,10 +155,12 @@ class Trainer:
         self.flat, self.flatb, self.index = flatten_module(self.model, dev, self.comm[n:], layout)
         self.in_shapes = [tuple(s) for s in in_shapes]
         # two gradient buckets only where an exchange overlaps the stem backward (Plan)
+        buckets = int(os.environ.get("ISG_BUCKETS", "0")) or (2 if self.dp_plan else 1)
+        self.fused_tail = (not self.dp_plan and buckets == 1) if fused_tail is None else bool(fused_tail)
         self.plan = Plan(self.model, self.in_shapes, True, True,
-                         tuple(False for _ in self.in_shapes),
-                         buckets=int(os.environ.get("ISG_BUCKETS", "0")) or (2 if self.dp_plan else 1),
-                         layout=layout)
+                         tuple(False for _ in self.in_shapes), buckets=buckets, layout=layout,
+                         fused_tail=self.fused_tail)
+        self.fused_tail = self.plan.fused_tail
         g = self.plan.graph
         assert g.pgrad_size == n
         for k, (off, _) in zip(g.params, self.index):  # the plan's gradient layout is the flat one
@@ -191,7 +198,22 @@ class Trainer:
         self.inputs = [torch.empty(s, dtype=torch.float32 if len(s) == 4 else torch.float64,
                                    device=dev) for s in self.in_shapes]
         self.target = torch.empty(self.plan.out_shapes[0], dtype=torch.float32, device=dev)
+        # the fused tail's operands (Plan fused_tail): hyperparameters as device doubles (so
+        # a captured graph follows load_optimizer_state_dict), the owner mask (bit 0: Adam
+        # updates the element, bit 1: a grad_final item writes its gradient)
+        self.hyper = torch.tensor(self._hyper_vec(), dtype=torch.float64, device=dev)
+        owner = live.clone()
+        for off, cnt in self.plan.tail_owned:
+            owner[off:off + cnt] |= 2
+        self.owner = owner.to(dev)
         self.table = self._make_table()
+        self.tail_items = None
+        if self.fused_tail:
+            gf, bnu = self.plan.tail_tables(self.table)
+            self.tail_items = [torch.frombuffer(bytearray(b or b"\0"), dtype=torch.uint8).to(dev)
+                               for b in (gf, bnu)]
+            self.table[S_TAILGF] = self.tail_items[0].data_ptr()
+            self.table[S_TAILBNU] = self.tail_items[1].data_ptr() if bnu else None
         self.graphs = None
         self._captured = (None, None)
         self.events = []
@@ -216,6 +238,12 @@ class Trainer:
             tab[S_IN[i]] = x.data_ptr()
         tab[S_OUT[0]] = self.logits.data_ptr()
         tab[S_DOUT[0]] = self.dlogits.data_ptr()
+        tab[S_PARAM] = self.flat.data_ptr()
+        tab[S_EXPAVG] = self.exp_avg.data_ptr()
+        tab[S_EXPAVGSQ] = self.exp_avg_sq.data_ptr()
+        tab[S_OWNER] = self.owner.data_ptr()
+        tab[S_STEP] = self.step_dev.data_ptr()
+        tab[S_HYPER] = self.hyper.data_ptr()
         tensors = [p for _, p in self.model.named_parameters()] + \
                   [b for _, b in self.model.named_buffers()]
         for j, t in enumerate(tensors):
@@ -226,6 +254,10 @@ class Trainer:
     def _hyper(self):
         return (float(self.lr), tuple(float(b) for b in self.betas), float(self.eps),
                 float(self.wd))
+
+    def _hyper_vec(self):
+        return [float(self.lr), float(self.betas[0]), float(self.betas[1]), float(self.eps),
+                float(self.wd)]
 
     def _adam(self):
         L.check(L.lib().isg_adam_dev(self.flat.data_ptr(), self.grad_flat.data_ptr(),
@@ -297,7 +329,8 @@ class Trainer:
                     units += [self._mask_buffers, "coll1"]
         if dp:
             units.append("coll2")
-        units.append(self._adam)
+        if not self.fused_tail:  # (fused: Adam ran inside the backward's step tail)
+            units.append(self._adam)
         return units
 
     def stamp_reset(self):
@@ -467,6 +500,7 @@ class Trainer:
                 assert st["exp_avg"].shape == params[i].shape
         self.step_dev.fill_(max(steps) if steps else 0)
         self.step_count = max(steps) if steps else 0
+        self.hyper.copy_(torch.tensor(self._hyper_vec(), dtype=torch.float64))
         # isg_adam_dev takes lr/betas/eps/wd by value, so a captured graph holds the old
         # ones: re-record the step when the loaded hyperparameters differ
         if self.graphs and self._captured[1] != self._hyper():

@@ -320,3 +320,41 @@ def test_bn_final_launches_match_default(monkeypatch):
         err = (g - base).abs().max().item()
         print("ISG_BN_FINAL=1", i, f"max abs diff {err:.2e} (scale {scale:.2e})")
         assert err <= 1e-5 * scale, (i, err)
+
+
+@pytest.mark.parametrize("graph", [True, False], ids=["graph", "eager"])
+def test_fused_step_tail_matches_separate_launches(graph):
+    """The world-1 step's fused tail (isg.h isg_step_tail: replica fold + gradient
+    finalisation + Adam + BatchNorm running statistics in one launch, the step counter
+    advanced on the side stream) against the separate launches it replaces (OP_SUM_REP,
+    the OP_GRAD_FINAL lists, isg_adam_dev, the forward's OP_BN_UPDATE lists): over three
+    steps on the keypoint path, the flat gradient, parameters, both Adam moments, the
+    running statistics and the step counter are bit-identical."""
+    from instancesegmentation_amd.data import device_batch
+    torch.manual_seed(321)
+    init = Segment(20).state_dict()
+    xs, mask = device_batch(2, 256, 256, DEV, seed=77, keypoints=True)
+
+    def run(fused):
+        m = Segment(20)
+        m.load_state_dict(init)
+        tr = Trainer(m, 2, [tuple(x.shape) for x in xs], device=DEV, fused_tail=fused)
+        assert tr.fused_tail == fused
+        if graph:
+            tr.capture()
+        out = []
+        for _ in range(3):
+            tr.step(xs, mask)
+            torch.cuda.synchronize()
+            out.append([t.detach().clone() for t in (tr.grad_flat, tr.flat, tr.exp_avg,
+                                                     tr.exp_avg_sq, tr.flatb, tr.step_dev)])
+        return out, tr.loss()
+
+    (a, la), (b, lb) = run(True), run(False)
+    names = ("grad", "params", "exp_avg", "exp_avg_sq", "running stats", "step")
+    for k, (sa, sb) in enumerate(zip(a, b)):
+        diff = [int((u != v).sum()) for u, v in zip(sa, sb)]
+        print(f"step {k + 1}: elements differing fused vs separate {dict(zip(names, diff))}")
+        assert diff == [0] * 6, (k, diff)
+    assert int(a[-1][5].item()) == 3
+    assert abs(la - lb) <= 1e-12 * max(1.0, abs(lb))

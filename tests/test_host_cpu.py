@@ -465,3 +465,48 @@ def test_library_has_no_undefined_isg_symbols():
     out = subprocess.run([nm, "-D", so], capture_output=True, text=True, check=True).stdout
     undef = [l.split()[-1] for l in out.splitlines() if " U " in l and l.split()[-1].startswith("isg_")]
     assert not undef, undef
+
+
+def test_fused_step_tail_plan():
+    """Plan(fused_tail=True) (the Trainer at world size 1): the forward has no BN-update
+    list, the backward no replica fold / finalisation lists; it starts with the step
+    counter forked on the side stream and ends in ONE OP_STEP_TAIL that joins every forked
+    record; the item tables resolve to non-NULL pointers and the owned gradient ranges are
+    exactly the grad_final outputs (BN gamma/beta, PReLU slopes, conv biases before BN)."""
+    import ctypes
+    from instancesegmentation_amd.engine import S_PGRAD, S_STATS, S_TENSOR0, Record, param_layout
+    from instancesegmentation_amd.train import flatten_module
+    m = Segment(20)
+    lay = param_layout(m)
+    flatten_module(m, "cpu", order=lay)
+    shapes = [(2, 3, 128, 128), (2, 17, 3)]
+    p = Plan(m, shapes, True, True, (False, False), buckets=1, layout=lay, fused_tail=True)
+    q = Plan(m, shapes, True, True, (False, False), buckets=1, layout=lay)
+    assert p.fused_tail and not q.fused_tail
+    assert not any(r.kind == L.OP_BN_UPDATE for r in p.fwd.recs)
+    assert not any(r.kind in (L.OP_SUM_REP, L.OP_GRAD_FINAL) for r in p.bwd.recs)
+    first, last = p.bwd.recs[0], p.bwd.recs[-1]
+    assert first.kind == L.OP_STEP_INC and first.flags & Record.OPF_SIDE and first.flags & Record.OPF_FORK_NOW
+    assert last.kind == L.OP_STEP_TAIL and last.flags & Record.OPF_JOIN and not last.flags >> Record.EXCL_SHIFT
+    assert [r.label for r in p.bwd.recs[1:-1]] == [r.label for r in q.bwd.recs
+                                                   if r.kind not in (L.OP_SUM_REP, L.OP_GRAD_FINAL)]
+    ngf = sum(len(r.body) - ctypes.sizeof(L.ListRec) for r in q.bwd.recs if r.kind == L.OP_GRAD_FINAL)
+    nbnu = sum(len(r.body) - ctypes.sizeof(L.ListRec) for r in q.fwd.recs if r.kind == L.OP_BN_UPDATE)
+    tab = (ctypes.c_void_p * (S_TENSOR0 + len(p.graph.tensor_names)))()
+    for i in range(len(tab)):
+        tab[i] = 0x100000 * (i + 1)
+    gf, bnu = p.tail_tables(tab)
+    assert len(gf) == ngf and len(bnu) == nbnu
+    items = (L.GradFinal * (len(gf) // ctypes.sizeof(L.GradFinal))).from_buffer_copy(gf)
+    base = tab[S_PGRAD]
+    owned = set()
+    for it in items:
+        assert it.stats is None or it.stats >= tab[S_STATS]
+        for f in ("dgamma", "dbeta", "dconv_bias", "dslope"):
+            v = getattr(it, f)
+            if v:
+                owned |= set(range((v - base) // 4, (v - base) // 4 + it.C))
+    want = set()
+    for off, cnt in p.tail_owned:
+        want |= set(range(off, off + cnt))
+    assert owned == want and len(want) > 0
