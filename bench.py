@@ -40,7 +40,10 @@ def parse():
     ap.add_argument("--dominant", default="",
                     help="phase:label of the roofline op (skips the per-op timing pass, so a "
                          "profiler sees training steps only), e.g. bwd:d_out0")
-    ap.add_argument("--eager", action="store_true", help="no HIP graph capture")
+    ap.add_argument("--eager", action="store_true", help="(the default) no HIP graph capture")
+    ap.add_argument("--graph", action="store_true",
+                    help="capture the step into HIP graphs (round 6 measured the executor's "
+                         "eager issue faster: DESIGN §3.6)")
     ap.add_argument("--no-infer", action="store_true", help="skip the inference leg")
     ap.add_argument("--input", default="keypoints", choices=("keypoints", "heatmaps"),
                     help="what the data loader hands the step: keypoints (the 17 heatmaps "
@@ -158,7 +161,8 @@ def stamp_op(trainer, phase, label, args):
         return None
     rec = ol.recs[idx]
     trainer.stamp_at = (phase, idx)
-    trainer.capture()
+    if args.graph:
+        trainer.capture()
     for _ in range(2):
         trainer.step(loss=False)
     torch.cuda.synchronize()
@@ -388,7 +392,7 @@ def _train_leg(args, dev, world, rank, keypoints, roofline, dp_plan=None):
         ol = trainer.plan.fwd if dom[0] == "fwd" else trainer.plan.bwd
         dom_rec = ol.recs[dom[1]]
         trainer.stamp_at = dom
-    if not args.eager:
+    if args.graph:
         trainer.capture()
     # loss=False: the step's BCE still accumulates the summed loss in the graph (reported
     # through trainer.loss() below); only the per-step eager division for a returned mean
@@ -428,7 +432,7 @@ def _train_leg(args, dev, world, rank, keypoints, roofline, dp_plan=None):
         roof["traffic"] = pmc_traffic(dom_rec.label, args)
     res = {"value": world * args.batch * args.steps / elapsed,
            "ms_per_step": 1e3 * elapsed / args.steps, "loss": trainer.loss(), "roofline": roof}
-    if roofline and not args.eager:
+    if roofline:
         # north_star's target op: the backbone (stem) convs, each stamped in place the same
         # way in a re-captured step after the timed region (segment.py:19-31)
         res["roofline_backbone"] = [r for r in (stamp_op(trainer, ph, lab, args)
@@ -481,7 +485,8 @@ def main():
                                f"{args.size}x{args.size}", "global_batch": world * args.batch,
                    "image_size": args.size, "parallelism": f"dp{world}",
                    "input": "keypoints" if kp else ("heatmaps" if args.cin == 20 else "image"),
-                   "execution": "eager" if args.eager else "hip-graph"},
+                   "execution": "hip-graph" if args.graph else
+                                "eager C++ executor (isg_exec_ms2), two side streams"},
         "roofline": main_leg["roofline"], "loss": round(main_leg["loss"], 6),
     }
     if main_leg.get("roofline_backbone"):

@@ -427,8 +427,17 @@ class Trainer:
             self.target.copy_(target, non_blocking=True)
         self.step_count += 1
         self._throttle()
-        self._run(self.graphs if self.graphs else self._schedule(self.split))
+        self._run(self.graphs if self.graphs else self._eager_units())
         return self.loss_acc / self.logits.numel() if loss else None
+
+    def _eager_units(self):
+        """The uncaptured step's units, built once per (split, stamp_at) — a stamped list is
+        a compiled copy, not something to rebuild on every step."""
+        key = (self.split, self.stamp_at)
+        if getattr(self, "_eager_key", None) != key:
+            self._eager = self._schedule(self.split)
+            self._eager_key = key
+        return self._eager
 
     def _throttle(self):
         """Keep at most `max_inflight` steps queued on the GPU: the host waits for the end of
