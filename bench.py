@@ -341,14 +341,6 @@ def train_leg(args, dev, world, rank, keypoints, roofline, dp_plan=None):
     """Time args.steps captured train steps (after args.warmup) on one input form; the
     dominant op (per-op timing pass) is bracketed by timestamp launches inside every timed
     step when `roofline`. dp_plan: the data-parallel step structure (Trainer dp_plan)."""
-    prio = os.environ.get("ISG_MAIN_PRIO")  # round-6 measurement knob: the step's stream priority
-    if prio is not None:
-        with torch.cuda.stream(torch.cuda.Stream(device=dev, priority=int(prio))):
-            return _train_leg(args, dev, world, rank, keypoints, roofline, dp_plan)
-    return _train_leg(args, dev, world, rank, keypoints, roofline, dp_plan)
-
-
-def _train_leg(args, dev, world, rank, keypoints, roofline, dp_plan=None):
     from instancesegmentation_amd.data import device_batch
     from instancesegmentation_amd.model.segment import Segment
     from instancesegmentation_amd.train import Trainer
@@ -358,8 +350,7 @@ def _train_leg(args, dev, world, rank, keypoints, roofline, dp_plan=None):
     xs, mask = device_batch(args.batch, args.size, args.size, dev, seed=100 + rank, cin=args.cin,
                             keypoints=keypoints and args.cin == 20)
     in_shapes = [tuple(x.shape) for x in xs]
-    trainer = Trainer(model, args.batch, in_shapes, device=dev, dp_plan=dp_plan,
-                      fused_tail=False if os.environ.get("ISG_NO_FUSED_TAIL") else None)
+    trainer = Trainer(model, args.batch, in_shapes, device=dev, dp_plan=dp_plan)
     trainer.step(xs, mask)
     torch.cuda.synchronize()
 

@@ -539,12 +539,6 @@ int32_t isg_exec_ms(const void* ops, int32_t nops, void* const* table, isg_strea
 int32_t isg_exec_ms2(const void* ops, int32_t nops, void* const* table, isg_stream_t stream,
                      isg_stream_t side, isg_stream_t side2);
 
-/* A side stream for the executor whose kernels may occupy only `keep` of every 8 compute
- * units (CU mask: bit i set when i % 8 < keep; keep 8 = the whole chip), so the forked
- * weight gradients never take every CU from the input-gradient chain on the main stream.
- * *out receives the hipStream_t (release with hipStreamDestroy). */
-int32_t isg_side_stream_create(int32_t keep, isg_stream_t* out);
-
 /* sizeof() of the ABI structs and executor records (0 vtensor, 1 sinks, 2 conv record,
  * 3 wgrad record, 4 pool record, 5 tail, 6 tail_grad, 7 bn_update, 8 grad_final,
  * 9 bce record, 10 conv_geom, 11 bn, 12 vseg, 13 sink, 14 sum_rep record, 15 kp_stem,

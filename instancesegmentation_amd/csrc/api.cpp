@@ -445,13 +445,11 @@ int32_t isg_exec_ms2(const void* ops, int32_t nops, void* const* table, isg_stre
     alignas(16) char buf[8192];
     hipEvent_t ev_join = nullptr, ev_join2 = nullptr, *ev_forks = nullptr, *ev_done = nullptr;
     bool forked = false, forked2 = false;  // side-stream work outstanding since the last join
-    // weight gradients deferred per fork: 48 with two side streams and one backward
-    // part (4.415 -> 4.365 ms/step against 24; 36: 4.405, 64: 4.42, 96: 4.48 — r03y)
-    static const int batch = [] {  // (ISG_SIDE_BATCH: round-6 measurement knob)
-        const char* e = getenv("ISG_SIDE_BATCH");
-        const int b = e ? atoi(e) : 48;
-        return b < 1 ? 1 : b;
-    }();
+    // weight gradients deferred per fork. Round 6 (eager issue, fused step tail,
+    // profiles/r08e_ab_side_batch.txt): 16 -> 3.385 ms/step, 8: 3.377, 24: 3.407, 48: 3.67 —
+    // a batch of 48 held the first weight gradients until deep into the backward and then
+    // flooded the chain's kernels (round 3 had measured 48 best: 4.365 vs 4.415 at 24)
+    constexpr int batch = 16;
     // grouped 1x1 weight gradients in weight-gradient batches (4.04 -> 3.96
     // ms/step, 2 interleaved 200-step pairs)
     constexpr bool pwg_group_on = true;
@@ -656,22 +654,6 @@ int32_t isg_exec_ms(const void* ops, int32_t nops, void* const* table, isg_strea
 
 int32_t isg_exec(const void* ops, int32_t nops, void* const* table, isg_stream_t st) {
     return isg_exec_ms2(ops, nops, table, st, nullptr, nullptr);
-}
-
-int32_t isg_side_stream_create(int32_t keep, isg_stream_t* out) {
-    if (!out || keep < 1 || keep > 8) return isg_set_error(ISG_ERR_INVALID, "side stream: keep %d of 8", keep);
-    int dev = 0, cus = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
-        return isg_check_launch("side stream: CU count");
-    std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0u);
-    for (int i = 0; i < cus; ++i)
-        if (i % 8 < keep) mask[(size_t)i / 32] |= 1u << (i % 32);
-    hipStream_t s = nullptr;
-    if (hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()) != hipSuccess)
-        return isg_check_launch("side stream: hipExtStreamCreateWithCUMask");
-    *out = s;
-    return ISG_OK;
 }
 
 // sizes of the executor records, so the Python planner can verify its ctypes mirrors

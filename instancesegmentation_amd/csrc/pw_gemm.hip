@@ -1031,10 +1031,10 @@ int32_t isg_pw_gemm(const isg_conv_geom* g, const isg_vtensor* src, const float*
     // (round 3, after the single-segment prologue: the 48 -> 128 expansions and their
     // transposes, M = 128 rows over K = 48, on 32 x 64 tiles — kbench fwd 15.3 -> 14.8 us,
     // dgrad 18.4 -> 17.2 us against the chunked kernel)
-    static const bool wide_k = getenv("ISG_PWX_WIDEK") != nullptr;  // round-6 measurement knob
+    // (round 6, measured: the slab for K = 256 — bottle3_1's stacked 256 -> 176 pair at
+    // 32 x 32 tiles — step 3.654 -> 3.680 ms, 3.573 -> 3.595 eager: kept on the chunked kernel)
     const bool slab_pays = res || (!dgrad && a.P >= 65536) || (dgrad && a.M <= 64 && a.K <= 128) ||
-                           (!dgrad && a.M <= 64 && a.K <= 128) || (a.M <= 128 && a.K <= 64) ||
-                           (wide_k && a.K > 128);
+                           (!dgrad && a.M <= 64 && a.K <= 128) || (a.M <= 128 && a.K <= 64);
     if (slab_pays && wmode && pwx_src_ok(*src, a.HW) && a.P < ((int64_t)1 << 31)) {
         PwxArgs b{};
         b.src = a.src; b.out = a.out; b.w = w; b.rs = a.rs; b.cs = a.cs;

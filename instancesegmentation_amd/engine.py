@@ -678,10 +678,7 @@ def _join_exclusions(recs):
     count of excluded (later) side records goes into the header flags' upper bits
     (api.cpp OPF_JOIN); joins without recorded dependencies wait for everything."""
     order = []
-    off = os.environ.get("ISG_NO_JOIN_EXCL", "0") == "1"  # round-6 measurement knob
     for r in recs:
-        if r.flags & Record.OPF_JOIN and off:
-            continue
         if r.flags & Record.OPF_JOIN:
             r.flags &= (1 << Record.EXCL_SHIFT) - 1
             deps = getattr(r, "join_deps", None)

@@ -219,10 +219,6 @@ class Trainer:
         self.events = []
         self.split = None
         self.stamp_at = None  # (phase, index): OP_STAMP records around that op (stamp_times)
-        # steps allowed in flight before the host waits (_throttle); 0 = unbounded
-        self.max_inflight = int(os.environ.get("ISG_MAX_INFLIGHT", "0"))
-        self._inflight = []
-        self._pending_mark = None
         self.stamp_buf = torch.zeros(4, dtype=torch.int64, device=dev)  # isg_stamp's sums / max / min
         self.table[S_STAMP] = self.stamp_buf.data_ptr()
 
@@ -387,14 +383,6 @@ class Trainer:
         return self
 
     def _run(self, units):
-        try:
-            self._run_units(units)
-        finally:
-            if self._pending_mark is not None:  # the step's end on the main stream
-                self._pending_mark.record(torch.cuda.current_stream(self.device))
-                self._pending_mark = None
-
-    def _run_units(self, units):
         ev = None
         for u in units:
             if isinstance(u, torch.cuda.CUDAGraph):
@@ -426,7 +414,6 @@ class Trainer:
         if target is not None:
             self.target.copy_(target, non_blocking=True)
         self.step_count += 1
-        self._throttle()
         self._run(self.graphs if self.graphs else self._eager_units())
         return self.loss_acc / self.logits.numel() if loss else None
 
@@ -438,21 +425,6 @@ class Trainer:
             self._eager = self._schedule(self.split)
             self._eager_key = key
         return self._eager
-
-    def _throttle(self):
-        """Keep at most `max_inflight` steps queued on the GPU: the host waits for the end of
-        the step issued max_inflight steps ago before issuing this one. A host running many
-        steps ahead fills the hardware queues, and a full queue then holds the host at an op
-        of one stream while the other stream runs dry (head-of-line blocking)."""
-        n = self.max_inflight
-        if n <= 0:
-            return
-        evs = self._inflight
-        if len(evs) >= n:
-            evs.pop(0).synchronize()
-        e = torch.cuda.Event()
-        evs.append(e)
-        self._pending_mark = e
 
     def loss(self):
         return (self.loss_acc / self.logits.numel()).item()

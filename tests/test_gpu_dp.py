@@ -143,7 +143,7 @@ def test_train_loop_fit_two_ranks(tmp_path):
     assert d0 == 0.0 and d1 == 0.0
 
 
-def _nccl_world1_worker(rank, port, out):
+def _nccl_world1_worker(rank, port, graph, out):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     from instancesegmentation_amd.data import device_batch
@@ -168,15 +168,21 @@ def _nccl_world1_worker(rank, port, out):
     # the world-1 default plan (one graph, no exchange) first, without any process group
     m0 = Segment(20)
     m0.load_state_dict(init)
-    ref = run(Trainer(m0, n, shapes, device=dev).capture())
+    t0 = Trainer(m0, n, shapes, device=dev)
+    ref = run(t0.capture() if graph else t0)
     dist.init_process_group("nccl", rank=rank, world_size=1, device_id=dev)
     try:
         assert dist.get_backend() == "nccl"
         m1 = Segment(20)
         m1.load_state_dict(init)
-        tr = Trainer(m1, n, shapes, device=dev, dp_plan=True).capture()
-        assert tr.world == 1 and tr.sync.active and len(tr.graphs) >= 3
-        assert "coll1" in tr.graphs and "coll2" in tr.graphs
+        tr = Trainer(m1, n, shapes, device=dev, dp_plan=True)
+        assert tr.world == 1 and tr.sync.active and not tr.fused_tail
+        if graph:
+            tr.capture()
+            assert len(tr.graphs) >= 3 and "coll1" in tr.graphs and "coll2" in tr.graphs
+        else:
+            units = tr._schedule()
+            assert "coll1" in units and "coll2" in units
         got = run(tr)
         diffs = []
         for (g0, p0, b0, l0), (g1, p1, b1, l1) in zip(ref, got):
@@ -187,17 +193,20 @@ def _nccl_world1_worker(rank, port, out):
         dist.destroy_process_group()
 
 
-def test_dp_plan_over_rccl_at_world1_matches_default_plan():
+@pytest.mark.parametrize("graph", [True, False], ids=["graph", "eager"])
+def test_dp_plan_over_rccl_at_world1_matches_default_plan(graph):
     """RCCL (the "nccl" backend) on the one leased GPU: a world-size-1
     nccl process group in a fresh process drives the data-parallel step structure with REAL
     one-rank RCCL all-reduces — the three captured graphs, bucket 1 launched asynchronously
     on RCCL's stream while backward part 2 (the stem) runs, bucket 2, the wait, the running
     statistics in the exchange buffer — and two steps of it equal the world-1 default plan
     (one graph, no exchange) bit for bit: gradient, parameters after Adam, running
-    statistics (a one-rank SUM is the identity; the backward is deterministic)."""
+    statistics (a one-rank SUM is the identity; the backward is deterministic). Both with
+    the step captured into graphs (collectives between them) and issued eagerly; the
+    default plan it is compared with ends in the fused step tail (isg_step_tail)."""
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_nccl_world1_worker, args=(_free_port(), out), nprocs=1, join=True)
+    mp.spawn(_nccl_world1_worker, args=(_free_port(), graph, out), nprocs=1, join=True)
     for step, (dg, dp, db, dl) in enumerate(out[0], 1):
         print(f"step {step}: elements differing (grad, params, running stats) {dg}, {dp}, {db}; "
               f"loss diff {dl:.2e}")
