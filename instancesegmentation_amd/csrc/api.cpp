@@ -475,11 +475,13 @@ int32_t isg_exec_ms2(const void* ops, int32_t nops, void* const* table, isg_stre
         // a batch of weight gradients only (independent accumulations into the replica
         // buffers) is dealt over both side streams: their grids (128-512 workgroups) leave
         // most of the chip idle one at a time; anything else keeps its order on stream 0
+        // (the step counter too: it touches nothing else — as a non-spread batch at the head
+        // of the backward it had kept every later batch off side 2, round 6)
         bool spread = side2 != nullptr;
         for (auto& op : bt.ops)
             spread = spread && (op.first == OP_CONV_WGRAD || op.first == OP_KP_STEM_WGRAD ||
                                 op.first == OP_HEAD_FOLD || op.first == OP_GRAD_FINAL ||
-                                op.first == OP_BN_UPDATE);
+                                op.first == OP_BN_UPDATE || op.first == OP_STEP_INC);
         // a batch behind a side-only one (the gradient finalisation lists behind the replica
         // fold at ISG_SIDE_CLOSE=1) may read what that one writes: it stays on `side`, in order
         if (spread && side_serial) spread = false;

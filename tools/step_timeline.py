@@ -20,7 +20,7 @@ def main():
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), int(r["Queue_Id"]),
                          n.split("(")[0].strip(), int(r["Grid_Size_X"]) // max(1, int(r["Workgroup_Size_X"]))))
     rows.sort()
-    adam = [i for i, r in enumerate(rows) if "adam" in r[3]]
+    adam = [i for i, r in enumerate(rows) if "adam" in r[3] or "step_tail" in r[3]]
     a, b = adam[-k - 1] + 1, adam[-k] + 1
     step = rows[a:b]
     t0 = step[0][0]
