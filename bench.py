@@ -151,10 +151,13 @@ BACKBONE_OPS = [("fwd", "init_conv.layer2"), ("bwd", "dx_init_conv.layer2"),
                 ("bwd", "dw_init_conv.layer1")]
 
 
-def stamp_op(trainer, phase, label, args):
-    """The roofline of one recorded op timed in place: the step re-captured with OP_STAMP
-    records around it (Trainer.stamp_at), args.steps replays after 2 warm-up replays. A
-    side-stream op (a weight gradient) is moved onto the main stream for its bracket."""
+def stamp_op(trainer, phase, label, args, rows=None):
+    """The roofline of one recorded op timed in place: the step re-run with OP_STAMP records
+    around it (Trainer.stamp_at), args.steps steps after 2 warm-up steps; a side-stream op (a
+    weight gradient) is moved onto the main stream for its bracket. In place, the op shares
+    the chip with whatever the side stream runs beside it (the stem's layer-2 input and
+    weight gradients overlap each other); `rows` (the per-op pass: the op alone, 20 launches
+    in a graph) adds the kernel's own time as `alone_ms` / `alone_frac`."""
     ol = trainer.plan.fwd if phase == "fwd" else trainer.plan.bwd
     idx = next((i for i, r in enumerate(ol.recs) if r.label == label), None)
     if idx is None:
@@ -177,6 +180,11 @@ def stamp_op(trainer, phase, label, args):
     r["avg_ms"] = round(ms, 4)
     r["gflop"] = round(rec.flops / 1e9, 4)
     r["traffic"] = pmc_traffic(label, args)
+    alone = next((x["ms"] for x in rows or [] if x["phase"] == phase and x["label"] == label), None)
+    if alone:
+        a = roofline_of(rec, alone)
+        r["alone_ms"] = round(alone, 4)
+        r["alone_frac"] = a["frac"]
     return r
 
 
@@ -356,6 +364,7 @@ def train_leg(args, dev, world, rank, keypoints, roofline, dp_plan=None):
 
     # ---- dominant op (per-op timing pass, untimed) ----------------------------------
     dom = None
+    rows = None
     if roofline and args.dominant:
         ph, lab = args.dominant.split(":", 1)
         ol = trainer.plan.fwd if ph == "fwd" else trainer.plan.bwd
@@ -426,7 +435,7 @@ def train_leg(args, dev, world, rank, keypoints, roofline, dp_plan=None):
     if roofline:
         # north_star's target op: the backbone (stem) convs, each stamped in place the same
         # way in a re-captured step after the timed region (segment.py:19-31)
-        res["roofline_backbone"] = [r for r in (stamp_op(trainer, ph, lab, args)
+        res["roofline_backbone"] = [r for r in (stamp_op(trainer, ph, lab, args, rows)
                                                 for ph, lab in BACKBONE_OPS) if r is not None]
     del trainer
     torch.cuda.synchronize()
@@ -486,10 +495,13 @@ def main():
         # stem's 5x5 s2 convs), each op stamped in place; aggregate = their flops / time
         tot_f = sum(r["gflop"] for r in bb)
         tot_ms = sum(r["avg_ms"] for r in bb)
+        agg = lambda ms: round(tot_f * 1e9 / (ms * 1e-3) / 1e12 / PEAK_F32_MFMA_TFLOPS, 4)
         out["roofline_backbone"] = {
-            "ops": bb, "aggregate_frac": round(tot_f * 1e9 / (tot_ms * 1e-3) / 1e12 /
-                                               PEAK_F32_MFMA_TFLOPS, 4),
-            "unit": "fraction of the fp32 MFMA peak (157.3 TFLOP/s)"}
+            "ops": bb, "aggregate_frac": agg(tot_ms),
+            "aggregate_frac_alone": agg(sum(r["alone_ms"] for r in bb))
+            if all("alone_ms" in r for r in bb) else None,
+            "unit": "fraction of the fp32 MFMA peak (157.3 TFLOP/s); in place (stamped inside "
+                    "the step) and alone (the per-op pass)"}
     if dense_leg is not None:
         out["dense_heatmaps"] = {"value": round(dense_leg["value"], 3),
                                  "ms_per_step": round(dense_leg["ms_per_step"], 3),

@@ -309,8 +309,11 @@ _SIDE2 = {}
 
 def side_stream2_ptr(device=None):
     """The executor's second side stream (batches of weight gradients are dealt over both),
-    or None when disabled (ISG_NO_SIDE2=1, under its own parity test)."""
-    if os.environ.get("ISG_NO_SIDE2", "0") == "1":
+    or None — the default since round 6: with the eager executor and the fused step tail a
+    second side stream made the step slower, 3.36 -> 3.46 ms (profiles/r08g_ab_side2.txt),
+    its extra weight gradients in flight taking CUs from the input-gradient chain.
+    ISG_SIDE2=1 enables it (under its own parity test)."""
+    if os.environ.get("ISG_SIDE2", "0") != "1":
         return None
     d = torch.cuda.current_device() if device is None else torch.device(device).index
     if d is None:

@@ -257,14 +257,15 @@ def test_loaded_adam_hyperparameters_reach_the_captured_step():
 def test_side_close_orders_after_second_side_stream(monkeypatch):
     """ADVICE r03 (api.cpp flush): with two gradient buckets and bucket 1's replica fold +
     gradient finalisation on the side stream (ISG_SIDE_CLOSE=1), that fold must run after
-    the weight gradients dealt onto the second side stream. The gradients must equal those
-    of the same plan with the second side stream off (ISG_NO_SIDE2=1) and of the default
-    plan; a dropped weight-gradient contribution would show up as an O(1) relative error."""
+    the weight gradients dealt onto the second side stream (ISG_SIDE2=1). The gradients must
+    equal those of the same plan with one side stream (the default) and of the default plan,
+    also with two side streams; a dropped weight-gradient contribution would show up as an
+    O(1) relative error."""
     fx = SegmentFixture("segment20_n2_128.npz")
     xs, y = _inputs(fx.x), torch.from_numpy(fx.mask).to(DEV)
 
     def grads(env):
-        for k in ("ISG_BUCKETS", "ISG_SIDE_CLOSE", "ISG_NO_SIDE2"):
+        for k in ("ISG_BUCKETS", "ISG_SIDE_CLOSE", "ISG_SIDE2"):
             monkeypatch.delenv(k, raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)
@@ -282,8 +283,8 @@ def test_side_close_orders_after_second_side_stream(monkeypatch):
 
     base = grads({})[0]
     scale = base.abs().max().item()
-    for env in ({"ISG_BUCKETS": "2", "ISG_SIDE_CLOSE": "1"},
-                {"ISG_BUCKETS": "2", "ISG_SIDE_CLOSE": "1", "ISG_NO_SIDE2": "1"}, {}):
+    for env in ({"ISG_BUCKETS": "2", "ISG_SIDE_CLOSE": "1", "ISG_SIDE2": "1"},
+                {"ISG_BUCKETS": "2", "ISG_SIDE_CLOSE": "1"}, {"ISG_SIDE2": "1"}, {}):
         for i, g in enumerate(grads(env)):
             err = (g - base).abs().max().item()
             print(env, i, f"max abs diff {err:.2e} (scale {scale:.2e})")
