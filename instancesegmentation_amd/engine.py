@@ -753,6 +753,19 @@ def _fork_late_wgrads(recs, late):
             recs[i], recs[i + 1] = b, a
 
 
+def _trailing_on_main(recs):
+    """Side records after the backward's last main-stream record (the stem's layer-1 weight
+    gradients, behind the last input gradient) overlap nothing on the main stream, which then
+    only waits at the final join, while on the side stream they queue behind every weight
+    gradient forked before them: run them on the main stream instead (round 6 kernel trace:
+    the main stream idled 161 us before the step tail)."""
+    i = len(recs)
+    while i > 0 and recs[i - 1].flags & Record.OPF_SIDE:
+        i -= 1
+    for r in recs[i:]:
+        r.flags &= ~(Record.OPF_SIDE | Record.OPF_FORK_NOW)
+
+
 def _fold_tails(g):
     """Residual tails folded into their first consumer: a tail
     out = act(BN(y) + x) (segment.py:75-77, 107-109, 259: BatchNorm'd raw conv output plus a
@@ -1662,6 +1675,7 @@ class Plan:
             if r.kind in (L.OP_CONV_WGRAD, L.OP_KP_STEM_WGRAD, L.OP_HEAD_FOLD):
                 r.flags |= Record.OPF_SIDE  # nothing later in the list reads a weight gradient
         _fork_late_wgrads(body.recs, self._late_prefix(g))
+        _trailing_on_main(body.recs)
         self.din_written = [isinstance(v, Value) and v.grad and
                             bool(gs.inited.get(id(v.segs[0].buf))) for v in ins]
         # finalisation of BN / PReLU / conv-bias-before-BN gradients: (module, item)

@@ -196,7 +196,11 @@ def test_keypoint_stem_plan_and_synthetic_keypoints():
     kinds = [r.kind for r in p.fwd.recs]
     assert kinds.count(L.OP_KP_POOL) == 1 and kinds.count(L.OP_KP_STEM_FWD) == 1
     bk = [r for r in p.bwd.recs if r.kind == L.OP_KP_STEM_WGRAD]
-    assert len(bk) == 1 and bk[0].flags & 1  # forked onto the side stream like any wgrad
+    # the last records of the backward: on the main stream (engine._trailing_on_main), no
+    # side record after the last main-stream record
+    assert len(bk) == 1 and not bk[0].flags & 1
+    last_main = max(i for i, r in enumerate(p.bwd.recs) if not r.flags & 1)
+    assert p.bwd.recs.index(bk[0]) < last_main or all(r.flags & 1 == 0 for r in p.bwd.recs[last_main:])
     conv = next(r for r in p.fwd.recs if r.label == "init_conv.layer1")
     g = L.ConvRec.from_buffer_copy(conv.body).g
     assert (g.Ci, g.w_ci) == (3, 20)
