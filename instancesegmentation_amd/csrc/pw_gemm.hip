@@ -77,29 +77,12 @@ __global__ __launch_bounds__(kThreads) void pw_kernel(PwArgs a) {
 
     for (int c = tid; c < a.K; c += kThreads) tab[c] = ch_table_entry(a.src, c, a.HW);
     for (int r = tid; r < BM; r += kThreads) {
-        const int m = m0 + r;
         RowInfo q = {};
         q.mode = -1;
-        if (r < Mb) {
-            const int s = sink_of(a.out, m);
-            const isg_sink& k = s == 2 ? a.out.s[2] : (s == 1 ? a.out.s[1] : a.out.s[0]);
-            const int cl = m - k.c0;
-            q.p = k.p ? k.p + (int64_t)cl * a.HW : nullptr;
-            q.y = k.y ? k.y + (int64_t)cl * a.HW : nullptr;
-            q.ns = (int)k.n_stride;
-            q.yns = (int)k.y_n_stride;
-            q.mode = k.mode;
-            q.act = k.act;
-            q.bias = k.bias ? k.bias[cl] : 0.f;
-            q.f = SinkCoef{0.f, 1.f, 0.f, 0.f};
-            if (k.mode == ISG_SINK_ACTBWD) {
-                if (k.bn.stats || !k.bn.train) {
-                    const ChanCoef f = k.bn.coef ? fwd_coef(k.bn, nullptr, cl)
-                                                 : coef_slow(k.bn, nullptr, cl, 0);
-                    q.f.mean = f.c0; q.f.scale = f.c1; q.f.beta = f.c2;
-                }
-                q.f.slope = k.slope ? k.slope[cl] : 0.f;
-            }
+        if (r < Mb) {  // (sink_row: the lane's sink read at a constant index)
+            const SinkRow w = sink_row(a.out, m0 + r, a.HW);
+            q.p = w.p; q.y = w.y; q.ns = (int)w.ns; q.yns = (int)w.yns;
+            q.mode = w.mode; q.act = w.act; q.bias = w.bias; q.f = w.f;
         }
         ri[r] = q;
     }
@@ -240,25 +223,7 @@ __global__ __launch_bounds__(kThreads) void pw_kernel(PwArgs a) {
 #pragma unroll
             for (int j = 0; j < 3; ++j)
                 red[0][j][rl] = ((red[0][j][rl] + red[1][j][rl]) + red[2][j][rl]) + red[3][j][rl];
-            const int m = m0 + rl;
-            const int s = sink_of(a.out, m);
-            const isg_sink& k = s == 2 ? a.out.s[2] : (s == 1 ? a.out.s[1] : a.out.s[0]);
-            const int cl = m - k.c0;
-            if (k.mode == ISG_SINK_STORE || k.mode == ISG_SINK_ACCUM) {
-                if (k.stats) {
-                    double* sp = rep_ptr(k.stats, 4 * k.C);
-                    atomicAdd(&sp[cl], (double)red[0][0][rl]);
-                    atomicAdd(&sp[k.C + cl], (double)red[0][1][rl]);
-                }
-            } else if (k.mode == ISG_SINK_ACTBWD) {
-                if (k.bn.stats) {
-                    double* sp = rep_ptr(k.bn.stats, 4 * k.C);
-                    atomicAdd(&sp[2 * k.C + cl], (double)red[0][0][rl]);
-                    atomicAdd(&sp[3 * k.C + cl], (double)red[0][1][rl]);
-                }
-                if (k.slope_grad && k.act == ISG_ACT_PRELU)
-                    atomicAdd(&rep_ptr(k.slope_grad, k.C)[cl], (double)red[0][2][rl]);
-            }
+            sink_row_flush(a.out, m0 + rl, red[0][0][rl], red[0][1][rl], red[0][2][rl]);
         }
     }
 }
@@ -615,8 +580,102 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
         __syncthreads();
     }
     STAMP(5);
+    // one sink: its mode / activation / bases are lane-invariant (scalar), only the rows'
+    // coefficients and biases come from LDS — every row's read issued before the first use.
+    // (The generic loop below reads the whole row record per row behind a branch on its
+    // mode: a chain of dependent LDS round trips per element.) Same arithmetic per element.
+    if constexpr (SINK1) {
+        const SinkLite& k0 = ks.s0;
+        const int mode = k0.mode, act = k0.act;
+        const bool live = mode == ISG_SINK_STORE || mode == ISG_SINK_ACCUM || mode == ISG_SINK_ACTBWD;
+#pragma unroll
+        for (int i = 0; i < TPW; ++i) {
+            const int t = wave + 4 * i;
+            if (t >= nt || !live) continue;  // wave-uniform
+            const int rt = t / CT, ct = t % CT;
+            if (rt * 16 >= Mb) continue;
+            const int64_t pe = p0 + ct * 16 + pl;
+            const bool pve = pe < a.P;
+            const int ne = pve ? (int)((uint32_t)pe / (uint32_t)a.HW) : 0;
+            const int pixe = pve ? (int)pe - ne * a.HW : 0;
+            SinkCoef fr[4];
+            float br[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const RowInfo& qi = ri[min(rt * 16 + kk * 4 + r, Mb - 1)];
+                fr[r] = qi.f;
+                br[r] = qi.bias;
+            }
+            float s0[4], s1[4], s2[4], s3[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                s0[r] = s1[r] = s2[r] = s3[r] = 0.f;
+                const int rl = rt * 16 + kk * 4 + r;
+                if (!pve || rl >= Mb) continue;
+                float v = acc[i][r];
+                const int64_t cl = rl + m0 - k0.c0;
+                const int64_t off = cl * a.HW + (int64_t)ne * k0.ns + pixe;
+                if (mode == ISG_SINK_STORE) {
+                    v += br[r];
+                    gst(k0.p, off, v);
+                    s0[r] = v;
+                    s1[r] = v * v;
+                } else if (mode == ISG_SINK_ACCUM) {
+                    gst(k0.p, off, pre[i][r] + v);
+                    s0[r] = v;
+                    s1[r] = v * v;
+                } else {
+                    const SinkCoef& f = fr[r];
+                    const float y = pre[i][r];
+                    float z = (y - f.mean) * f.scale + f.beta;
+                    ChanCoef k2 = {0.f, 1.f, 0.f, 0.f};
+                    if constexpr (RES) {  // residual form: + old gradient, + residual term
+                        v = pro[i][r] + v;
+                        float rv = prr[i][r];
+                        if (rbn_out) {  // the residual's own BatchNorm (two-BN tail)
+                            k2 = tabK2[rl];
+                            rv = (rv - k2.c0) * k2.c1 + k2.c2;
+                        }
+                        z = z + rv;
+                    }
+                    float gv = v;
+                    if (act == ISG_ACT_RELU) {
+                        gv = z > 0.f ? v : 0.f;
+                    } else if (act == ISG_ACT_PRELU) {
+                        gv = z > 0.f ? v : v * f.slope;
+                        s2[r] = z > 0.f ? 0.f : z * v;
+                    }
+                    gst(k0.p, off, gv);
+                    if constexpr (RES) {
+                        if (k0.p2)
+                            gst(k0.p2, cl * a.HW + (int64_t)ne * k0.p2ns + pixe, k0.p2acc ? pp2[i][r] + gv : gv);
+                        if (rbn_out) s3[r] = gv * (prr[i][r] - k2.c0);  // centred on the residual's mean
+                    }
+                    s0[r] = gv;
+                    s1[r] = gv * (y - f.mean);
+                }
+            }
+            if (need_red) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float t0 = row16_sum(s0[r]);
+                    const float t1 = row16_sum(s1[r]);
+                    const float t2 = row16_sum(s2[r]);
+                    const float t3 = rbn_out ? row16_sum(s3[r]) : 0.f;
+                    const int rl = rt * 16 + kk * 4 + r;
+                    if (pl == 0 && rl < Mb) {
+                        red[wave][0][rl] += t0;
+                        red[wave][1][rl] += t1;
+                        red[wave][2][rl] += t2;
+                        red[wave][3][rl] += t3;
+                    }
+                }
+            }
+        }
+    }
 #pragma unroll
     for (int i = 0; i < TPW; ++i) {
+        if constexpr (SINK1) break;
         const int t = wave + 4 * i;
         if (t >= nt) continue;  // wave-uniform
         const int rt = t / CT, ct = t % CT;
@@ -698,7 +757,8 @@ __global__ __launch_bounds__(kThreads) void pwx_kernel(PwxArgs a) {
 #pragma unroll
             for (int j = 0; j < 4; ++j)
                 red[0][j][rl] = ((red[0][j][rl] + red[1][j][rl]) + red[2][j][rl]) + red[3][j][rl];
-            sink_row_flush(a.out, m0 + rl, red[0][0][rl], red[0][1][rl], red[0][2][rl]);
+            if constexpr (SINK1) sink_row_flush1(a.out.s[0], m0 + rl, red[0][0][rl], red[0][1][rl], red[0][2][rl]);
+            else sink_row_flush(a.out, m0 + rl, red[0][0][rl], red[0][1][rl], red[0][2][rl]);
             if (rbn_out && a.out.s[0].rbn.stats) {  // the residual BatchNorm's backward sums
                 const isg_sink& k = a.out.s[0];
                 double* sp = rep_ptr(k.rbn.stats, 4 * k.rbn.C);

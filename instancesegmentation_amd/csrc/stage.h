@@ -216,10 +216,10 @@ struct SinkRow {
     SinkCoef f;
 };
 
-ISG_DEV SinkRow sink_row(const isg_sinks& sk, int m, int64_t hw) {
+// one sink's row record; `k` must be a kernel-argument sink at a constant index (its fields
+// are then scalar loads — see sink_row)
+ISG_DEV SinkRow sink_row1(const isg_sink& k, int m, int64_t hw) {
     SinkRow q = {};
-    const int s = sink_of(sk, m);
-    const isg_sink& k = s == 2 ? sk.s[2] : (s == 1 ? sk.s[1] : sk.s[0]);
     const int cl = m - k.c0;
     q.p = k.p ? k.p + (int64_t)cl * hw : nullptr;
     q.y = k.y ? k.y + (int64_t)cl * hw : nullptr;
@@ -237,6 +237,18 @@ ISG_DEV SinkRow sink_row(const isg_sinks& sk, int m, int64_t hw) {
         q.f.slope = k.slope ? k.slope[cl] : 0.f;
     }
     return q;
+}
+// Row m's record: the lane's sink chosen first, then each branch reads ITS sink at a
+// constant index (a per-lane selected struct made hipcc load every field per lane from
+// kernel-argument memory, each load waited for before the next).
+ISG_DEV SinkRow sink_row(const isg_sinks& sk, int m, int64_t hw) {
+    const int ns = __builtin_amdgcn_readfirstlane(sk.nsink);
+    int s = 0;  // sink_of's rule
+    if (ns > 1 && m >= __builtin_amdgcn_readfirstlane(sk.s[1].c0)) s = 1;
+    if (ns > 2 && m >= __builtin_amdgcn_readfirstlane(sk.s[2].c0)) s = 2;
+    if (s == 0) return sink_row1(sk.s[0], m, hw);
+    if (s == 1) return sink_row1(sk.s[1], m, hw);
+    return sink_row1(sk.s[2], m, hw);
 }
 
 // Apply row q's sink to value v at flat offset (n, pix); returns the values to reduce
@@ -574,23 +586,71 @@ ISG_DEV SinkRow sink_finish(const SkSel sk, int m, int64_t hw, const SinkLoad& l
     return q;
 }
 
-// Fold row m's block-reduced sums into the sink's replicated fp64 accumulators.
-ISG_DEV void sink_row_flush(const isg_sinks& sk, int m, float r0, float r1, float r2) {
-    const int s = sink_of(sk, m);
-    const isg_sink& k = s == 2 ? sk.s[2] : (s == 1 ? sk.s[1] : sk.s[0]);
-    const int cl = m - k.c0;
-    if (k.mode == ISG_SINK_STORE || k.mode == ISG_SINK_ACCUM) {
-        if (k.stats) {
-            double* sp = rep_ptr(k.stats, 4 * k.C);
+// sink_row_flush for a launch with ONE sink (k = sinks.s[0]): its fields are scalar
+// kernel-argument loads. (sink_row_flush selects the sink per lane, which hipcc turns into
+// per-lane global loads of kernel-argument fields, each waited for before the next: a
+// serial chain of round trips at the very end of every 1x1 launch.)
+ISG_DEV void sink_row_flush1(const isg_sink& k, int m, float r0, float r1, float r2) {
+    const int cl = m - sgpr_i(k.c0);
+    const int C = sgpr_i(k.C), mode = sgpr_i(k.mode);
+    if (mode == ISG_SINK_STORE || mode == ISG_SINK_ACCUM) {
+        double* const st = sgpr_p(k.stats);
+        if (st) {
+            double* sp = rep_ptr(st, 4 * C);
             atomicAdd(&sp[cl], (double)r0);
-            atomicAdd(&sp[k.C + cl], (double)r1);
+            atomicAdd(&sp[C + cl], (double)r1);
         }
-    } else if (k.mode == ISG_SINK_ACTBWD) {
-        if (k.bn.stats) {
-            double* sp = rep_ptr(k.bn.stats, 4 * k.C);
-            atomicAdd(&sp[2 * k.C + cl], (double)r0);
-            atomicAdd(&sp[3 * k.C + cl], (double)r1);
+    } else if (mode == ISG_SINK_ACTBWD) {
+        double* const st = sgpr_p(k.bn.stats);
+        if (st) {
+            double* sp = rep_ptr(st, 4 * C);
+            atomicAdd(&sp[2 * C + cl], (double)r0);
+            atomicAdd(&sp[3 * C + cl], (double)r1);
         }
-        if (k.slope_grad && k.act == ISG_ACT_PRELU) atomicAdd(&rep_ptr(k.slope_grad, k.C)[cl], (double)r2);
+        double* const sg = sgpr_p(k.slope_grad);
+        if (sg && sgpr_i(k.act) == ISG_ACT_PRELU) atomicAdd(&rep_ptr(sg, C)[cl], (double)r2);
+    }
+}
+
+// Fold row m's block-reduced sums into the sink's replicated fp64 accumulators. The three
+// sinks' fields are made scalars first and the lane's sink selected among them (v_cndmask):
+// selecting the kernel-argument struct per lane made hipcc load every field per lane from
+// kernel-argument memory, one waited global load after another (see sgpr_i).
+struct FlushLite {
+    double *st, *bst, *sg;
+    int C, mode, act, c0;
+};
+ISG_DEV FlushLite flush_lite(const isg_sink& k) {
+    FlushLite f;
+    f.st = sgpr_p(k.stats); f.bst = sgpr_p(k.bn.stats); f.sg = sgpr_p(k.slope_grad);
+    f.C = sgpr_i(k.C); f.mode = sgpr_i(k.mode); f.act = sgpr_i(k.act); f.c0 = sgpr_i(k.c0);
+    return f;
+}
+ISG_DEV void sink_row_flush(const isg_sinks& sk, int m, float r0, float r1, float r2) {
+    const int ns = sgpr_i(sk.nsink);
+    const FlushLite f0 = flush_lite(sk.s[0]), f1 = flush_lite(sk.s[1]), f2 = flush_lite(sk.s[2]);
+    int s = 0;  // sink_of's rule
+    if (ns > 1 && m >= f1.c0) s = 1;
+    if (ns > 2 && m >= f2.c0) s = 2;
+#define ISG_FSEL(f) (s == 2 ? f2.f : (s == 1 ? f1.f : f0.f))
+    double* const st = ISG_FSEL(st);
+    double* const bst = ISG_FSEL(bst);
+    double* const sg = ISG_FSEL(sg);
+    const int C = ISG_FSEL(C), mode = ISG_FSEL(mode), act = ISG_FSEL(act);
+    const int cl = m - ISG_FSEL(c0);
+#undef ISG_FSEL
+    if (mode == ISG_SINK_STORE || mode == ISG_SINK_ACCUM) {
+        if (st) {
+            double* sp = rep_ptr(st, 4 * C);
+            atomicAdd(&sp[cl], (double)r0);
+            atomicAdd(&sp[C + cl], (double)r1);
+        }
+    } else if (mode == ISG_SINK_ACTBWD) {
+        if (bst) {
+            double* sp = rep_ptr(bst, 4 * C);
+            atomicAdd(&sp[2 * C + cl], (double)r0);
+            atomicAdd(&sp[3 * C + cl], (double)r1);
+        }
+        if (sg && act == ISG_ACT_PRELU) atomicAdd(&rep_ptr(sg, C)[cl], (double)r2);
     }
 }
