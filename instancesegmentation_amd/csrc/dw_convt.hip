@@ -570,6 +570,22 @@ __global__ __launch_bounds__(kThreads) void dw_bwd_tile_kernel(DwBwdArgs b) {
         const bool okx = rr < RH && jy >= 0 && jy < H && jx >= 0 && jx < W;
         xr[u] = xp[okx ? (int64_t)jy * W + jx : 0];
     }
+    // the sink's operand of this lane's 4 outputs (ACTBWD: the saved forward output; ACCUM:
+    // the old value) in the same round trip as the tiles, not behind the compute
+    typedef f32x4 __attribute__((address_space(1)))* g4p;
+    typedef const f32x4 __attribute__((address_space(1)))* gc4p;
+    const int ty = threadIdx.x >> 4, tq = threadIdx.x & 15;
+    const int oy = oy0 + ty, ox = ox0 + 4 * tq;
+    const bool oin = oy < H && ox < W;
+    const isg_sink& o = a.out;
+    const int omode = o.mode;
+    // (branch-free: a load behind a branch drains every load in flight at the join; a mode
+    // without an operand reads the weights' first quad instead and never uses it)
+    const bool has_op = omode == ISG_SINK_ACTBWD || omode == ISG_SINK_ACCUM;
+    const int64_t opix = has_op ? (int64_t)c * hw + (int64_t)(oin ? oy : 0) * W + (oin ? ox : 0) : 0;
+    const float* const osrc = omode == ISG_SINK_ACTBWD ? o.y + (int64_t)n * o.y_n_stride
+                              : (omode == ISG_SINK_ACCUM ? o.p + (int64_t)n * o.n_stride : a.w);
+    const f32x4 opre = *(gc4p)((gcfloat_p)osrc + opix);
     const ChanCoef kd = seg_coef(sd, c);
     const ChanCoef kx = seg_coef(sx, c);
     const Sink1 f = sink1_coef(a.out, c);
@@ -587,7 +603,6 @@ __global__ __launch_bounds__(kThreads) void dw_bwd_tile_kernel(DwBwdArgs b) {
         Xs[rr * kDtMaxC + cc] = okx ? seg_xform(sx, kx, xr[u], 0.f) : 0.f;
     }
     __syncthreads();
-    const int ty = threadIdx.x >> 4, tq = threadIdx.x & 15;
     // ---- input gradient (dw_tile_kernel<true>'s arithmetic)
     const float* wc = a.w + c * KK;
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
@@ -625,15 +640,12 @@ __global__ __launch_bounds__(kThreads) void dw_bwd_tile_kernel(DwBwdArgs b) {
             red[3 + kh * KW_ + kw] = v;
         }
     // ---- dx through the sink: 16-B accesses, 4 outputs
-    const int oy = oy0 + ty, ox = ox0 + 4 * tq;
-    if (oy < H && ox < W) {
-        const isg_sink& o = a.out;
+    if (oin) {
         const int64_t off = (int64_t)n * o.n_stride + (int64_t)c * hw + (int64_t)oy * W + ox;
-        typedef f32x4 __attribute__((address_space(1)))* g4p;
         if (o.mode == ISG_SINK_STORE || o.mode == ISG_SINK_ACCUM) {
             f32x4 v = {acc[0], acc[1], acc[2], acc[3]};
             if (o.mode == ISG_SINK_STORE && o.bias) v += o.bias[c];
-            if (o.mode == ISG_SINK_ACCUM) v += *(g4p)((gfloat_p)o.p + off);
+            if (o.mode == ISG_SINK_ACCUM) v += opre;
             else {
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
@@ -650,8 +662,7 @@ __global__ __launch_bounds__(kThreads) void dw_bwd_tile_kernel(DwBwdArgs b) {
             }
             *(g4p)((gfloat_p)o.p + off) = v;
         } else if (o.mode == ISG_SINK_ACTBWD) {
-            const f32x4 y4 = *(const f32x4 __attribute__((address_space(1)))*)((gcfloat_p)o.y +
-                              (int64_t)n * o.y_n_stride + (int64_t)c * hw + (int64_t)oy * W + ox);
+            const f32x4 y4 = opre;
             f32x4 g4;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {

@@ -885,8 +885,17 @@ struct ThinPwArgs {
 
 // gf32x4_p: common.h
 
-ISG_DEV void sink_row_apply4(const SinkRow& q, int n, int64_t pix, f32x4 v, float& s0, float& s1,
-                             float& s2) {
+// the row's sink operand (ACTBWD: the saved forward output, ACCUM: the old value), loaded
+// branch-free before the compute (`any`: a valid address standing in for modes without one)
+ISG_DEV f32x4 sink_operand4(const SinkRow& q, int n, int64_t pix, bool pv, const float* any) {
+    const bool ab = q.mode == ISG_SINK_ACTBWD, ac = q.mode == ISG_SINK_ACCUM;
+    const float* src = ab ? q.y : (ac ? q.p : any);
+    const int64_t off = (ab || ac) && pv ? (int64_t)n * (ab ? q.yns : q.ns) + pix : 0;
+    return gld4(src, off);
+}
+
+ISG_DEV void sink_row_apply4(const SinkRow& q, int n, int64_t pix, f32x4 v, f32x4 opnd, float& s0,
+                             float& s1, float& s2) {
     const int64_t off = (int64_t)n * q.ns + pix;
     s0 = s1 = s2 = 0.f;
     if (q.mode == ISG_SINK_STORE) {
@@ -895,12 +904,12 @@ ISG_DEV void sink_row_apply4(const SinkRow& q, int n, int64_t pix, f32x4 v, floa
         s0 = (v[0] + v[1]) + (v[2] + v[3]);
         s1 = (v[0] * v[0] + v[1] * v[1]) + (v[2] * v[2] + v[3] * v[3]);
     } else if (q.mode == ISG_SINK_ACCUM) {
-        const f32x4 o = gld4(q.p, off);
+        const f32x4 o = opnd;
         *(gf32x4_p)((gfloat_p)q.p + off) = o + v;
         s0 = (v[0] + v[1]) + (v[2] + v[3]);
         s1 = (v[0] * v[0] + v[1] * v[1]) + (v[2] * v[2] + v[3] * v[3]);
     } else if (q.mode == ISG_SINK_ACTBWD) {
-        const f32x4 y = gld4(q.y, (int64_t)n * q.yns + pix);
+        const f32x4 y = opnd;
         f32x4 g;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -924,7 +933,9 @@ ISG_DEV void sink_row_apply4(const SinkRow& q, int n, int64_t pix, f32x4 v, floa
 // meet in LDS, so a launch adds (quads / 64 / kThinWaves) atomics per statistics address —
 // at 4 replicas the one-wave form queued 512 atomics on each address (+10 us per op)
 constexpr int kThinWaves = 4;
-template <int K, int M>
+// PRE: some sink reads an operand (ACTBWD / ACCUM), prefetched with the activations (its
+// registers exist only in these instantiations)
+template <int K, int M, bool PRE>
 __global__ __launch_bounds__(64 * kThinWaves) void thin_pw_kernel(ThinPwArgs a) {
     constexpr int M4 = M / 4;
     __shared__ f32x4 wl[K * M4];  // [k][m/4]
@@ -954,6 +965,12 @@ __global__ __launch_bounds__(64 * kThinWaves) void thin_pw_kernel(ThinPwArgs a) 
         raw[k] = gld4(t.p, (int64_t)n * t.ns + pix);
         ry[k] = gld4(t.y, (int64_t)n * yns + pix);
     }
+    // the sinks' operands in the same round trip (they were loaded after the compute, one
+    // row at a time between the rows' reductions)
+    f32x4 opnd[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m)
+        opnd[m] = PRE ? sink_operand4(ri[m], n, pix, pv, a.w) : f32x4{0.f, 0.f, 0.f, 0.f};
     f32x4 acc[M];
 #pragma unroll
     for (int m = 0; m < M; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -974,7 +991,7 @@ __global__ __launch_bounds__(64 * kThinWaves) void thin_pw_kernel(ThinPwArgs a) 
 #pragma unroll
     for (int m = 0; m < M; ++m) {
         float s0 = 0.f, s1 = 0.f, s2 = 0.f;
-        if (pv) sink_row_apply4(ri[m], n, pix, acc[m], s0, s1, s2);
+        if (pv) sink_row_apply4(ri[m], n, pix, acc[m], opnd[m], s0, s1, s2);
         if (red) {
             s0 = wave_sum(s0);
             s1 = wave_sum(s1);
@@ -1020,11 +1037,15 @@ int32_t thin_pw(const PwArgs& a, hipStream_t st) {
     b.src = a.src; b.out = a.out; b.w = a.w; b.rs = a.rs; b.cs = a.cs; b.HW = a.HW;
     b.Q = a.P / 4;
     const dim3 grid((unsigned)((b.Q + 64 * kThinWaves - 1) / (64 * kThinWaves)));
-#define ISG_THIN_PW(KK, MM)                                                          \
-    if (a.K == KK && a.M == MM) {                                                     \
-        hipLaunchKernelGGL((thin_pw_kernel<KK, MM>), grid, dim3(64 * kThinWaves), 0, st, b); \
-        const int32_t e = isg_check_launch("thin_pw_kernel");                        \
-        return e ? e : 1;                                                            \
+    bool pre = false;
+    for (int s = 0; s < a.out.nsink; ++s)
+        pre |= a.out.s[s].mode == ISG_SINK_ACTBWD || a.out.s[s].mode == ISG_SINK_ACCUM;
+#define ISG_THIN_PW(KK, MM)                                                                      \
+    if (a.K == KK && a.M == MM) {                                                                 \
+        if (pre) hipLaunchKernelGGL((thin_pw_kernel<KK, MM, true>), grid, dim3(64 * kThinWaves), 0, st, b); \
+        else hipLaunchKernelGGL((thin_pw_kernel<KK, MM, false>), grid, dim3(64 * kThinWaves), 0, st, b); \
+        const int32_t e = isg_check_launch("thin_pw_kernel");                                    \
+        return e ? e : 1;                                                                        \
     }
     ISG_THIN_PW(4, 16)
     ISG_THIN_PW(16, 4)
