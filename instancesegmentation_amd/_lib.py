@@ -20,7 +20,7 @@ SINK_STORE, SINK_ACCUM, SINK_ACTBWD, SINK_NONE = 0, 1, 2, 3
 MAX_SEGS = 3
 LIST_CHUNK = 32
 STAT_REP = int(os.environ.get("ISG_STAT_REP", "4"))  # accumulator replicas (isg.h ISG_STAT_REP)
-ABI_VERSION = 10
+ABI_VERSION = 11
 WREP = int(os.environ.get("ISG_WREP", "16"))  # weight-gradient replicas (isg.h ISG_WREP)
 
 

@@ -107,7 +107,7 @@ static isg_vtensor resolve_y(const isg_vtensor* v) { return isg_resolve_y(v); } 
 extern "C" {
 
 const char* isg_last_error(void) { return g_last_error.c_str(); }
-int32_t isg_abi_version(void) { return 10; }
+int32_t isg_abi_version(void) { return 11; }
 int32_t isg_stat_replicas(void) { return ISG_STAT_REP; }
 
 int32_t isg_conv_fwd(const isg_conv_geom* g, const isg_vtensor* x_, const float* w,
