@@ -216,8 +216,7 @@ struct SinkRow {
     SinkCoef f;
 };
 
-// one sink's row record; `k` must be a kernel-argument sink at a constant index (its fields
-// are then scalar loads — see sink_row)
+// one sink's row record
 ISG_DEV SinkRow sink_row1(const isg_sink& k, int m, int64_t hw) {
     SinkRow q = {};
     const int cl = m - k.c0;
@@ -238,17 +237,13 @@ ISG_DEV SinkRow sink_row1(const isg_sink& k, int m, int64_t hw) {
     }
     return q;
 }
-// Row m's record: the lane's sink chosen first, then each branch reads ITS sink at a
-// constant index (a per-lane selected struct made hipcc load every field per lane from
-// kernel-argument memory, each load waited for before the next).
+// Row m's record. (Round 6, measured: choosing the sink first and reading it at a constant
+// index in per-sink branches made the stem's layer-2 forward 37.6 -> 64.1 us — the branches
+// around loads in the prologue drained every load in flight; the per-lane struct select
+// below keeps the prologue one round trip.)
 ISG_DEV SinkRow sink_row(const isg_sinks& sk, int m, int64_t hw) {
-    const int ns = __builtin_amdgcn_readfirstlane(sk.nsink);
-    int s = 0;  // sink_of's rule
-    if (ns > 1 && m >= __builtin_amdgcn_readfirstlane(sk.s[1].c0)) s = 1;
-    if (ns > 2 && m >= __builtin_amdgcn_readfirstlane(sk.s[2].c0)) s = 2;
-    if (s == 0) return sink_row1(sk.s[0], m, hw);
-    if (s == 1) return sink_row1(sk.s[1], m, hw);
-    return sink_row1(sk.s[2], m, hw);
+    const int s = sink_of(sk, m);
+    return sink_row1(s == 2 ? sk.s[2] : (s == 1 ? sk.s[1] : sk.s[0]), m, hw);
 }
 
 // Apply row q's sink to value v at flat offset (n, pix); returns the values to reduce
