@@ -486,7 +486,7 @@ def main():
                    "image_size": args.size, "parallelism": f"dp{world}",
                    "input": "keypoints" if kp else ("heatmaps" if args.cin == 20 else "image"),
                    "execution": "hip-graph" if args.graph else
-                                "eager C++ executor (isg_exec_ms2), two side streams"},
+                                "eager C++ executor (isg_exec_ms2), one side stream"},
         "roofline": main_leg["roofline"], "loss": round(main_leg["loss"], 6),
     }
     if main_leg.get("roofline_backbone"):
