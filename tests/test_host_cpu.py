@@ -215,6 +215,23 @@ def test_keypoint_stem_plan_and_synthetic_keypoints():
         assert np.array_equal(keypoint_heatmaps(pts, 96, 64), hm[b])
 
 
+def _joined_before(recs, k):
+    """The side-stream records (list indices) the main stream has waited for by the time
+    record k runs, by the executor's rule (api.cpp isg_exec_ms2): a join with exclusion
+    count e (header flags >> Record.EXCL_SHIFT, 0 < e <= side records so far) waits for all
+    but the e most recent side records; any other join waits for every one."""
+    from instancesegmentation_amd.engine import Record
+    side, done = [], set()
+    for j in range(k + 1):
+        r = recs[j]
+        if r.flags & Record.OPF_JOIN:
+            e = r.flags >> Record.EXCL_SHIFT
+            done |= set(side[:len(side) - e] if 0 < e <= len(side) else side)
+        if r.flags & Record.OPF_SIDE:
+            side.append(j)
+    return done
+
+
 def test_forward_side_branches_fork_and_join():
     """engine._fork_branches: the residual branches of BottleneckDown2 / BottleneckDim_Res /
     BottleneckUp_Res run on the side stream in the forward pass, and the first main-stream
@@ -238,9 +255,11 @@ def test_forward_side_branches_fork_and_join():
         assert recs[i].flags & Record.OPF_SIDE
         readers = [j for j, r in enumerate(recs[i + 1:], i + 1) if not r.flags & Record.OPF_SIDE
                    and any(fs == o.slot and o.off <= off < hi for _, fs, off in r.fix)]
-        if readers:  # a join between the fork and the first main-stream reader
-            assert any(recs[j].flags & Record.OPF_JOIN for j in range(i + 1, readers[0] + 1)), \
-                op.out.name
+        if readers:  # a join between the fork and the first main-stream reader, and one
+            # that covers this record (a partial join excludes the side records after the
+            # ones it reads)
+            assert i in _joined_before(recs, readers[0]), op.out.name
+    assert any(r.flags >> Record.EXCL_SHIFT for r in recs)  # partial joins are in use
     # backward: no branch work on the side stream (shared dx sinks); only bucket 1's
     # replica fold and gradient finalisation fork there (after every statistic is done),
     # and weight gradients (engine._fork_late_wgrads: the batch pending when the stem's
@@ -250,6 +269,45 @@ def test_forward_side_branches_fork_and_join():
                                      L.OP_KP_STEM_WGRAD))
     assert all(r.flags & Record.OPF_SIDE for r in p.bwd.recs if r.flags & Record.OPF_FORK_NOW
                and r.kind in (L.OP_CONV_WGRAD, L.OP_KP_STEM_WGRAD))
+
+
+def test_stamped_side_record_keeps_partial_joins_covering():
+    """OpList.stamped(idx) on a forked forward record (bench.py times a side-stream op on
+    the main stream): one side record fewer, so every partial join is recounted; every
+    forked pool / branch output must still be joined before its first main-stream reader,
+    by the executor's rule (_joined_before)."""
+    from instancesegmentation_amd.engine import Record
+    m = Segment(20)
+    p = Plan(m, [(2, 3, 128, 128), (2, 17, 3)], True, True, (False, False))
+    recs = p.fwd.recs
+    outs = {op.out.name: op.out for op in p.graph.ops if getattr(op, "side", False)}
+
+    def ranges(rs):
+        for i, r in enumerate(rs):
+            if not r.flags & Record.OPF_SIDE:
+                continue
+            if getattr(r, "out_range", None) is not None:
+                yield i, r.out_range
+            elif r.label in outs:
+                o = outs[r.label].ptr()
+                yield i, (o.slot, o.off, o.off + outs[r.label].numel * 4)
+
+    side_idx = [i for i, r in enumerate(recs) if r.flags & Record.OPF_SIDE]
+    assert len(side_idx) >= 6
+    for idx in side_idx[:3] + side_idx[-3:]:
+        st = p.fwd.stamped(idx).recs
+        assert sum(1 for r in st if r.flags & Record.OPF_SIDE) == len(side_idx) - 1
+        n = 0
+        for i, (slot, lo, hi) in ranges(st):
+            # (the moved record itself is no reader: the stem's two pools write disjoint
+            # channel slices of init_down, the reason _fork_pools forks them together)
+            readers = [j for j in range(i + 1, len(st)) if not st[j].flags & Record.OPF_SIDE
+                       and st[j].label != recs[idx].label
+                       and any(fs == slot and lo <= off < hi for _, fs, off in st[j].fix)]
+            if readers:
+                n += 1
+                assert i in _joined_before(st, readers[0]), (recs[idx].label, st[i].label)
+        assert n >= 4
 
 
 def test_residual_tails_fold_into_the_next_1x1(monkeypatch):
@@ -449,8 +507,7 @@ def test_forked_pools_join_before_any_reader_of_their_buffer(n):
         if recs[i].kind == L.OP_KP_POOL:
             assert readers
         if readers:  # (bottle1_1.pool is read by side-stream branches only)
-            assert any(recs[j].flags & Record.OPF_JOIN for j in range(i + 1, readers[0] + 1)), \
-                (n, recs[i].label, recs[readers[0]].label)
+            assert i in _joined_before(recs, readers[0]), (n, recs[i].label, recs[readers[0]].label)
 
 
 def test_library_has_no_undefined_isg_symbols():
