@@ -512,8 +512,8 @@ def main():
         out["dp_plan_at_world1"] = {
             "value": round(dp_leg["value"], 3), "ms_per_step": round(dp_leg["ms_per_step"], 3),
             "what": "the step as it runs at world > 1 (two backward parts, two gradient buckets, "
-                    "three HIP graphs with the RCCL exchange points between them), at world 1 "
-                    "where the exchanges are no-ops: the per-GPU ceiling of weak scaling"}
+                    "the RCCL exchange points between the executor calls, no fused tail), at "
+                    "world 1 where the exchanges are no-ops: the per-GPU ceiling of weak scaling"}
     if dp_nccl_leg is not None:
         out["dp_plan_at_world1_nccl"] = {
             "value": round(dp_nccl_leg["value"], 3),
