@@ -528,7 +528,11 @@ int32_t isg_exec(const void* ops, int32_t nops, void* const* table, isg_stream_t
  * op issued before them on `stream`; ops flagged "join" (and the end of the list) wait
  * for all forked work. side == NULL runs everything on `stream`. Under HIP-graph
  * capture the fork/join become graph edges, so the weight gradients overlap the
- * input-gradient chain. */
+ * input-gradient chain. Header flags (api.cpp OpHdr.flags): bit 0 side, bit 1 join,
+ * bit 2 fork-now (the side op depends on everything issued on `stream` so far; consecutive
+ * fork-now ops share one fork), bits 8+ of a join: how many of the most recent side ops it
+ * does NOT wait for (0: all). Side ops are otherwise issued in batches of 16 behind one
+ * fork each. */
 int32_t isg_exec_ms(const void* ops, int32_t nops, void* const* table, isg_stream_t stream,
                     isg_stream_t side);
 

@@ -286,7 +286,7 @@ struct StampRec {  // OP_STAMP: isg_stamp(buf, slot, sign)
 struct OpHdr {
     int32_t kind, desc_bytes, nfix, flags;  // flags: ISG_OPF_SIDE | ISG_OPF_JOIN
 };
-enum { ISG_OPF_SIDE = 1, ISG_OPF_JOIN = 2, ISG_OPF_FORK_NOW = 4 };  // FORK_NOW: no batching
+enum { ISG_OPF_SIDE = 1, ISG_OPF_JOIN = 2, ISG_OPF_FORK_NOW = 4 };  // FORK_NOW: forked at the next main-stream op
 // flags >> 8 of a JOIN: how many of the most recent side records (in list order) the op does
 // NOT depend on — it waits only for the side work up to the one before them (engine.py
 // _join_exclusions); 0 = wait for all side work
