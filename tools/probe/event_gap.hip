@@ -30,11 +30,16 @@ int main(int argc, char** argv) {
     hipStream_t m, s;
     CK(hipStreamCreateWithFlags(&m, hipStreamNonBlocking));
     CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-    hipEvent_t ev[chain], t0, t1;
-    for (int i = 0; i < chain; ++i) CK(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
+    hipEvent_t ev0[chain], ev4[chain], ev5[chain], t0, t1;
+    for (int i = 0; i < chain; ++i) {
+        CK(hipEventCreateWithFlags(&ev0[i], hipEventDisableTiming));
+        CK(hipEventCreateWithFlags(&ev4[i], hipEventDisableTiming | hipEventDisableSystemFence));
+        CK(hipEventCreateWithFlags(&ev5[i], hipEventDisableTiming | hipEventReleaseToDevice));
+    }
     CK(hipEventCreate(&t0));
     CK(hipEventCreate(&t1));
-    for (int mode = 0; mode < 4; ++mode) {
+    for (int mode = 0; mode < 9; ++mode) {
+        hipEvent_t* ev = mode == 4 ? ev4 : (mode == 5 ? ev5 : ev0);
         for (int rep = 0; rep < 3; ++rep) {
             CK(hipEventRecord(t0, m));
             for (int i = 0; i < chain; ++i) {
@@ -43,8 +48,10 @@ int main(int argc, char** argv) {
                 } else {
                     hipLaunchKernelGGL(busy, dim3(n / 256), dim3(256), 0, m, a, n, 200);
                 }
-                if (mode == 1) CK(hipEventRecord(ev[i], m));
-                if (mode == 1 || mode == 2) {
+                if (mode == 1 || mode >= 4) CK(hipEventRecord(ev[i], m));
+                if (mode == 7 || mode == 8) CK(hipStreamWaitEvent(s, ev[i], 0));
+                if (mode == 8 && i % 8 == 7) hipLaunchKernelGGL(busy, dim3(1), dim3(64), 0, s, b, 64, 10);
+                if (mode == 1 || mode == 2 || mode == 4 || mode == 5) {
                     CK(hipStreamWaitEvent(s, ev[i], 0));
                     hipLaunchKernelGGL(busy, dim3(1), dim3(64), 0, s, b, 64, 10);
                 }
